@@ -1,0 +1,198 @@
+#!/usr/bin/env python3
+"""Benchmark: frames/s of forward-backward + Viterbi (BASELINE.json metric).
+
+Workload (BASELINE configs[1] / the north-star shape): HMMPyTorch with a 128-state
+left-to-right (0.7) transition matrix, B=32 sequences of T=2000 frames per GPU, emissions
+softmax(randn(B,T,N)) (examples/benchmark.py:160-162), synthetic, resident in HBM.
+One step = HMMPyTorch.forward_backward (posterior, forward, backward) + viterbi_decode
+(states, trellis) over the batch; the two run on two HIP streams of the same GPU.
+N GPUs = one process per GPU (torchrun), B=32 per rank (weak scaling; BASELINE config 4
+is B=256 over 8 GPUs), no collective in the data path; with --gather the posteriors and
+states are gathered to rank 0 over RCCL after every step (config 4's gather).
+
+Prints ONE JSON line on rank 0.  Besides the contract fields it carries
+  roofline     for the dominant kernel (HIP events on its stream, over the timed steps)
+  cpu_baseline the oracle (torch-CPU restatement, bit-identical to the reference) timed on
+               the host cores on a bounded sample (rank 0, N=1 only)
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+import torch.distributed as dist
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, HERE)
+
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=20)
+    p.add_argument("--warmup", type=int, default=3)
+    p.add_argument("--batch", type=int, default=32, help="sequences per GPU")
+    p.add_argument("--T", type=int, default=2000)
+    p.add_argument("--N", type=int, default=128)
+    p.add_argument("--gather", action="store_true", help="RCCL gather of posteriors+states to rank 0 each step")
+    p.add_argument("--serial", action="store_true", help="run FB and Viterbi on one stream")
+    p.add_argument("--cpu-seconds", type=float, default=12.0, help="bounded CPU-baseline budget (0 = skip)")
+    return p.parse_args()
+
+
+def setup_dist(args):
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    else:
+        torch.cuda.set_device(0)
+    return rank, world, local
+
+
+def cpu_baseline(B, T, N, budget):
+    """Time the oracle (reference op sequence on torch-CPU) on the NS workload, repeated
+    until `budget` seconds of CPU work are spent (at least one FB+Viterbi pair)."""
+    from oracle import hmm_oracle as O
+    threads = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
+    threads = max(1, min(threads, os.cpu_count() or 1))
+    torch.set_num_threads(threads)
+    g = torch.Generator().manual_seed(1234)
+    obs = torch.softmax(torch.randn(B, T, N, generator=g), dim=-1)
+    lP, lp0 = O.hmm_params(O.left_to_right_matrix(N, 0.7))
+    frames, elapsed, reps = 0, 0.0, 0
+    with torch.no_grad():
+        while reps == 0 or (elapsed < budget and reps < 8):
+            t0 = time.perf_counter()
+            O.forward_backward(obs, lP, lp0)
+            O.viterbi_decode(obs, lP, lp0)
+            elapsed += time.perf_counter() - t0
+            frames += B * T
+            reps += 1
+    return {"value": frames / elapsed, "unit": "frames/s", "cores": threads, "kind": "port",
+            "sample": f"{reps} x (forward_backward + viterbi_decode) at B={B} T={T} N={N} "
+                      f"(oracle/hmm_oracle.py, the reference op sequence on torch-CPU, "
+                      f"{threads} threads, {elapsed:.1f}s)"}
+
+
+def main():
+    args = parse()
+    rank, world, local = setup_dist(args)
+    dev = torch.device("cuda", local)
+    import pytorch_hmm_amd as ph
+    from pytorch_hmm_amd import ops
+
+    B, T, N = args.batch, args.T, args.N
+    hmm = ph.HMMPyTorch(ph.create_left_to_right_matrix(N, 0.7))
+    g = torch.Generator(device=dev).manual_seed(1234 + rank)
+    obs = torch.softmax(torch.randn(B, T, N, device=dev, generator=g), dim=-1)
+    hmm._params_for(obs)
+    lP, lp0 = hmm.log_P.to(dev), hmm.log_p0.to(dev)
+
+    s_fb = torch.cuda.Stream(dev)
+    s_vit = s_fb if args.serial else torch.cuda.Stream(dev)
+    main_s = torch.cuda.current_stream(dev)
+    ev = {k: [] for k in ("fb", "vit")}
+
+    gather_bufs = None
+    if args.gather and world > 1 and rank == 0:
+        gather_bufs = ([torch.empty(B, T, N, device=dev) for _ in range(world)],
+                       [torch.empty(B, T, dtype=torch.int64, device=dev) for _ in range(world)])
+
+    def step(record):
+        s_fb.wait_stream(main_s)
+        s_vit.wait_stream(main_s)
+        with torch.cuda.stream(s_fb):
+            e0 = torch.cuda.Event(enable_timing=True) if record else None
+            if record:
+                e0.record(s_fb)
+            post, fwd, bwd, _, _ = ops.forward_backward(obs, lP, lp0, ops.OBS_PROB, 7)
+            if record:
+                e1 = torch.cuda.Event(enable_timing=True)
+                e1.record(s_fb)
+                ev["fb"].append((e0, e1))
+        with torch.cuda.stream(s_vit):
+            if record:
+                v0 = torch.cuda.Event(enable_timing=True)
+                v0.record(s_vit)
+            states, delta, _ = ops.viterbi(obs, lP, lp0, ops.OBS_PROB)
+            if record:
+                v1 = torch.cuda.Event(enable_timing=True)
+                v1.record(s_vit)
+                ev["vit"].append((v0, v1))
+        main_s.wait_stream(s_fb)
+        main_s.wait_stream(s_vit)
+        if args.gather and world > 1:
+            if rank == 0:
+                dist.gather(post, gather_bufs[0], dst=0)
+                dist.gather(states, gather_bufs[1], dst=0)
+            else:
+                dist.gather(post, None, dst=0)
+                dist.gather(states, None, dst=0)
+        return post, states
+
+    for _ in range(args.warmup):
+        step(False)
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step(True)
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        tt = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        elapsed = float(tt.item())
+
+    fb_ms = sum(a.elapsed_time(b) for a, b in ev["fb"]) / len(ev["fb"])
+    vit_ms = sum(a.elapsed_time(b) for a, b in ev["vit"]) / len(ev["vit"])
+    frames_total = B * T * world * args.steps
+    value = frames_total / elapsed
+    ms_per_step = elapsed / args.steps * 1e3
+
+    # roofline of the dominant op, algorithmic bytes per SURVEY.md §8(d)
+    if fb_ms >= vit_ms:
+        dom, dur_ms, bytes_per_launch = "forward_backward", fb_ms, 16 * N * B * T
+        kernels = "fb_recur_kernel + fb_posterior_kernel"
+    else:
+        dom, dur_ms, bytes_per_launch = "viterbi", vit_ms, (8 * N + 8) * B * T
+        kernels = "vit_fwd_kernel + vit_psi_kernel + vit_backtrace_kernel"
+    achieved = bytes_per_launch / (dur_ms * 1e-3) / 1e9
+    out = {
+        "metric": "frames/sec forward-backward+Viterbi, B=32 T=2000 N=128, 1/2/4/8 GPU",
+        "value": value, "unit": "frames/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": ms_per_step, "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+        "dtype": "f32", "data": "synthetic: softmax(randn(B,T,N)) emissions, left-to-right(0.7) transitions",
+        "config": {"workload": "HMMPyTorch forward_backward + viterbi_decode", "batch_per_gpu": B,
+                   "global_batch": B * world, "seq_len": T, "num_states": N,
+                   "transition": "left_to_right(0.7)", "parallelism": f"batch-sharded x{world}",
+                   "streams": 1 if args.serial else 2, "gather": bool(args.gather and world > 1)},
+        "op_ms": {"forward_backward": fb_ms, "viterbi": vit_ms},
+        "roofline": {"bound": "hbm", "kernel": dom, "kernels": kernels, "achieved": achieved,
+                     "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
+                     "traffic": None, "bytes_per_launch": bytes_per_launch, "avg_launch_ms": dur_ms},
+    }
+    if rank == 0 and world == 1 and args.cpu_seconds > 0:
+        out["cpu_baseline"] = cpu_baseline(B, T, N, args.cpu_seconds)
+        out["cpu_baseline"]["speedup_gpu_over_cpu"] = value / out["cpu_baseline"]["value"]
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,126 @@
+/*
+ * hmm355 — MI355X (gfx950) HMM inference core: the C ABI.
+ *
+ * This is the drop-in boundary for the hot path of crlotwhite/pytorch_hmm.  The reference
+ * is pure Python over ATen (no FFI of its own); each entry point below replaces the
+ * per-time-step Python loop of one reference routine (file:line into
+ * /root/reference/pytorch_hmm) and is what a binding (ctypes, pybind11, or the
+ * torch.library custom ops in pytorch_hmm_amd/ops.py) calls.
+ *
+ * Conventions (all entry points)
+ *   - Plain device pointers and sizes; no framework types.  Every buffer is caller-owned
+ *     device memory (hipMalloc / torch allocator); the library allocates nothing.
+ *   - Dense row-major fp32, (B, T, N) = batch, time, states; states int64 (B, T).
+ *   - `stream` is a hipStream_t (NULL = legacy default stream).  Launches are
+ *     stream-ordered and asynchronous; there is no host synchronisation and no global
+ *     mutable state, so calls are re-entrant and may run concurrently on different streams
+ *     (and may be captured into a hipGraph).
+ *   - Return 0 on success, a negative HMM355_E* code on a rejected argument (nothing is
+ *     launched), or a positive hipError_t if a launch failed.  hmm355_strerror() names it.
+ *   - Supported sizes: 1 <= N <= 256 states (padded internally to 64/128/256),
+ *     T >= 1, B >= 0 (B == 0 is a no-op).
+ */
+#ifndef HMM355_H
+#define HMM355_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define HMM355_OK 0
+#define HMM355_E_ARG (-1)       /* null pointer or negative size                      */
+#define HMM355_E_STATES (-2)    /* N outside [1, 256]                                  */
+#define HMM355_E_SHAPE (-3)     /* T < 1, or a size product overflows                  */
+#define HMM355_E_WORKSPACE (-4) /* workspace smaller than *_workspace_bytes() reports   */
+#define HMM355_E_DURATION (-5)  /* HSMM max_duration outside [1, 255]                  */
+
+/* Emission encodings accepted by the recursions. */
+#define HMM355_OBS_PROB 0   /* x is a probability: the kernel uses log(x + 1e-8) / x + 1e-8 (hmm.py:86,152) */
+#define HMM355_OBS_LOG 1    /* x is already a log-emission (mixture_gaussian.py:354, hsmm.py:225)           */
+
+/* forward_backward output mask bits */
+#define HMM355_FB_POSTERIOR 1u   /* posterior (B,T,N)              hmm.py:120-126 */
+#define HMM355_FB_FORWARD 2u     /* forward = exp(log alpha)        hmm.py:127     */
+#define HMM355_FB_BACKWARD 4u    /* backward = exp(log beta)        hmm.py:128     */
+
+const char* hmm355_strerror(int code);
+int hmm355_version(void);
+
+/* ---------------------------------------------------------------------------------
+ * Forward-backward.  Replaces HMMPyTorch.forward_backward (hmm.py:66-130) and the
+ * likelihood of HMMPyTorch.compute_likelihood (hmm.py:186-211).
+ *   obs        (B,T,N) emissions, encoding `obs_mode`
+ *   log_P      (N,N) log transition matrix, exactly as the reference holds it
+ *              (log(P/rowsum + 1e-8), hmm.py:39-42, or hmm_layer.py:84)
+ *   log_p0     (N) log initial distribution (hmm.py:55 / hmm_layer.py:86)
+ *   posterior, forward, backward  (B,T,N) outputs, written iff the mask bit is set
+ *   loglik     (B) or NULL: log sum_j alpha_{T-1}[j] (the well-defined sequence
+ *              log-likelihood the reference's exp() underflow hides)
+ *   lik_ref    (B) or NULL: the reference's compute_likelihood value
+ *              logsumexp_j(log(exp(log alpha_{T-1}[j]) + 1e-8))  (hmm.py:206)
+ *   workspace  >= hmm355_fb_workspace_bytes(B,T,N) bytes of device memory
+ * ------------------------------------------------------------------------------ */
+size_t hmm355_fb_workspace_bytes(int B, int T, int N);
+int hmm355_forward_backward_f32(const float* obs, int obs_mode, const float* log_P,
+                                const float* log_p0, int B, int T, int N, unsigned out_mask,
+                                float* posterior, float* forward, float* backward,
+                                float* loglik, float* lik_ref, void* workspace,
+                                size_t workspace_bytes, void* stream);
+
+/* ---------------------------------------------------------------------------------
+ * Viterbi.  Replaces HMMPyTorch.viterbi_decode (hmm.py:132-184) and
+ * MixtureGaussianHMMLayer._viterbi_decode (mixture_gaussian.py:290-338).
+ *   init       (N) additive t=0 vector: log_p0 (hmm.py:159), or -log(S) per state
+ *              (mixture_gaussian.py:312; lp + (-c) == lp - c exactly in fp32)
+ *   states     (B,T) int64: backtraced path, first index on ties (hmm.py:167,174)
+ *   log_delta  (B,T,N) fp32: the trellis the reference returns as `scores`
+ *   final_score (B) or NULL: max_j delta_{T-1}[j] (mixture_gaussian.py:327)
+ *   workspace  >= hmm355_viterbi_workspace_bytes(B,T,N) bytes
+ * Given identical fp32 log-emissions and log_P the result is bit-identical to the
+ * reference's (every delta is one fp32 add of an exact max).
+ * ------------------------------------------------------------------------------ */
+size_t hmm355_viterbi_workspace_bytes(int B, int T, int N);
+int hmm355_viterbi_f32(const float* obs, int obs_mode, const float* log_P, const float* init,
+                       int B, int T, int N, int64_t* states, float* log_delta,
+                       float* final_score, void* workspace, size_t workspace_bytes,
+                       void* stream);
+
+/* ---------------------------------------------------------------------------------
+ * Diagonal-covariance Gaussian-mixture emission scorer.  Replaces
+ * MixtureGaussianHMMLayer.get_observation_log_probs for covariance_type='diag'
+ * (mixture_gaussian.py:157-214, LSE of :141-155) and, with C == 1 and log_w == 0,
+ * GaussianHMMLayer._compute_gaussian_log_probs 'diag'/'full' (hmm_layer.py:300-321) and
+ * HSMMLayer.get_observation_log_probs (hsmm.py:181-206).
+ *   x (B,T,D); means, log_vars (S,C,D); log_w (S,C) = log(clamp(softmax(w),1e-8));
+ *   out (B,T,S) = LSE_c[ -0.5*(sum_d (x-mu)^2/exp(lv) + sum_d lv + D*log(2pi)) + log_w ].
+ * `mix_lse` selects the reference's mixture LSE (clamped sum, :141-155); with C == 1 pass 0
+ * to get the plain component log-density.  Supported: 1 <= D <= 128, 1 <= C <= 256,
+ * 1 <= S*C <= 65536.  workspace >= hmm355_gmm_workspace_bytes(D,S,C) (per-component
+ * precomputed scales; written by the call).
+ * ------------------------------------------------------------------------------ */
+size_t hmm355_gmm_workspace_bytes(int D, int S, int C);
+int hmm355_gmm_diag_logprob_f32(const float* x, const float* means, const float* log_vars,
+                                const float* log_w, int B, int T, int D, int S, int C,
+                                int mix_lse, float* out, void* workspace,
+                                size_t workspace_bytes, void* stream);
+
+/* ---------------------------------------------------------------------------------
+ * HSMM segment Viterbi.  Replaces HSMMLayer.viterbi_decode_hsmm / _viterbi_decode_single
+ * (hsmm.py:208-354), reproducing its candidate order (s' outer, d' inner, strict >), its
+ * fp32 addition order ((prev + logT) + obs_sum) + dur and torch-CPU's summation order for
+ * obs_sum, so paths are bit-identical given identical fp32 inputs.
+ *   lp (B,T,S) obs log-probs; dur_lp (S,Dmax) = log(p_dur + 1e-8); log_T (S,S)
+ *   states (B,T) int64; scores (B) fp32
+ * ------------------------------------------------------------------------------ */
+size_t hmm355_hsmm_workspace_bytes(int B, int T, int S, int Dmax);
+int hmm355_hsmm_viterbi_f32(const float* lp, const float* dur_lp, const float* log_T, int B,
+                            int T, int S, int Dmax, int64_t* states, float* scores,
+                            void* workspace, size_t workspace_bytes, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* HMM355_H */

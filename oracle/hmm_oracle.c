@@ -1,0 +1,300 @@
+/*
+ * TEST INFRASTRUCTURE ONLY — plain-C parity oracle for the HMM hot path.
+ * Never linked into the product (pytorch_hmm_amd); loaded by tests/ and bench.py's
+ * cpu_baseline leg through ctypes (oracle/lib/liboracle.so, built by oracle/Makefile).
+ *
+ * Restates, from the reference's published behaviour (crlotwhite/pytorch_hmm):
+ *   viterbi_f32         hmm.py:154-184 and mixture_gaussian.py:306-338 — max-plus recursion,
+ *                       first-index argmax on ties (torch.max / torch.argmax semantics).
+ *                       Bit-exact given identical fp32 log-emissions: every delta is one
+ *                       fp32 add of an exact max, independent of reduction order.
+ *   fb_f64              hmm.py:89-130 in float64 (tolerance reference, not bit-exact).
+ *   gmm_diag_f64        mixture_gaussian.py:157-214 in float64 (tolerance reference).
+ *   hsmm_viterbi_literal hsmm.py:245-354, the literal 5-deep loop, incl. torch's CPU order
+ *                       for sum(obs_log_probs[t:t+d, s]) (strided slice: 4 accumulators over
+ *                       whole groups of 4, tail folded into acc0, then ((a0+a1)+a2)+a3 —
+ *                       measured 31200/31200 matches against torch 2.10 CPU).
+ *   hsmm_viterbi_fast   the same recursion reorganised (max over d' hoisted out of the
+ *                       candidate loop, exact tie re-resolution per d) — bit-identical to
+ *                       the literal form; cross-checked in tests/test_oracle.py.
+ */
+#include <math.h>
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+
+/* ---------------------------------------------------------------- Viterbi (exact) */
+void viterbi_f32(const float* log_obs, const float* log_P, const float* init, int B, int T,
+                 int N, int64_t* states, float* delta, uint8_t* psi_opt) {
+    uint8_t* psi = psi_opt ? psi_opt : (uint8_t*)malloc((size_t)T * N);
+    for (int b = 0; b < B; ++b) {
+        const float* lo = log_obs + (size_t)b * T * N;
+        float* dl = delta + (size_t)b * T * N;
+        uint8_t* ps = psi_opt ? psi + (size_t)b * T * N : psi;
+        for (int j = 0; j < N; ++j) { dl[j] = init[j] + lo[j]; ps[j] = 0; }
+        for (int t = 1; t < T; ++t) {
+            const float* dp = dl + (size_t)(t - 1) * N;
+            for (int j = 0; j < N; ++j) {
+                float best = dp[0] + log_P[j];
+                int bi = 0;
+                for (int i = 1; i < N; ++i) {
+                    float s = dp[i] + log_P[(size_t)i * N + j];
+                    if (s > best) { best = s; bi = i; }
+                }
+                dl[(size_t)t * N + j] = best + lo[(size_t)t * N + j];
+                ps[(size_t)t * N + j] = (uint8_t)bi;   /* N <= 256 */
+            }
+        }
+        const float* dlast = dl + (size_t)(T - 1) * N;
+        int s = 0;
+        for (int j = 1; j < N; ++j) if (dlast[j] > dlast[s]) s = j;
+        int64_t* st = states + (size_t)b * T;
+        st[T - 1] = s;
+        for (int t = T - 2; t >= 0; --t) { s = ps[(size_t)(t + 1) * N + s]; st[t] = s; }
+    }
+    if (!psi_opt) free(psi);
+}
+
+/* ------------------------------------------------------- forward-backward (float64) */
+static double lse(const double* v, int n) {
+    double m = -INFINITY;
+    for (int i = 0; i < n; ++i) if (v[i] > m) m = v[i];
+    if (!isfinite(m)) return m;
+    double s = 0.0;
+    for (int i = 0; i < n; ++i) s += exp(v[i] - m);
+    return m + log(s);
+}
+
+/* log_alpha/log_beta/posterior are (B,T,N) float64; loglik (B) = LSE(alpha_{T-1}). */
+void fb_f64(const float* log_obs, const float* log_P, const float* log_p0, int B, int T, int N,
+            double* log_alpha, double* log_beta, double* posterior, double* loglik) {
+    double* tmp = (double*)malloc(sizeof(double) * N);
+    for (int b = 0; b < B; ++b) {
+        const float* lo = log_obs + (size_t)b * T * N;
+        double* la = log_alpha + (size_t)b * T * N;
+        double* lb = log_beta + (size_t)b * T * N;
+        for (int j = 0; j < N; ++j) la[j] = (double)log_p0[j] + lo[j];
+        for (int t = 1; t < T; ++t)
+            for (int j = 0; j < N; ++j) {
+                for (int i = 0; i < N; ++i) tmp[i] = la[(size_t)(t - 1) * N + i] + log_P[(size_t)i * N + j];
+                la[(size_t)t * N + j] = lse(tmp, N) + lo[(size_t)t * N + j];
+            }
+        for (int j = 0; j < N; ++j) lb[(size_t)(T - 1) * N + j] = 0.0;
+        for (int t = T - 2; t >= 0; --t)
+            for (int i = 0; i < N; ++i) {
+                for (int j = 0; j < N; ++j)
+                    tmp[j] = (double)log_P[(size_t)i * N + j] + lo[(size_t)(t + 1) * N + j] + lb[(size_t)(t + 1) * N + j];
+                lb[(size_t)t * N + i] = lse(tmp, N);
+            }
+        for (int t = 0; t < T; ++t) {
+            double* pr = posterior + ((size_t)b * T + t) * N;
+            for (int j = 0; j < N; ++j) tmp[j] = la[(size_t)t * N + j] + lb[(size_t)t * N + j];
+            double z = lse(tmp, N);
+            for (int j = 0; j < N; ++j) pr[j] = exp(tmp[j] - z);
+        }
+        loglik[b] = lse(la + (size_t)(T - 1) * N, N);
+    }
+    free(tmp);
+}
+
+/* ------------------------------------------------ diagonal GMM emission (float64) */
+void gmm_diag_f64(const float* x, const float* means, const float* log_vars, const float* log_w,
+                  int B, int T, int D, int S, int C, double* out) {
+    const double l2pi = log(2.0 * M_PI);
+    double* comp = (double*)malloc(sizeof(double) * C);
+    for (size_t f = 0; f < (size_t)B * T; ++f) {
+        const float* xf = x + f * D;
+        for (int s = 0; s < S; ++s) {
+            for (int c = 0; c < C; ++c) {
+                const float* mu = means + ((size_t)s * C + c) * D;
+                const float* lv = log_vars + ((size_t)s * C + c) * D;
+                double q = 0.0, slv = 0.0;
+                for (int d = 0; d < D; ++d) {
+                    double df = (double)xf[d] - mu[d];
+                    q += df * df / exp((double)lv[d]);
+                    slv += lv[d];
+                }
+                comp[c] = -0.5 * (q + slv + D * l2pi) + log_w[(size_t)s * C + c];
+            }
+            double m = -INFINITY;
+            for (int c = 0; c < C; ++c) if (comp[c] > m) m = comp[c];
+            if (isinf(m)) m = 0.0;
+            double sum = 0.0;
+            for (int c = 0; c < C; ++c) sum += exp(comp[c] - m);
+            if (sum < 1e-8) sum = 1e-8;
+            out[f * S + s] = log(sum) + m;
+        }
+    }
+    free(comp);
+}
+
+/* ----------------------------------------------------------------- HSMM (exact) */
+/* torch 2.10 CPU order for torch.sum over a strided 1-D slice of length d. */
+static float tsum(const float* lp, int S, int t0, int d, int s) {
+    float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
+    int m = d & ~3, i = 0;
+    for (; i < m; i += 4) {
+        a0 += lp[(size_t)(t0 + i) * S + s];
+        a1 += lp[(size_t)(t0 + i + 1) * S + s];
+        a2 += lp[(size_t)(t0 + i + 2) * S + s];
+        a3 += lp[(size_t)(t0 + i + 3) * S + s];
+    }
+    for (; i < d; ++i) a0 += lp[(size_t)(t0 + i) * S + s];
+    float r = 0.f + a0;
+    r = r + a1;
+    r = r + a2;
+    r = r + a3;
+    return r;
+}
+
+static void hsmm_backtrack(int T, int S, int Dm, const int16_t* psi_s, const int16_t* psi_d,
+                           int fs, int fd, int64_t* states) {
+    int t = T - 1, cs = fs, cd = fd;
+    while (t >= 0) {
+        int start = t - cd + 1;
+        if (start < 0) start = 0;
+        for (int u = start; u <= t; ++u) states[u] = cs;
+        if (start > 0) {
+            int di = ((cd - 1) % Dm + Dm) % Dm;            /* python negative index wrap */
+            size_t k = ((size_t)t * S + cs) * Dm + di;
+            int ns = psi_s[k], nd = psi_d[k];
+            t = start - 1; cs = ns; cd = nd;
+        } else {
+            break;
+        }
+    }
+}
+
+/* Literal hsmm.py:245-354 for one sequence.  lp (T,S); dur (S,Dm); logT (S,S). */
+void hsmm_viterbi_literal(const float* lp, const float* dur, const float* logT, int T, int S,
+                          int Dm, int64_t* states, float* score) {
+    size_t n = (size_t)T * S * Dm;
+    float* delta = (float*)malloc(n * sizeof(float));
+    int16_t* psi_s = (int16_t*)calloc(n, sizeof(int16_t));
+    int16_t* psi_d = (int16_t*)calloc(n, sizeof(int16_t));
+    for (size_t k = 0; k < n; ++k) delta[k] = -INFINITY;
+#define DL(e, s, d) delta[((size_t)(e) * S + (s)) * Dm + (d)]
+    int dl0 = Dm < T ? Dm : T;
+    for (int s = 0; s < S; ++s)
+        for (int d = 1; d <= dl0; ++d) DL(d - 1, s, d - 1) = tsum(lp, S, 0, d, s) + dur[(size_t)s * Dm + d - 1];
+    for (int t = 1; t < T; ++t)
+        for (int s = 0; s < S; ++s) {
+            int dlim = Dm < T - t ? Dm : T - t;
+            for (int d = 1; d <= dlim; ++d) {
+                int end = t + d - 1;
+                float os = tsum(lp, S, t, d, s), du = dur[(size_t)s * Dm + d - 1];
+                float best = -INFINITY;
+                int bs = 0, bd = 1;
+                for (int ps = 0; ps < S; ++ps) {
+                    if (ps == s) continue;
+                    for (int pd = 1; pd <= Dm; ++pd) {
+                        int pst = t - 1 - pd + 1;
+                        if (pst < 0) continue;
+                        float prev = DL(t - 1, ps, pd - 1);
+                        if (prev == -INFINITY) continue;
+                        float tot = ((prev + logT[(size_t)ps * S + s]) + os) + du;
+                        if (tot > best) { best = tot; bs = ps; bd = pd; }
+                    }
+                }
+                if (best != -INFINITY) {
+                    size_t k = ((size_t)end * S + s) * Dm + d - 1;
+                    delta[k] = best; psi_s[k] = (int16_t)bs; psi_d[k] = (int16_t)bd;
+                }
+            }
+        }
+    float best = -INFINITY;
+    int fs = 0, fd = 1;
+    for (int s = 0; s < S; ++s)
+        for (int d = 1; d <= Dm; ++d) {
+            float sc = DL(T - 1, s, d - 1);
+            if (sc > best) { best = sc; fs = s; fd = d; }
+        }
+#undef DL
+    hsmm_backtrack(T, S, Dm, psi_s, psi_d, fs, fd, states);
+    *score = best;
+    free(delta); free(psi_s); free(psi_d);
+}
+
+/* Exact fast form.  M[st][s] = max_{s'!=s,d'} fl(delta[st-1][s'][d'-1] + logT[s'][s]);
+ * delta[st+d-1][s][d-1] = fl(fl(M + obs_sum(st,s,d)) + dur[s][d-1]) (st = 0: fl(obs_sum + dur)).
+ * g_d(x) = fl(fl(x + o_d) + u_d) is monotone, so the literal max over candidates equals
+ * g_d(M); the literal first-argmax is the first candidate (s' asc, d' asc) whose
+ * g_d(x) == g_d(M): the first candidate attaining M unless an EARLIER candidate rounds
+ * to the same final value, which is checked exactly (rare path). */
+void hsmm_viterbi_fast(const float* lp, const float* dur, const float* logT, int T, int S,
+                       int Dm, int64_t* states, float* score) {
+    size_t n = (size_t)T * S * Dm;
+    float* Mst = (float*)malloc(sizeof(float) * (size_t)T * S);
+    int16_t* psi_s = (int16_t*)calloc(n, sizeof(int16_t));
+    int16_t* psi_d = (int16_t*)calloc(n, sizeof(int16_t));
+    float* prevd = (float*)malloc(sizeof(float) * (size_t)S * Dm);   /* delta[st-1][s'][d'-1] */
+    float* x = (float*)malloc(sizeof(float) * (size_t)S * Dm);
+    float* dmax = (float*)malloc(sizeof(float) * S);
+    /* delta value at end e, state s, duration d (start e-d+1) from M */
+#define DELTA_AT(e, s, d) ({ int _st = (e) - (d) + 1; float _r;                                  \
+        if (_st < 0) _r = -INFINITY;                                                             \
+        else { float _o = tsum(lp, S, _st, (d), (s)); float _u = dur[(size_t)(s) * Dm + (d) - 1]; \
+               if (_st == 0) _r = _o + _u;                                                       \
+               else { float _m = Mst[(size_t)_st * S + (s)];                                     \
+                      _r = (_m == -INFINITY) ? -INFINITY : (_m + _o) + _u; } }                   \
+        _r; })
+    for (int st = 1; st < T; ++st) {
+        for (int sp = 0; sp < S; ++sp) {
+            float mx = -INFINITY;
+            for (int dp = 1; dp <= Dm; ++dp) {
+                float v = DELTA_AT(st - 1, sp, dp);
+                prevd[(size_t)sp * Dm + dp - 1] = v;
+                if (v > mx) mx = v;
+            }
+            dmax[sp] = mx;
+        }
+        int dlim = Dm < T - st ? Dm : T - st;
+        for (int s = 0; s < S; ++s) {
+            float M = -INFINITY;
+            for (int sp = 0; sp < S; ++sp) {
+                if (sp == s || dmax[sp] == -INFINITY) continue;
+                float v = dmax[sp] + logT[(size_t)sp * S + s];
+                if (v > M) M = v;
+            }
+            Mst[(size_t)st * S + s] = M;
+            if (M == -INFINITY) continue;               /* literal: delta/psi never written */
+            /* candidate values and the first candidate attaining M */
+            int p1 = -1;
+            float xb = -INFINITY;                       /* max over candidates before p1 */
+            for (int sp = 0; sp < S; ++sp)
+                for (int dp = 1; dp <= Dm; ++dp) {
+                    int k = sp * Dm + dp - 1;
+                    float pv = prevd[k];
+                    float v = (sp == s || pv == -INFINITY) ? -INFINITY : pv + logT[(size_t)sp * S + s];
+                    x[k] = v;
+                    if (p1 < 0) {
+                        if (v == M) p1 = k;
+                        else if (v > xb) xb = v;
+                    }
+                }
+            for (int d = 1; d <= dlim; ++d) {
+                float od = tsum(lp, S, st, d, s), ud = dur[(size_t)s * Dm + d - 1];
+                float F = (M + od) + ud;
+                int win = p1;
+                if (xb != -INFINITY && ((xb + od) + ud) == F) {   /* rare: earlier tie */
+                    for (int k = 0; k < p1; ++k)
+                        if (x[k] != -INFINITY && ((x[k] + od) + ud) == F) { win = k; break; }
+                }
+                size_t e = (size_t)(st + d - 1);
+                psi_s[(e * S + s) * Dm + d - 1] = (int16_t)(win / Dm);
+                psi_d[(e * S + s) * Dm + d - 1] = (int16_t)(win % Dm + 1);
+            }
+        }
+    }
+    float best = -INFINITY;
+    int fs = 0, fd = 1;
+    for (int s = 0; s < S; ++s)
+        for (int d = 1; d <= Dm; ++d) {
+            float sc = DELTA_AT(T - 1, s, d);
+            if (sc > best) { best = sc; fs = s; fd = d; }
+        }
+#undef DELTA_AT
+    hsmm_backtrack(T, S, Dm, psi_s, psi_d, fs, fd, states);
+    *score = best;
+    free(Mst); free(psi_s); free(psi_d); free(prevd); free(x); free(dmax);
+}

@@ -1,0 +1,60 @@
+"""Build libhmm355.so (the gfx950 HIP kernels + C ABI) in-tree with hipcc.
+
+    python -m pytorch_hmm_amd.build_native      (or __graft_entry__.build())
+
+The shared library lands in pytorch_hmm_amd/lib/ so it travels with the repository
+snapshot to the GPU box (it is git-ignored, not gpurun-ignored).
+"""
+import os
+import subprocess
+import sys
+from concurrent.futures import ThreadPoolExecutor
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+CSRC = os.path.join(HERE, "csrc")
+LIBDIR = os.path.join(HERE, "lib")
+LIB = os.path.join(LIBDIR, "libhmm355.so")
+SOURCES = ["capi.hip", "fb.hip", "viterbi.hip", "gmm.hip", "hsmm.hip"]
+ARCH = os.environ.get("HMM355_ARCH", "gfx950")
+FLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-fno-slp-vectorize",
+         "-Wno-unused-result", "-I" + os.path.join(HERE, "..", "include")]
+
+
+def _hipcc():
+    for c in (os.environ.get("HIPCC"), "/opt/rocm/bin/hipcc", "hipcc"):
+        if c and (os.path.isabs(c) and os.path.exists(c) or not os.path.isabs(c)):
+            return c
+    raise RuntimeError("hipcc not found")
+
+
+def build(force=False, verbose=False):
+    os.makedirs(LIBDIR, exist_ok=True)
+    srcs = [s for s in SOURCES if os.path.exists(os.path.join(CSRC, s))]
+    deps = [os.path.join(CSRC, s) for s in srcs] + [os.path.join(CSRC, "common.h"),
+                                                    os.path.join(HERE, "..", "include", "hmm355.h")]
+    if not force and os.path.exists(LIB):
+        lt = os.path.getmtime(LIB)
+        if all(os.path.getmtime(d) <= lt for d in deps if os.path.exists(d)):
+            return LIB
+    hipcc = _hipcc()
+    objdir = os.path.join(LIBDIR, "obj")
+    os.makedirs(objdir, exist_ok=True)
+
+    def compile_one(s):
+        obj = os.path.join(objdir, s.replace(".hip", ".o"))
+        cmd = [hipcc, *FLAGS, "-c", os.path.join(CSRC, s), "-o", obj]
+        if verbose:
+            print(" ".join(cmd), flush=True)
+        subprocess.run(cmd, check=True)
+        return obj
+
+    with ThreadPoolExecutor(max_workers=min(8, len(srcs))) as ex:
+        objs = list(ex.map(compile_one, srcs))
+    tmp = LIB + ".tmp"
+    subprocess.run([hipcc, "-shared", f"--offload-arch={ARCH}", "-o", tmp, *objs], check=True)
+    os.replace(tmp, LIB)
+    return LIB
+
+
+if __name__ == "__main__":
+    print(build(force="--force" in sys.argv, verbose=True))

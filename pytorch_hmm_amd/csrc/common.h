@@ -1,0 +1,141 @@
+// hmm355 — shared device helpers for the gfx950 (CDNA4) kernels.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/hmm355.h"
+
+#define HMM355_API extern "C" __attribute__((visibility("default")))
+
+namespace hmm355 {
+
+constexpr int kWave = 64;
+
+// ---- DPP: row_newbcast:N — every lane of a 16-lane row receives lane N of that row. ----
+template <int N>
+__device__ __forceinline__ float row_bcast(float v) {
+  return __builtin_bit_cast(
+      float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x150 + N, 0xF, 0xF, false));
+}
+
+// acc += row_bcast<N>(v) * m as ONE instruction (v_fmac_f32_dpp).  hipcc does not fold the
+// DPP mov into v_fmac, so it is written out; the hazard recognizer still pads around it.
+template <int N>
+__device__ __forceinline__ void fmac_bcast(float& acc, float v, float m) {
+  asm("v_fmac_f32_dpp %0, %1, %2 row_newbcast:%3 row_mask:0xf bank_mask:0xf"
+      : "+v"(acc)
+      : "v"(v), "v"(m), "n"(N));
+}
+
+// ---- cross-lane sums / maxima without LDS ----
+// v_permlane16_swap / v_permlane32_swap written out: hipcc 7.2's
+// __builtin_amdgcn_permlane{16,32}_swap reads the same register for both halves of the
+// returned pair (miscompile observed at -O0 and -O3), so the pair is kept in two named
+// VGPRs here.  "s_nop 1" covers the VALU-write -> permlane-read hazard inside the asm.
+__device__ __forceinline__ void permlane16_swap(float& a, float& b) {
+  asm volatile("s_nop 1\n\tv_permlane16_swap_b32 %0, %1" : "+v"(a), "+v"(b));
+}
+__device__ __forceinline__ void permlane32_swap(float& a, float& b) {
+  asm volatile("s_nop 1\n\tv_permlane32_swap_b32 %0, %1" : "+v"(a), "+v"(b));
+}
+__device__ __forceinline__ void permlane16_swap_i(int& a, int& b) {
+  asm volatile("s_nop 1\n\tv_permlane16_swap_b32 %0, %1" : "+v"(a), "+v"(b));
+}
+__device__ __forceinline__ void permlane32_swap_i(int& a, int& b) {
+  asm volatile("s_nop 1\n\tv_permlane32_swap_b32 %0, %1" : "+v"(a), "+v"(b));
+}
+
+// sum over the four 16-lane rows of a wave (lanes c, c+16, c+32, c+48), result in every lane
+__device__ __forceinline__ float rows_sum(float x) {
+  float a = x, b = x;
+  permlane16_swap(a, b);   // a = rows [0,0,2,2], b = rows [1,1,3,3]
+  float y = a + b;
+  float c = y, d = y;
+  permlane32_swap(c, d);   // c = halves [0,0], d = halves [1,1]
+  return c + d;
+}
+
+__device__ __forceinline__ float rows_max(float x) {
+  float a = x, b = x;
+  permlane16_swap(a, b);
+  float y = fmaxf(a, b);
+  float c = y, d = y;
+  permlane32_swap(c, d);
+  return fmaxf(c, d);
+}
+
+template <int CTRL>
+__device__ __forceinline__ float dpp_f(float v) {
+  return __builtin_bit_cast(float,
+                            __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), CTRL, 0xF, 0xF, false));
+}
+template <int CTRL>
+__device__ __forceinline__ int dpp_i(int v) {
+  return __builtin_amdgcn_update_dpp(0, v, CTRL, 0xF, 0xF, false);
+}
+
+// sum over the 16 lanes of a row (all lanes of the row get the row sum)
+__device__ __forceinline__ float row16_sum(float x) {
+  x += dpp_f<0xB1>(x);   // quad_perm [1,0,3,2]
+  x += dpp_f<0x4E>(x);   // quad_perm [2,3,0,1]
+  x += dpp_f<0x124>(x);  // row_ror:4
+  x += dpp_f<0x128>(x);  // row_ror:8
+  return x;
+}
+
+// (value, index) argmax combine: larger value wins; equal values -> smaller index
+__device__ __forceinline__ void argmax_combine(float& v, int& i, float v2, int i2) {
+  bool take = (v2 > v) || (v2 == v && i2 < i);
+  v = take ? v2 : v;
+  i = take ? i2 : i;
+}
+
+// full-wave (value, index) argmax via ds_bpermute-free shuffles (used off the hot loop)
+__device__ __forceinline__ void wave_argmax(float& v, int& i) {
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) {
+    float v2 = __shfl_xor(v, off);
+    int i2 = __shfl_xor(i, off);
+    argmax_combine(v, i, v2, i2);
+  }
+}
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) v += __shfl_xor(v, off);
+  return v;
+}
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) v = fmaxf(v, __shfl_xor(v, off));
+  return v;
+}
+
+// Correctly rounded fp32 log(x + 1e-8f): the sum is formed in fp32 exactly as the
+// reference does (hmm.py:86), the log in fp64 then rounded once.  torch-CPU's logf agrees
+// with the correctly rounded value on all but ~2.5e-5 of softmax-distributed inputs.
+__device__ __forceinline__ float log_obs_cr(float x) {
+  float s = x + 1e-8f;
+  return (float)log((double)s);
+}
+
+// LDS barrier: waits for this wave's LDS ops, then s_barrier.  Global stores stay in flight
+// (no vmcnt(0) per step); the "memory" clobber keeps the compiler from moving LDS accesses
+// across it.
+__device__ __forceinline__ void lds_barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+}
+
+// Allow a kernel more than the default 64 KiB of dynamic LDS (gfx950 has 160 KiB per CU).
+template <typename K>
+inline hipError_t allow_lds(K kernel, size_t bytes) {
+  if (bytes <= 65536) return hipSuccess;
+  return hipFuncSetAttribute(reinterpret_cast<const void*>(kernel), hipFuncAttributeMaxDynamicSharedMemorySize,
+                             static_cast<int>(bytes));
+}
+
+inline int pad_states(int N) { return N <= 64 ? 64 : (N <= 128 ? 128 : 256); }
+
+inline size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
+
+}  // namespace hmm355

@@ -1,0 +1,378 @@
+// hmm355 — Viterbi on gfx950.
+//
+// Replaces HMMPyTorch.viterbi_decode (reference hmm.py:132-184) and
+// MixtureGaussianHMMLayer._viterbi_decode (mixture_gaussian.py:290-338).
+//
+// Kernel 1, vit_fwd<NP> (one workgroup per sequence): the max-plus recursion
+//     delta_t[j] = max_i(delta_{t-1}[i] + logP[i,j]) + log_obs_t[j]            (hmm.py:164-168)
+//   computing the max only.  Same lane layout as fb_recur (wave w -> outputs 16w..16w+15,
+//   row group r -> inputs 64*blk + 16r + n, logP slice in VGPRs, delta_{t-1} broadcast by
+//   DPP row_newbcast folded into v_add_f32_dpp, two candidates per v_max3_f32): 1.5 VALU per
+//   cell.  The max of a set of fp32 values is order-independent and each delta is one fp32
+//   add, so delta is bit-identical to the reference given identical log-emissions.  The
+//   emission log(x + 1e-8) is formed in fp32 and the log taken in fp64, rounded once.
+//
+// Kernel 2, vit_psi<NP> (one workgroup per (sequence, 64-step chunk), ~1000 workgroups):
+//   the argmax pointers psi_t[j] = first argmax_i(delta_{t-1}[i] + logP[i,j]) recomputed
+//   from the stored trellis — the same fp32 sums, so the same argmax the reference's
+//   torch.max(dim=1) returns (first index on ties, hmm.py:167).  Taking the argmax out of
+//   the serial loop (4 VALU per cell there) and onto the whole chip is what lets the serial
+//   kernel run at the max-only cost.  While the chunk's psi rows are in LDS the kernel also
+//   composes them into the chunk map G_c[j] = state at the end of chunk c-1 given state j
+//   at the end of chunk c (pointer jumping: 64 dependent LDS lookups per lane).
+//
+// Kernel 3, vit_backtrace<NP> (one wave per (sequence, chunk)): argmax of delta_{T-1}
+//   (first index, hmm.py:174), the chain of chunk maps from the last chunk down to this one
+//   (LDS lookups), then this chunk's 64-step walk (hmm.py:177-178).  The serial depth is
+//   T/64 + 64 lookups instead of T dependent gathers.
+#include "common.h"
+
+namespace hmm355 {
+
+constexpr int kChunk = 64;  // psi / backtrace chunk length (time steps)
+
+template <int NP>
+struct VF {
+  static constexpr int NW = NP / 16;
+  static constexpr int NT = NW * kWave;
+  static constexpr int NBLK = NP / 64;
+  static constexpr int RING = 32;
+  static constexpr int OFF_EMIS = 0;                       // [2][16][NP]
+  static constexpr int OFF_RING = OFF_EMIS + 2 * 16 * NP;  // [RING][NP]
+  static constexpr int LDS_FLOATS = OFF_RING + RING * NP;
+};
+
+struct VitArgs {
+  const float* obs;
+  const float* log_P;
+  const float* init;
+  float* delta;          // (B,T,N) output trellis
+  float* final_score;    // (B) or null
+  int64_t* states;       // (B,T)
+  uint8_t* psi;          // (B,T,NP) workspace
+  uint8_t* G;            // (B,nchunks,NP) workspace
+  int B, T, N, obs_mode, nchunks;
+};
+
+template <int NP>
+__device__ __forceinline__ void vit_load_block(const VitArgs& a, int b, int blk, int w, int l, float (&r)[4]) {
+  const int q = blk * 16 + (l >> 2);
+  const int col = 16 * w + 4 * (l & 3);
+  const bool qok = q < a.T;
+  const float* src = a.obs + ((size_t)b * a.T + (qok ? q : 0)) * a.N;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const bool ok = qok && col + k < a.N;
+    const float x = src[ok ? col + k : 0];
+    r[k] = x;
+  }
+}
+
+template <int NP>
+__device__ __forceinline__ void vit_store_block(const VitArgs& a, float* lds, int blk, int w, int l,
+                                                const float (&r)[4]) {
+  using C = VF<NP>;
+  const int sq = l >> 2;
+  const int col = 16 * w + 4 * (l & 3);
+  float e[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const float lo = a.obs_mode == HMM355_OBS_LOG ? r[k] : log_obs_cr(r[k]);
+    e[k] = col + k < a.N ? lo : -INFINITY;
+  }
+  *reinterpret_cast<float4*>(lds + C::OFF_EMIS + ((blk & 1) * 16 + sq) * NP + col) =
+      make_float4(e[0], e[1], e[2], e[3]);
+}
+
+template <int NP>
+__device__ __forceinline__ void vit_flush(const VitArgs& a, const float* lds, int b, int blk, int tid) {
+  using C = VF<NP>;
+  const int q_base = blk * 16;
+  if (a.N == NP) {
+    constexpr int PER_ROW = NP / 4;
+    const int row = tid / PER_ROW;
+    const int c4 = (tid % PER_ROW) * 4;
+    const int q = q_base + row;
+    if (q < a.T) {
+      const float4 v = *reinterpret_cast<const float4*>(lds + C::OFF_RING + (q % C::RING) * NP + c4);
+      *reinterpret_cast<float4*>(a.delta + ((size_t)b * a.T + q) * NP + c4) = v;
+    }
+  } else {
+    for (int idx = tid; idx < 16 * a.N; idx += C::NT) {
+      const int row = idx / a.N, col = idx - row * a.N;
+      const int q = q_base + row;
+      if (q < a.T) a.delta[((size_t)b * a.T + q) * a.N + col] = lds[C::OFF_RING + (q % C::RING) * NP + col];
+    }
+  }
+}
+
+template <int NP>
+__global__ void __launch_bounds__(VF<NP>::NT) vit_fwd_kernel(VitArgs a) {
+  using C = VF<NP>;
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  const int b = blockIdx.x;
+  const int tid = threadIdx.x;
+  const int w = tid >> 6, l = tid & 63, r = l >> 4, c = l & 15;
+  const int o = 16 * w + c;
+  const int T = a.T, N = a.N;
+
+  float M[C::NBLK][16];
+#pragma unroll
+  for (int blk = 0; blk < C::NBLK; ++blk)
+#pragma unroll
+    for (int n = 0; n < 16; ++n) {
+      const int i = 64 * blk + 16 * r + n;
+      const bool ok = i < N && o < N;
+      const float v = a.log_P[ok ? (size_t)i * N + o : 0];
+      M[blk][n] = ok ? v : -INFINITY;
+    }
+
+  const int nblocks = (T + 15) / 16;
+  float er0[4], er1[4];
+  vit_load_block<NP>(a, b, 0, w, l, er0);
+  if (nblocks > 1) vit_load_block<NP>(a, b, 1, w, l, er1);
+  vit_store_block<NP>(a, lds, 0, w, l, er0);
+  lds_barrier();
+  {
+    // delta_0 = init + log_obs_0  (hmm.py:159; mixture_gaussian.py:312)
+    const float lo = lds[C::OFF_EMIS + o];
+    const float ini = a.init[o < N ? o : 0];
+    if (r == 0) lds[C::OFF_RING + o] = o < N ? ini + lo : -INFINITY;
+  }
+  lds_barrier();
+
+  auto run_block = [&](int kb, float(&ernext)[4], float(&erfree)[4]) {
+    if (kb + 1 < nblocks) vit_store_block<NP>(a, lds, kb + 1, w, l, ernext);
+    if (kb + 2 < nblocks) vit_load_block<NP>(a, b, kb + 2, w, l, erfree);
+    if (kb >= 1) vit_flush<NP>(a, lds, b, kb - 1, tid);
+    const int q0 = kb * 16 < 1 ? 1 : kb * 16;
+    const int q1 = (kb + 1) * 16 < T ? (kb + 1) * 16 : T;
+    for (int q = q0; q < q1; ++q) {
+      float yv[C::NBLK];
+#pragma unroll
+      for (int blk = 0; blk < C::NBLK; ++blk)
+        yv[blk] = lds[C::OFF_RING + ((q - 1) % C::RING) * NP + 64 * blk + l];
+      float m0 = -INFINITY, m1 = -INFINITY, m2 = -INFINITY, m3 = -INFINITY;
+#pragma unroll
+      for (int blk = 0; blk < C::NBLK; ++blk) {
+        m0 = fmaxf(m0, fmaxf(row_bcast<0>(yv[blk]) + M[blk][0], row_bcast<1>(yv[blk]) + M[blk][1]));
+        m1 = fmaxf(m1, fmaxf(row_bcast<2>(yv[blk]) + M[blk][2], row_bcast<3>(yv[blk]) + M[blk][3]));
+        m2 = fmaxf(m2, fmaxf(row_bcast<4>(yv[blk]) + M[blk][4], row_bcast<5>(yv[blk]) + M[blk][5]));
+        m3 = fmaxf(m3, fmaxf(row_bcast<6>(yv[blk]) + M[blk][6], row_bcast<7>(yv[blk]) + M[blk][7]));
+        m0 = fmaxf(m0, fmaxf(row_bcast<8>(yv[blk]) + M[blk][8], row_bcast<9>(yv[blk]) + M[blk][9]));
+        m1 = fmaxf(m1, fmaxf(row_bcast<10>(yv[blk]) + M[blk][10], row_bcast<11>(yv[blk]) + M[blk][11]));
+        m2 = fmaxf(m2, fmaxf(row_bcast<12>(yv[blk]) + M[blk][12], row_bcast<13>(yv[blk]) + M[blk][13]));
+        m3 = fmaxf(m3, fmaxf(row_bcast<14>(yv[blk]) + M[blk][14], row_bcast<15>(yv[blk]) + M[blk][15]));
+      }
+      const float m = rows_max(fmaxf(fmaxf(m0, m1), fmaxf(m2, m3)));
+      const float lo = lds[C::OFF_EMIS + ((kb & 1) * 16 + (q & 15)) * NP + o];
+      if (r == 0) lds[C::OFF_RING + (q % C::RING) * NP + o] = m + lo;
+      lds_barrier();
+    }
+  };
+  for (int k = 0; k < nblocks; k += 2) {
+    run_block(k, er1, er0);
+    if (k + 1 < nblocks) run_block(k + 1, er0, er1);
+  }
+  vit_flush<NP>(a, lds, b, nblocks - 1, tid);
+}
+
+// ---------------------------------------------------------------------------- psi
+template <int NP>
+__global__ void __launch_bounds__(VF<NP>::NT) vit_psi_kernel(VitArgs a) {
+  using C = VF<NP>;
+  __shared__ __attribute__((aligned(16))) uint8_t prow[kChunk][NP];
+  const int chunk = blockIdx.x, b = blockIdx.y;
+  const int tid = threadIdx.x;
+  const int w = tid >> 6, l = tid & 63, r = l >> 4, c = l & 15;
+  const int o = 16 * w + c;
+  const int T = a.T, N = a.N;
+  const int t_lo = chunk * kChunk;
+  const int t_hi = (t_lo + kChunk < T ? t_lo + kChunk : T) - 1;
+
+  float M[C::NBLK][16];
+#pragma unroll
+  for (int blk = 0; blk < C::NBLK; ++blk)
+#pragma unroll
+    for (int n = 0; n < 16; ++n) {
+      const int i = 64 * blk + 16 * r + n;
+      const bool ok = i < N && o < N;
+      const float v = a.log_P[ok ? (size_t)i * N + o : 0];
+      M[blk][n] = ok ? v : -INFINITY;
+    }
+  if (t_lo == 0 && tid < NP) prow[0][tid] = 0;  // psi_0 (hmm.py:156 zeros)
+
+  const float* dbase = a.delta + (size_t)b * T * N;
+  auto load_row = [&](int t, float(&yv)[C::NBLK]) {
+#pragma unroll
+    for (int blk = 0; blk < C::NBLK; ++blk) {
+      const int i = 64 * blk + l;
+      const bool ok = i < N;
+      const float v = dbase[(size_t)(t - 1) * N + (ok ? i : 0)];
+      yv[blk] = ok ? v : -INFINITY;
+    }
+  };
+  const int t_first = t_lo > 0 ? t_lo : 1;
+  float ycur[C::NBLK], ynext[C::NBLK];
+  if (t_first <= t_hi) load_row(t_first, ycur);
+  for (int t = t_first; t <= t_hi; ++t) {
+    if (t + 1 <= t_hi) load_row(t + 1, ynext);
+    // lane-local scan in increasing i (i = 64*blk + 16r + n): strict > keeps the first
+    float bv = row_bcast<0>(ycur[0]) + M[0][0];
+    int bk = 0;  // local index 16*blk + n
+#pragma unroll
+    for (int blk = 0; blk < C::NBLK; ++blk) {
+#define PSI_STEP(n)                                                  \
+  if (blk != 0 || n != 0) {                                          \
+    const float s = row_bcast<n>(ycur[blk]) + M[blk][n];             \
+    const bool gt = s > bv;                                          \
+    bv = gt ? s : bv;                                                \
+    bk = gt ? 16 * blk + n : bk;                                     \
+  }
+      PSI_STEP(0) PSI_STEP(1) PSI_STEP(2) PSI_STEP(3) PSI_STEP(4) PSI_STEP(5) PSI_STEP(6) PSI_STEP(7)
+      PSI_STEP(8) PSI_STEP(9) PSI_STEP(10) PSI_STEP(11) PSI_STEP(12) PSI_STEP(13) PSI_STEP(14) PSI_STEP(15)
+#undef PSI_STEP
+    }
+    int bi = 64 * (bk >> 4) + 16 * r + (bk & 15);
+    // combine the four row groups: (value, index) lexicographic, ties -> smaller index
+    {
+      float va = bv, vb = bv;
+      int ia = bi, ib = bi;
+      permlane16_swap(va, vb);
+      permlane16_swap_i(ia, ib);
+      argmax_combine(va, ia, vb, ib);
+      float vc = va, vd = va;
+      int ic = ia, id = ia;
+      permlane32_swap(vc, vd);
+      permlane32_swap_i(ic, id);
+      argmax_combine(vc, ic, vd, id);
+      bi = ic;
+    }
+    if (r == 0) prow[t - t_lo][o] = (uint8_t)bi;
+#pragma unroll
+    for (int blk = 0; blk < C::NBLK; ++blk) ycur[blk] = ynext[blk];
+  }
+  __syncthreads();
+  // write psi rows (16 B per thread-iteration)
+  const int rows = t_hi - t_lo + 1;
+  uint8_t* pdst = a.psi + ((size_t)b * T + t_lo) * NP;
+  for (int idx = tid; idx < rows * NP / 16; idx += C::NT) {
+    const int row = idx / (NP / 16), c16 = (idx % (NP / 16)) * 16;
+    *reinterpret_cast<uint4*>(pdst + (size_t)row * NP + c16) = *reinterpret_cast<const uint4*>(&prow[row][c16]);
+  }
+  // chunk map: G[j] = state at t_lo - 1 given state j at t_hi
+  if (chunk > 0 && tid < NP) {
+    int s = tid < N ? tid : 0;
+    for (int t = t_hi; t > t_lo; --t) s = prow[t - t_lo][s];
+    a.G[((size_t)b * a.nchunks + chunk) * NP + tid] = prow[0][s];
+  }
+}
+
+// ----------------------------------------------------------------------- backtrace
+template <int NP>
+__global__ void __launch_bounds__(64) vit_backtrace_kernel(VitArgs a) {
+  constexpr int K = NP / 64;
+  constexpr int GB = 64;  // chunk maps staged per LDS batch
+  __shared__ __attribute__((aligned(16))) uint8_t gs[GB][NP];
+  __shared__ __attribute__((aligned(16))) uint8_t ps[kChunk][NP];
+  __shared__ int st[kChunk];
+  const int chunk = blockIdx.x, b = blockIdx.y;
+  const int l = threadIdx.x;
+  const int T = a.T, N = a.N, nc = a.nchunks;
+
+  // s_{T-1} = argmax delta_{T-1} (first index; hmm.py:174)
+  const float* dl = a.delta + ((size_t)b * T + T - 1) * N;
+  float bv = -INFINITY;
+  int bi = 0x7fffffff;
+#pragma unroll
+  for (int k = 0; k < K; ++k) {
+    const int j = l + 64 * k;
+    const bool ok = j < N;
+    const float v = dl[ok ? j : 0];
+    if (ok) argmax_combine(bv, bi, v, j);
+  }
+  wave_argmax(bv, bi);
+  if (chunk == 0 && l == 0 && a.final_score) a.final_score[b] = bv;
+  int s = bi;
+
+  // walk the chunk maps from the last chunk down to chunk+1
+  for (int hi = nc - 1; hi > chunk; hi -= GB) {
+    const int lo = hi - GB + 1 > chunk + 1 ? hi - GB + 1 : chunk + 1;
+    const int cnt = hi - lo + 1;
+    const uint8_t* gsrc = a.G + ((size_t)b * nc + lo) * NP;
+    for (int idx = l; idx < cnt * NP / 16; idx += 64)
+      *reinterpret_cast<uint4*>(&gs[0][0] + idx * 16) = *reinterpret_cast<const uint4*>(gsrc + idx * 16);
+    __syncthreads();
+    for (int cc = hi; cc >= lo; --cc) s = gs[cc - lo][s];
+    __syncthreads();
+  }
+  // this chunk's psi rows, then the walk
+  const int t_lo = chunk * kChunk;
+  const int t_hi = (t_lo + kChunk < T ? t_lo + kChunk : T) - 1;
+  const int rows = t_hi - t_lo + 1;
+  const uint8_t* psrc = a.psi + ((size_t)b * T + t_lo) * NP;
+  for (int idx = l; idx < rows * NP / 16; idx += 64)
+    *reinterpret_cast<uint4*>(&ps[0][0] + idx * 16) = *reinterpret_cast<const uint4*>(psrc + idx * 16);
+  __syncthreads();
+  if (l == 0) {
+    st[t_hi - t_lo] = s;
+    for (int t = t_hi; t > t_lo; --t) {
+      s = ps[t - t_lo][s];
+      st[t - 1 - t_lo] = s;
+    }
+  }
+  __syncthreads();
+  for (int i = l; i < rows; i += 64) a.states[(size_t)b * T + t_lo + i] = st[i];
+}
+
+template <int NP>
+static hipError_t launch_vit(const VitArgs& va, hipStream_t sm) {
+  using C = VF<NP>;
+  hipError_t e = allow_lds(vit_fwd_kernel<NP>, C::LDS_FLOATS * sizeof(float));
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(vit_fwd_kernel<NP>, dim3(va.B), dim3(C::NT), C::LDS_FLOATS * sizeof(float), sm, va);
+  e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(vit_psi_kernel<NP>, dim3(va.nchunks, va.B), dim3(C::NT), 0, sm, va);
+  e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(vit_backtrace_kernel<NP>, dim3(va.nchunks, va.B), dim3(64), 0, sm, va);
+  return hipGetLastError();
+}
+
+}  // namespace hmm355
+
+using namespace hmm355;
+
+HMM355_API size_t hmm355_viterbi_workspace_bytes(int B, int T, int N) {
+  if (B < 0 || T < 1 || N < 1 || N > 256) return 0;
+  const size_t NP = pad_states(N);
+  const size_t nc = (T + kChunk - 1) / kChunk;
+  return align_up((size_t)B * T * NP, 256) + align_up((size_t)B * nc * NP, 256);
+}
+
+HMM355_API int hmm355_viterbi_f32(const float* obs, int obs_mode, const float* log_P, const float* init, int B,
+                                  int T, int N, int64_t* states, float* log_delta, float* final_score,
+                                  void* workspace, size_t workspace_bytes, void* stream) {
+  if (B < 0 || N < 0) return HMM355_E_ARG;
+  if (N < 1 || N > 256) return HMM355_E_STATES;
+  if (T < 1) return HMM355_E_SHAPE;
+  if (B == 0) return HMM355_OK;
+  if (!obs || !log_P || !init || !states || !log_delta || !workspace) return HMM355_E_ARG;
+  if (obs_mode != HMM355_OBS_PROB && obs_mode != HMM355_OBS_LOG) return HMM355_E_ARG;
+  if ((size_t)B * T > (size_t)1 << 40 || B > 65535) return HMM355_E_SHAPE;
+  if (workspace_bytes < hmm355_viterbi_workspace_bytes(B, T, N)) return HMM355_E_WORKSPACE;
+  const int NP = pad_states(N);
+  const int nc = (T + kChunk - 1) / kChunk;
+  uint8_t* psi = static_cast<uint8_t*>(workspace);
+  uint8_t* G = psi + align_up((size_t)B * T * NP, 256);
+  VitArgs va{obs, log_P, init, log_delta, final_score, states, psi, G, B, T, N, obs_mode, nc};
+  hipStream_t sm = static_cast<hipStream_t>(stream);
+  hipError_t e;
+  switch (NP) {
+    case 64: e = launch_vit<64>(va, sm); break;
+    case 128: e = launch_vit<128>(va, sm); break;
+    default: e = launch_vit<256>(va, sm); break;
+  }
+  return e == hipSuccess ? HMM355_OK : (int)e;
+}

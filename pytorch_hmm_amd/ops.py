@@ -1,0 +1,150 @@
+"""PyTorch-ROCm custom ops over the hmm355 C ABI (namespace ``hmm355``).
+
+Each op allocates its outputs (and the C ABI's workspace) through the torch caching
+allocator on the input's device and launches on the current HIP stream.  The ops are
+registered with torch.library so they are visible to torch.compile / export and have
+shape-only fake implementations; their only real implementation is the HIP library.
+
+  torch.ops.hmm355.forward_backward(obs, log_P, log_p0, obs_mode, out_mask)
+      -> (posterior, forward, backward, loglik, lik_ref)
+  torch.ops.hmm355.viterbi(obs, log_P, init, obs_mode) -> (states, log_delta, final_score)
+  torch.ops.hmm355.gmm_diag_logprob(x, means, log_vars, log_w, mix_lse) -> log_probs
+  torch.ops.hmm355.hsmm_viterbi(lp, dur_lp, log_T) -> (states, scores)
+"""
+from typing import Tuple
+
+import torch
+from torch import Tensor
+
+from . import _native as nat
+
+OBS_PROB = nat.OBS_PROB
+OBS_LOG = nat.OBS_LOG
+FB_POSTERIOR = nat.FB_POSTERIOR
+FB_FORWARD = nat.FB_FORWARD
+FB_BACKWARD = nat.FB_BACKWARD
+
+_EMPTY = (0,)
+
+
+def _f32c(t):
+    return t.to(torch.float32).contiguous()
+
+
+def _workspace(nbytes, device):
+    return torch.empty(max(int(nbytes), 1), dtype=torch.uint8, device=device)
+
+
+# ------------------------------------------------------------------ forward-backward
+@torch.library.custom_op("hmm355::forward_backward", mutates_args=())
+def forward_backward(obs: Tensor, log_P: Tensor, log_p0: Tensor, obs_mode: int,
+                     out_mask: int) -> Tuple[Tensor, Tensor, Tensor, Tensor, Tensor]:
+    nat.require_gpu(obs, log_P, log_p0)
+    obs, log_P, log_p0 = _f32c(obs), _f32c(log_P), _f32c(log_p0)
+    B, T, N = obs.shape
+    dev = obs.device
+    L = nat.lib()
+    post = torch.empty((B, T, N) if out_mask & FB_POSTERIOR else _EMPTY, device=dev)
+    fwd = torch.empty((B, T, N) if out_mask & FB_FORWARD else _EMPTY, device=dev)
+    bwd = torch.empty((B, T, N) if out_mask & FB_BACKWARD else _EMPTY, device=dev)
+    loglik = torch.empty(B, device=dev)
+    lik_ref = torch.empty(B, device=dev)
+    if B == 0:
+        return post, fwd, bwd, loglik, lik_ref
+    nbytes = L.hmm355_fb_workspace_bytes(B, T, N)
+    ws = _workspace(nbytes, dev)
+    with torch.cuda.device(dev):
+        nat.check(L.hmm355_forward_backward_f32(
+            nat.ptr(obs), obs_mode, nat.ptr(log_P), nat.ptr(log_p0), B, T, N, out_mask,
+            nat.ptr(post) if out_mask & FB_POSTERIOR else None,
+            nat.ptr(fwd) if out_mask & FB_FORWARD else None,
+            nat.ptr(bwd) if out_mask & FB_BACKWARD else None,
+            nat.ptr(loglik), nat.ptr(lik_ref), nat.ptr(ws), ws.numel(), nat.stream_of(dev)))
+    return post, fwd, bwd, loglik, lik_ref
+
+
+@forward_backward.register_fake
+def _(obs, log_P, log_p0, obs_mode, out_mask):
+    B, T, N = obs.shape
+    mk = lambda bit: obs.new_empty((B, T, N) if out_mask & bit else _EMPTY)
+    return mk(FB_POSTERIOR), mk(FB_FORWARD), mk(FB_BACKWARD), obs.new_empty(B), obs.new_empty(B)
+
+
+# ---------------------------------------------------------------------------- Viterbi
+@torch.library.custom_op("hmm355::viterbi", mutates_args=())
+def viterbi(obs: Tensor, log_P: Tensor, init: Tensor, obs_mode: int) -> Tuple[Tensor, Tensor, Tensor]:
+    nat.require_gpu(obs, log_P, init)
+    obs, log_P, init = _f32c(obs), _f32c(log_P), _f32c(init)
+    B, T, N = obs.shape
+    dev = obs.device
+    L = nat.lib()
+    states = torch.empty((B, T), dtype=torch.int64, device=dev)
+    delta = torch.empty((B, T, N), device=dev)
+    final = torch.empty(B, device=dev)
+    if B == 0:
+        return states, delta, final
+    ws = _workspace(L.hmm355_viterbi_workspace_bytes(B, T, N), dev)
+    with torch.cuda.device(dev):
+        nat.check(L.hmm355_viterbi_f32(
+            nat.ptr(obs), obs_mode, nat.ptr(log_P), nat.ptr(init), B, T, N, nat.ptr(states),
+            nat.ptr(delta), nat.ptr(final), nat.ptr(ws), ws.numel(), nat.stream_of(dev)))
+    return states, delta, final
+
+
+@viterbi.register_fake
+def _(obs, log_P, init, obs_mode):
+    B, T, N = obs.shape
+    return (obs.new_empty((B, T), dtype=torch.int64), obs.new_empty((B, T, N)), obs.new_empty(B))
+
+
+# ------------------------------------------------------------------- GMM emission
+@torch.library.custom_op("hmm355::gmm_diag_logprob", mutates_args=())
+def gmm_diag_logprob(x: Tensor, means: Tensor, log_vars: Tensor, log_w: Tensor, mix_lse: int) -> Tensor:
+    nat.require_gpu(x, means, log_vars, log_w)
+    x, means, log_vars, log_w = _f32c(x), _f32c(means), _f32c(log_vars), _f32c(log_w)
+    B, T, D = x.shape
+    S, C, D2 = means.shape
+    if D2 != D:
+        raise ValueError(f"feature dim mismatch: x has {D}, means have {D2}")
+    out = torch.empty((B, T, S), device=x.device)
+    if B * T == 0:
+        return out
+    L = nat.lib()
+    ws = _workspace(L.hmm355_gmm_workspace_bytes(D, S, C), x.device)
+    with torch.cuda.device(x.device):
+        nat.check(L.hmm355_gmm_diag_logprob_f32(
+            nat.ptr(x), nat.ptr(means), nat.ptr(log_vars), nat.ptr(log_w), B, T, D, S, C, mix_lse,
+            nat.ptr(out), nat.ptr(ws), ws.numel(), nat.stream_of(x.device)))
+    return out
+
+
+@gmm_diag_logprob.register_fake
+def _(x, means, log_vars, log_w, mix_lse):
+    return x.new_empty((x.shape[0], x.shape[1], means.shape[0]))
+
+
+# ------------------------------------------------------------------------------- HSMM
+@torch.library.custom_op("hmm355::hsmm_viterbi", mutates_args=())
+def hsmm_viterbi(lp: Tensor, dur_lp: Tensor, log_T: Tensor) -> Tuple[Tensor, Tensor]:
+    nat.require_gpu(lp, dur_lp, log_T)
+    lp, dur_lp, log_T = _f32c(lp), _f32c(dur_lp), _f32c(log_T)
+    B, T, S = lp.shape
+    Dm = dur_lp.shape[1]
+    dev = lp.device
+    states = torch.empty((B, T), dtype=torch.int64, device=dev)
+    scores = torch.empty(B, device=dev)
+    if B == 0:
+        return states, scores
+    L = nat.lib()
+    ws = _workspace(L.hmm355_hsmm_workspace_bytes(B, T, S, Dm), dev)
+    with torch.cuda.device(dev):
+        nat.check(L.hmm355_hsmm_viterbi_f32(
+            nat.ptr(lp), nat.ptr(dur_lp), nat.ptr(log_T), B, T, S, Dm, nat.ptr(states),
+            nat.ptr(scores), nat.ptr(ws), ws.numel(), nat.stream_of(dev)))
+    return states, scores
+
+
+@hsmm_viterbi.register_fake
+def _(lp, dur_lp, log_T):
+    B, T, S = lp.shape
+    return lp.new_empty((B, T), dtype=torch.int64), lp.new_empty(B)

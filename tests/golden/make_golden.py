@@ -1,0 +1,293 @@
+#!/usr/bin/env python3
+"""Generate the golden fixtures in tests/golden/ by running the REFERENCE here.
+
+This script is the only place that imports crlotwhite/pytorch_hmm (read-only at
+/root/reference).  It runs in the build container only; the reference never travels
+to the GPU box.  What travels is the .npz files this script writes: inputs, the
+parameters the reference derived from them, and the reference's outputs.
+
+Run (from the repo root):
+    PYTHONDONTWRITEBYTECODE=1 python tests/golden/make_golden.py
+
+Each fixture records torch.__version__ and the sha256 of its inputs.  Reference call
+sites are cited per fixture (file:line into /root/reference/pytorch_hmm).
+"""
+import hashlib
+import math
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+REF = os.environ.get("HMM_REFERENCE", "/root/reference")
+sys.dont_write_bytecode = True
+sys.path.insert(0, REF)
+import pytorch_hmm  # noqa: E402  (prints its auto_configure banner)
+from pytorch_hmm.hmm import HMMPyTorch  # noqa: E402
+from pytorch_hmm.hmm_layer import HMMLayer, GaussianHMMLayer  # noqa: E402
+from pytorch_hmm.mixture_gaussian import MixtureGaussianHMMLayer  # noqa: E402
+from pytorch_hmm.hsmm import HSMMLayer  # noqa: E402
+from pytorch_hmm.utils import (  # noqa: E402
+    create_left_to_right_matrix, create_transition_matrix)
+
+OUT = os.path.dirname(os.path.abspath(__file__))
+torch.set_num_threads(min(8, os.cpu_count() or 1))
+
+
+def sha(*arrays):
+    h = hashlib.sha256()
+    for a in arrays:
+        h.update(np.ascontiguousarray(a).tobytes())
+    return h.hexdigest()
+
+
+def npf(t):
+    return t.detach().cpu().numpy()
+
+
+def save(name, **arrays):
+    meta = dict(torch_version=torch.__version__, generator="tests/golden/make_golden.py")
+    arrays = {k: (np.asarray(v) if not isinstance(v, np.ndarray) else v) for k, v in arrays.items()}
+    path = os.path.join(OUT, name + ".npz")
+    np.savez_compressed(path, __meta__=np.array(repr(meta)), **arrays)
+    print(f"  wrote {name}.npz ({os.path.getsize(path)/1024:.1f} KiB)")
+
+
+class CaptureExp:
+    """Record the arguments of torch.exp while the reference's forward_backward runs:
+    hmm.py:126-128 calls exp(log_posterior), exp(log_forward), exp(log_backward) in order."""
+
+    def __enter__(self):
+        self.args = []
+        self._orig = torch.exp
+
+        def rec(x, *a, **k):
+            self.args.append(x.detach().clone())
+            return self._orig(x, *a, **k)
+        torch.exp = rec
+        return self
+
+    def __exit__(self, *exc):
+        torch.exp = self._orig
+
+
+def fb_with_internals(hmm, obs):
+    with CaptureExp() as cap:
+        post, fwd, bwd = hmm.forward_backward(obs)
+    log_post, log_alpha, log_beta = cap.args[-3], cap.args[-2], cap.args[-1]
+    loglik = torch.logsumexp(log_alpha[:, -1], dim=-1)   # meaningful LSE(alpha_{T-1})
+    return post, fwd, bwd, log_alpha, log_beta, loglik
+
+
+def uniform_obs(seed, shape, lo=0.0, hi=1.0):
+    """Machine-independent inputs: integer PCG64 stream -> float32, no transcendentals."""
+    rng = np.random.default_rng(seed)
+    x = rng.random(shape, dtype=np.float32)
+    return (x * np.float32(hi - lo) + np.float32(lo)).astype(np.float32)
+
+
+# --------------------------------------------------------------------------------------
+def fx_hmmpytorch(name, P, B, T, seed, p0=None):
+    """HMMPyTorch forward_backward / viterbi_decode / compute_likelihood
+    (hmm.py:66-130, 132-184, 186-211)."""
+    torch.manual_seed(seed)
+    N = P.shape[0]
+    obs = torch.softmax(torch.randn(B, T, N), dim=-1)          # examples/benchmark.py:160-162
+    hmm = HMMPyTorch(P, p0) if p0 is not None else HMMPyTorch(P)
+    post, fwd, bwd, la, lb, ll = fb_with_internals(hmm, obs)
+    states, delta = hmm.viterbi_decode(obs)
+    lik = hmm.compute_likelihood(obs)
+    save(name, P=npf(P), p0=(npf(p0) if p0 is not None else np.zeros(0, np.float32)),
+         obs=npf(obs), log_obs=npf(torch.log(obs + 1e-8)), log_P=npf(hmm.log_P),
+         log_p0=npf(hmm.log_p0), posterior=npf(post), forward=npf(fwd), backward=npf(bwd),
+         log_alpha=npf(la), log_beta=npf(lb), loglik=npf(ll), states=npf(states),
+         log_delta=npf(delta), compute_likelihood=npf(lik), input_sha256=sha(npf(obs)))
+
+
+def fx_ties():
+    """First-index tie semantics (torch.max, hmm.py:167; argmax :174)."""
+    N, B, T = 8, 2, 50
+    P = create_left_to_right_matrix(N, 0.5)
+    obs = torch.full((B, T, N), 1.0 / N)
+    hmm = HMMPyTorch(P)
+    s1, d1 = hmm.viterbi_decode(obs)
+    Pu = torch.ones(N, N)                                    # ergodic, all-equal rows
+    hmm2 = HMMPyTorch(Pu)
+    s2, d2 = hmm2.viterbi_decode(obs)
+    save("ties", P=npf(P), Pu=npf(Pu), obs=npf(obs), log_obs=npf(torch.log(obs + 1e-8)),
+         log_P=npf(hmm.log_P), log_p0=npf(hmm.log_p0), states=npf(s1), log_delta=npf(d1),
+         log_Pu=npf(hmm2.log_P), log_p0u=npf(hmm2.log_p0), states_u=npf(s2), log_delta_u=npf(d2))
+
+
+def fx_wiki():
+    """tests/test_hmm.py:306-333 weather example (2-D input -> squeezed outputs)."""
+    P = torch.tensor([[0.7, 0.3], [0.4, 0.6]])
+    p0 = torch.tensor([0.6, 0.4])
+    hmm = HMMPyTorch(P, p0)
+    obs = torch.tensor([[0.1, 0.4, 0.5], [0.6, 0.3, 0.1]]).T.contiguous()
+    states, delta = hmm.viterbi_decode(obs)
+    post, fwd, bwd = hmm.forward_backward(obs)
+    lik = hmm.compute_likelihood(obs)
+    save("wiki", P=npf(P), p0=npf(p0), obs=npf(obs), log_P=npf(hmm.log_P), log_p0=npf(hmm.log_p0),
+         states=npf(states), log_delta=npf(delta), posterior=npf(post), forward=npf(fwd),
+         backward=npf(bwd), compute_likelihood=npf(lik))
+
+
+def fx_hmmlayer_c1():
+    """BASELINE config 1: HMMLayer(5), x ~ randn(2,100,5), seed 0 (hmm_layer.py:91-191).
+    Call order matters: call 1 renormalises P (hmm.py:39), later calls do not (hmm_layer.py:83-86)."""
+    torch.manual_seed(0)
+    layer = HMMLayer(5)
+    x = torch.randn(2, 100, 5)
+    layer.train()
+    with CaptureExp() as cap:
+        post1 = layer(x)                                       # call 1 -> HMMPyTorch(P, p0)
+    la1, lb1 = cap.args[-2], cap.args[-1]
+    log_P1, log_p01 = layer._hmm.log_P.detach().clone(), layer._hmm.log_p0.detach().clone()
+    layer.eval()
+    onehot2, align2 = layer(x, return_alignment=True)          # call 2 -> log(P+1e-8)
+    log_P2, log_p02 = layer._hmm.log_P.detach().clone(), layer._hmm.log_p0.detach().clone()
+    states3, delta3 = layer.align(x)                           # call 3
+    layer.train()
+    loss4 = layer.compute_loss(x)                              # call 4 (unsupervised NLL)
+    lik4 = layer._hmm.compute_likelihood(torch.sigmoid(x))
+    save("hmmlayer_c1", x=npf(x), obs=npf(torch.sigmoid(x)),
+         log_obs=npf(torch.log(torch.sigmoid(x) + 1e-8)),
+         logits=npf(layer.log_transition_logits), init_logits=npf(layer.log_initial_logits),
+         posterior1=npf(post1), log_alpha1=npf(la1), log_beta1=npf(lb1),
+         log_P1=npf(log_P1), log_p01=npf(log_p01), log_P2=npf(log_P2), log_p02=npf(log_p02),
+         onehot2=npf(onehot2), align2=npf(align2), states3=npf(states3), log_delta3=npf(delta3),
+         loss4=npf(loss4), likelihood4=npf(lik4), input_sha256=sha(npf(x)))
+
+
+def fx_gaussian(name, K, D, B, T, seed):
+    """GaussianHMMLayer (hmm_layer.py:220-359): diag Gaussian log-probs -> exp -> HMMLayer."""
+    torch.manual_seed(seed)
+    layer = GaussianHMMLayer(K, D)
+    x = torch.randn(B, T, D)
+    lp = layer._compute_gaussian_log_probs(x)
+    probs = torch.exp(lp)
+    layer.train()
+    post = layer(x)                                              # call 1 (FB)
+    layer.eval()
+    onehot, states = layer.hmm_layer(probs, return_alignment=True)   # call 2 (Viterbi)
+    loss = layer.compute_loss(x)                                 # call 3
+    save(name, x=npf(x), means=npf(layer.means), log_scales=npf(layer.log_scales),
+         logits=npf(layer.hmm_layer.log_transition_logits),
+         init_logits=npf(layer.hmm_layer.log_initial_logits), log_probs=npf(lp), probs=npf(probs),
+         posterior=npf(post), onehot=npf(onehot), states=npf(states), loss=npf(loss),
+         input_sha256=sha(npf(x)))
+
+
+def fx_mixture(name, S, D, C, B, T, seed, x=None):
+    """MixtureGaussianHMMLayer (mixture_gaussian.py:157-214, 290-365)."""
+    torch.manual_seed(seed)
+    m = MixtureGaussianHMMLayer(S, D, num_components=C)
+    if x is None:
+        x = torch.randn(B, T, D)
+    with torch.no_grad():
+        lp = m.get_observation_log_probs(x)
+        log_T = m._safe_log(m.get_transition_matrix())
+        log_w = m._safe_log(torch.softmax(m.mixture_weights_logits, dim=-1))
+        states, scores = m(x, return_log_probs=True)
+    save(name, x=npf(x), transition_logits=npf(m.transition_logits),
+         mixture_weights_logits=npf(m.mixture_weights_logits), means=npf(m.means),
+         log_vars=npf(m.log_vars), log_probs=npf(lp), log_T=npf(log_T), log_w=npf(log_w),
+         states=npf(states), scores=npf(scores), input_sha256=sha(npf(x)))
+
+
+def fx_hsmm(name, S, D, Dmax, B, T, seed):
+    """HSMMLayer segment Viterbi (hsmm.py:181-354); the literal 5-deep loop, small sizes only."""
+    torch.manual_seed(seed)
+    h = HSMMLayer(S, D, max_duration=Dmax)
+    x = torch.randn(B, T, D)
+    with torch.no_grad():
+        lp = h.get_observation_log_probs(x)
+        dur_lp = torch.log(h.get_duration_probabilities() + h.eps)
+        log_T = torch.log(h.get_transition_matrix() + h.eps)
+        t0 = time.time()
+        states, scores = h(x)
+    print(f"    hsmm {name}: {time.time()-t0:.1f}s")
+    save(name, x=npf(x), transition_logits=npf(h.transition_logits),
+         observation_means=npf(h.observation_means), observation_log_vars=npf(h.observation_log_vars),
+         duration_shape=npf(h.duration_shape), duration_rate=npf(h.duration_rate),
+         log_probs=npf(lp), dur_log_probs=npf(dur_lp), log_T=npf(log_T),
+         states=npf(states), scores=npf(scores), input_sha256=sha(npf(x)))
+
+
+def fx_fullsize_ns():
+    """North-star shape B=32, T=2000, N=128 (left-to-right 0.7): machine-independent uniform
+    inputs (PCG64 -> float32) so the GPU box can regenerate them bit-for-bit.  Stores the
+    reference's Viterbi states (uint8), per-sequence LSE(alpha_{T-1}), final delta row and
+    a few posterior rows; the full tensors are checked on the box against the oracle."""
+    B, T, N = 32, 2000, 128
+    obs_np = uniform_obs(20251015, (B, T, N))
+    obs = torch.from_numpy(obs_np)
+    hmm = HMMPyTorch(create_left_to_right_matrix(N, 0.7))
+    t0 = time.time()
+    post, fwd, bwd, la, lb, ll = fb_with_internals(hmm, obs)
+    t1 = time.time()
+    states, delta = hmm.viterbi_decode(obs)
+    t2 = time.time()
+    print(f"    NS reference: FB {t1-t0:.3f}s  Viterbi {t2-t1:.3f}s")
+    rows = np.array([0, 1, 999, 1998, 1999])
+    save("fullsize_ns", seed=np.int64(20251015), shape=np.array([B, T, N]),
+         log_P=npf(hmm.log_P), log_p0=npf(hmm.log_p0),
+         states=npf(states).astype(np.uint8), loglik=npf(ll), delta_last=npf(delta[:, -1]),
+         post_rows=rows, posterior_rows=npf(post[:, rows]), log_alpha_last=npf(la[:, -1]),
+         log_beta_first=npf(lb[:, 0]), compute_likelihood=npf(hmm.compute_likelihood(obs)),
+         log_obs_sha256=sha(npf(torch.log(obs + 1e-8))), input_sha256=sha(obs_np),
+         ref_fb_seconds=np.float64(t1 - t0), ref_viterbi_seconds=np.float64(t2 - t1))
+
+
+def fx_fullsize_mixture():
+    """BASELINE config 3 shape (S=128, C=4, D=80, B=32, T=2000) with machine-independent x."""
+    B, T, D, S, C = 32, 2000, 80, 128, 4
+    x = torch.from_numpy(uniform_obs(7, (B, T, D), -2.0, 2.0))
+    torch.manual_seed(0)
+    m = MixtureGaussianHMMLayer(S, D, num_components=C)
+    with torch.no_grad():
+        t0 = time.time()
+        lp = m.get_observation_log_probs(x)
+        states, scores = m(x, return_log_probs=True)
+        print(f"    C3 reference: {time.time()-t0:.2f}s")
+    save("fullsize_mixture", shape=np.array([B, T, D, S, C]), x_seed=np.int64(7),
+         transition_logits=npf(m.transition_logits),
+         mixture_weights_logits=npf(m.mixture_weights_logits), means=npf(m.means),
+         log_vars=npf(m.log_vars), states=npf(states).astype(np.uint8), scores=npf(scores),
+         lp_rows=npf(lp[:, :4]), lp_sha256=sha(npf(lp)), input_sha256=sha(npf(x)))
+
+
+def main():
+    only = set(sys.argv[1:])
+    jobs = [
+        ("hmmpytorch_l2r", lambda: fx_hmmpytorch("hmmpytorch_l2r", create_left_to_right_matrix(128, 0.7), 2, 256, 1234)),
+        ("hmmpytorch_ergodic", lambda: fx_hmmpytorch("hmmpytorch_ergodic", create_transition_matrix(128, "ergodic"), 2, 256, 1235)),
+        ("hmmpytorch_small", lambda: fx_hmmpytorch("hmmpytorch_small", create_left_to_right_matrix(3, 0.7), 2, 10, 5,
+                                                    p0=torch.tensor([0.5, 0.3, 0.2]))),
+        ("hmmpytorch_n200", lambda: fx_hmmpytorch("hmmpytorch_n200", create_transition_matrix(200, "left_to_right_skip", 0.5, 0.4, 0.1), 2, 64, 77)),
+        ("ties", fx_ties),
+        ("wiki", fx_wiki),
+        ("hmmlayer_c1", fx_hmmlayer_c1),
+        ("gaussian_c2", lambda: fx_gaussian("gaussian_c2", 64, 80, 2, 128, 0)),
+        ("gaussian_small", lambda: fx_gaussian("gaussian_small", 3, 5, 2, 12, 1)),
+        ("mixture_s16", lambda: fx_mixture("mixture_s16", 16, 80, 4, 2, 256, 0)),
+        ("mixture_s128", lambda: fx_mixture("mixture_s128", 128, 80, 4, 1, 64, 0)),
+        ("mixture_single", lambda: fx_mixture("mixture_single", 1, 10, 1, 1, 20, 3)),
+        ("hsmm_s5", lambda: fx_hsmm("hsmm_s5", 5, 30, 20, 2, 30, 0)),
+        ("hsmm_s2", lambda: fx_hsmm("hsmm_s2", 2, 3, 2, 1, 4, 1)),
+        ("hsmm_s8", lambda: fx_hsmm("hsmm_s8", 8, 20, 10, 1, 40, 2)),
+        ("fullsize_ns", fx_fullsize_ns),
+        ("fullsize_mixture", fx_fullsize_mixture),
+    ]
+    for name, fn in jobs:
+        if only and name not in only:
+            continue
+        print(name)
+        fn()
+
+
+if __name__ == "__main__":
+    main()

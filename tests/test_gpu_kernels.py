@@ -1,0 +1,180 @@
+"""GPU parity: the HIP kernels (through the C ABI / torch ops) against the reference's
+golden vectors (tests/golden, produced by the reference itself) and the oracle.
+
+Contracts:
+  * Viterbi, mixture Viterbi, HSMM: bit-exact states and scores/trellis given identical
+    fp32 log-emissions and log-transition tables.
+  * Forward-backward: fp32 tolerances written per test (the reference's own fp32 result
+    differs from float64 by up to ~6e-4 on posteriors at T=2000, N=128).
+"""
+import math
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import golden
+from oracle import hmm_oracle as O
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda"
+
+
+def t(a, dtype=torch.float32):
+    return torch.as_tensor(np.asarray(a)).to(DEV, dtype)
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _native():
+    import pytorch_hmm_amd._native as nat
+    nat.lib()  # fail loudly if the HIP library is missing
+    assert torch.cuda.is_available()
+
+
+def ops():
+    from pytorch_hmm_amd import ops as o
+    return o
+
+
+# ---------------------------------------------------------------------------- Viterbi
+@pytest.mark.parametrize("name", ["hmmpytorch_l2r", "hmmpytorch_ergodic", "hmmpytorch_small",
+                                  "hmmpytorch_n200"])
+def test_viterbi_bitexact_given_log_obs(name):
+    g = golden(name)
+    o = ops()
+    states, delta, final = o.viterbi(t(g["log_obs"]), t(g["log_P"]), t(g["log_p0"]), o.OBS_LOG)
+    torch.cuda.synchronize()
+    assert np.array_equal(states.cpu().numpy(), g["states"])
+    assert np.array_equal(delta.cpu().numpy().view(np.int32), g["log_delta"].view(np.int32))
+    assert np.array_equal(final.cpu().numpy(), g["log_delta"][:, -1].max(-1))
+
+
+@pytest.mark.parametrize("name", ["hmmpytorch_l2r", "hmmpytorch_ergodic", "hmmpytorch_small",
+                                  "hmmpytorch_n200"])
+def test_viterbi_end_to_end_prob_input(name):
+    """In-kernel log(x + 1e-8) (correctly rounded) vs the reference's torch-CPU log."""
+    g = golden(name)
+    o = ops()
+    states, delta, _ = o.viterbi(t(g["obs"]), t(g["log_P"]), t(g["log_p0"]), o.OBS_PROB)
+    lo_gpu_path = delta.cpu().numpy()
+    assert np.array_equal(states.cpu().numpy(), g["states"])
+    # any difference can only come from a 1-ulp log difference on an emission
+    np.testing.assert_allclose(lo_gpu_path, g["log_delta"], rtol=2e-6, atol=1e-5)
+
+
+def test_viterbi_ties_first_index():
+    g = golden("ties")
+    o = ops()
+    s1, d1, _ = o.viterbi(t(g["log_obs"]), t(g["log_P"]), t(g["log_p0"]), o.OBS_LOG)
+    s2, d2, _ = o.viterbi(t(g["log_obs"]), t(g["log_Pu"]), t(g["log_p0u"]), o.OBS_LOG)
+    assert np.array_equal(s1.cpu().numpy(), g["states"])
+    assert np.array_equal(s2.cpu().numpy(), g["states_u"])
+    assert np.array_equal(d2.cpu().numpy(), g["log_delta_u"])
+
+
+def test_viterbi_hmmlayer_c1_params():
+    g = golden("hmmlayer_c1")
+    o = ops()
+    states, delta, _ = o.viterbi(t(g["log_obs"]), t(g["log_P2"]), t(g["log_p02"]), o.OBS_LOG)
+    assert np.array_equal(states.cpu().numpy(), g["states3"])
+    assert np.array_equal(delta.cpu().numpy(), g["log_delta3"])
+
+
+@pytest.mark.parametrize("B,T,N", [(3, 1, 7), (2, 65, 64), (5, 129, 100), (1, 300, 256), (4, 64, 128),
+                                   (2, 257, 33)])
+def test_viterbi_vs_c_oracle_shapes(B, T, N):
+    """Ragged T around the 16-step staging blocks and 64-step chunks, N padded to 64/128/256."""
+    rng = np.random.default_rng(B * 1000 + T * 7 + N)
+    lo = np.log(rng.random((B, T, N), dtype=np.float32) + np.float32(1e-8)).astype(np.float32)
+    P = rng.random((N, N), dtype=np.float32) ** 4
+    lP = np.log(P / P.sum(1, keepdims=True) + np.float32(1e-8)).astype(np.float32)
+    init = np.log(np.full(N, 1.0 / N, np.float32) + np.float32(1e-8)).astype(np.float32)
+    cs, cd, _ = O.c_viterbi(lo, lP, init)
+    o = ops()
+    states, delta, final = o.viterbi(t(lo), t(lP), t(init), o.OBS_LOG)
+    assert np.array_equal(states.cpu().numpy(), cs)
+    assert np.array_equal(delta.cpu().numpy(), cd)
+
+
+# --------------------------------------------------------------------- forward-backward
+@pytest.mark.parametrize("name", ["hmmpytorch_l2r", "hmmpytorch_ergodic", "hmmpytorch_small",
+                                  "hmmpytorch_n200", "wiki"])
+def test_forward_backward_vs_reference(name):
+    g = golden(name)
+    o = ops()
+    obs = g["obs"] if g["obs"].ndim == 3 else g["obs"][None]
+    post, fwd, bwd, loglik, lik_ref = o.forward_backward(
+        t(obs), t(g["log_P"]), t(g["log_p0"]), o.OBS_PROB, o.FB_POSTERIOR | o.FB_FORWARD | o.FB_BACKWARD)
+    post, fwd, bwd = post.cpu().numpy(), fwd.cpu().numpy(), bwd.cpu().numpy()
+    # posterior: absolute tolerance 2e-4 (reference fp32 vs fp64 differs by up to 7.7e-5 here)
+    np.testing.assert_allclose(post, g["posterior"], atol=2e-4, rtol=0)
+    # forward/backward = exp(log alpha)/exp(log beta): relative 1e-4 where representable
+    for ours, ref in ((fwd, g["forward"]), (bwd, g["backward"])):
+        big = ref > 1e-30
+        np.testing.assert_allclose(ours[big], ref[big], rtol=1e-4)
+        assert np.all(np.abs(ours[~big]) < 1e-29)
+    if "loglik" in g:
+        np.testing.assert_allclose(loglik.cpu().numpy(), g["loglik"], rtol=1e-5)
+    lik = g["compute_likelihood"].reshape(-1)
+    np.testing.assert_allclose(lik_ref.cpu().numpy(), lik, rtol=1e-5, atol=1e-5)
+
+
+def test_forward_backward_vs_fp64_oracle_shapes():
+    for (B, T, N) in [(2, 1, 5), (3, 17, 64), (2, 300, 100), (1, 50, 256), (2, 33, 130)]:
+        rng = np.random.default_rng(T * N)
+        obs = rng.random((B, T, N), dtype=np.float32)
+        P = rng.random((N, N), dtype=np.float32)
+        lP, lp0 = O.hmm_params(torch.from_numpy(P))
+        la, lb, post64, ll64 = O.c_fb64(np.log(obs + np.float32(1e-8)), lP.numpy(), lp0.numpy())
+        o = ops()
+        post, _, _, loglik, _ = o.forward_backward(t(obs), t(lP), t(lp0), o.OBS_PROB, o.FB_POSTERIOR)
+        np.testing.assert_allclose(post.cpu().numpy(), post64, atol=2e-5)
+        np.testing.assert_allclose(loglik.cpu().numpy(), ll64, rtol=2e-6)
+
+
+# ------------------------------------------------------------------------- mixture
+@pytest.mark.parametrize("name", ["mixture_s16", "mixture_s128", "mixture_single"])
+def test_gmm_emission_vs_reference(name):
+    g = golden(name)
+    o = ops()
+    lp = o.gmm_diag_logprob(t(g["x"]), t(g["means"]), t(g["log_vars"]), t(g["log_w"]), 1).cpu().numpy()
+    ref = g["log_probs"]
+    # fp32 summation-order differences only: relative 2e-6 of the magnitude
+    np.testing.assert_allclose(lp, ref, rtol=2e-6, atol=2e-5)
+    lp64 = O.c_gmm64(g["x"], g["means"], g["log_vars"], g["log_w"])
+    np.testing.assert_allclose(lp, lp64, rtol=2e-6, atol=2e-5)
+
+
+@pytest.mark.parametrize("name", ["mixture_s16", "mixture_s128", "mixture_single"])
+def test_mixture_viterbi_bitexact_given_lp(name):
+    g = golden(name)
+    o = ops()
+    S = g["log_T"].shape[0]
+    init = O.mixture_init_vector(S).numpy()
+    states, _, final = o.viterbi(t(g["log_probs"]), t(g["log_T"]), t(init), o.OBS_LOG)
+    assert np.array_equal(states.cpu().numpy(), g["states"])
+    assert np.array_equal(final.cpu().numpy(), g["scores"])
+
+
+# ---------------------------------------------------------------------------- HSMM
+@pytest.mark.parametrize("name", ["hsmm_s5", "hsmm_s2", "hsmm_s8"])
+def test_hsmm_bitexact_given_lp(name):
+    g = golden(name)
+    o = ops()
+    states, scores = o.hsmm_viterbi(t(g["log_probs"]), t(g["dur_log_probs"]), t(g["log_T"]))
+    assert np.array_equal(states.cpu().numpy(), g["states"])
+    assert np.array_equal(scores.cpu().numpy(), g["scores"])
+
+
+@pytest.mark.parametrize("B,T,S,Dm", [(2, 150, 16, 12), (1, 300, 64, 40), (3, 70, 7, 63)])
+def test_hsmm_vs_c_oracle(B, T, S, Dm):
+    rng = np.random.default_rng(T + S + Dm)
+    lp = (-(rng.random((B, T, S), dtype=np.float32) * 40 + 80)).astype(np.float32)
+    dur = np.log(rng.random((S, Dm), dtype=np.float32) + np.float32(1e-8)).astype(np.float32)
+    logT = np.log(rng.random((S, S), dtype=np.float32) + np.float32(1e-8)).astype(np.float32)
+    cs, csc = O.c_hsmm(lp, dur, logT)
+    o = ops()
+    states, scores = o.hsmm_viterbi(t(lp), t(dur), t(logT))
+    assert np.array_equal(states.cpu().numpy(), cs)
+    assert np.array_equal(scores.cpu().numpy(), csc)

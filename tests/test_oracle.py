@@ -1,0 +1,152 @@
+"""CPU: pin the oracle to the reference's golden vectors (bit-exact), and cross-check the
+C restatement against the torch restatement.  No GPU needed."""
+import numpy as np
+import pytest
+import torch
+
+from conftest import golden
+from oracle import hmm_oracle as O
+
+
+def eq(a, b):
+    a, b = np.asarray(a), np.asarray(b)
+    return a.shape == b.shape and np.array_equal(a, b)
+
+
+@pytest.mark.parametrize("name", ["hmmpytorch_l2r", "hmmpytorch_ergodic", "hmmpytorch_small", "hmmpytorch_n200"])
+def test_hmmpytorch_oracle_bitexact(name):
+    g = golden(name)
+    p0 = torch.from_numpy(g["p0"]) if g["p0"].size else None
+    lP, lp0 = O.hmm_params(torch.from_numpy(g["P"]), p0)
+    assert eq(lP, g["log_P"]) and eq(lp0, g["log_p0"])
+    obs = torch.from_numpy(g["obs"])
+    post, fwd, bwd, la, lb = O.forward_backward(obs, lP, lp0)
+    for got, key in ((post, "posterior"), (fwd, "forward"), (bwd, "backward"), (la, "log_alpha"), (lb, "log_beta")):
+        assert eq(got, g[key]), key
+    s, d = O.viterbi_decode(obs, lP, lp0)
+    assert eq(s, g["states"]) and eq(d, g["log_delta"])
+    assert eq(O.compute_likelihood(obs, lP, lp0), g["compute_likelihood"])
+    assert eq(torch.log(obs + 1e-8), g["log_obs"])
+
+
+@pytest.mark.parametrize("name", ["hmmpytorch_l2r", "hmmpytorch_n200"])
+def test_c_viterbi_matches_reference(name):
+    g = golden(name)
+    s, d, _ = O.c_viterbi(g["log_obs"], g["log_P"], g["log_p0"])
+    assert eq(s, g["states"]) and eq(d, g["log_delta"])
+
+
+def test_fb64_close_to_reference():
+    g = golden("hmmpytorch_l2r")
+    _, _, post, ll = O.c_fb64(g["log_obs"], g["log_P"], g["log_p0"])
+    assert np.abs(post - g["posterior"]).max() < 2e-4
+    np.testing.assert_allclose(ll, g["loglik"], rtol=1e-5)
+
+
+def test_ties_and_wiki():
+    g = golden("ties")
+    s, d = O.viterbi_from_log(torch.from_numpy(g["log_obs"]), torch.from_numpy(g["log_P"]), torch.from_numpy(g["log_p0"]))
+    assert eq(s, g["states"]) and eq(d, g["log_delta"])
+    s, d, _ = O.c_viterbi(g["log_obs"], g["log_Pu"], g["log_p0u"])
+    assert eq(s, g["states_u"])
+    assert np.all(g["states_u"] == 0)  # all-equal scores -> index 0 everywhere (first index)
+    w = golden("wiki")
+    lP, lp0 = O.hmm_params(torch.from_numpy(w["P"]), torch.from_numpy(w["p0"]))
+    s, d = O.viterbi_decode(torch.from_numpy(w["obs"]), lP, lp0)
+    assert eq(s, w["states"]) and eq(d, w["log_delta"])
+    post, fwd, bwd, _, _ = O.forward_backward(torch.from_numpy(w["obs"]), lP, lp0)
+    assert eq(post, w["posterior"]) and eq(fwd, w["forward"])
+
+
+def test_hmmlayer_first_call_renormalises():
+    g = golden("hmmlayer_c1")
+    logits, init = torch.from_numpy(g["logits"]), torch.from_numpy(g["init_logits"])
+    lP1, lp01 = O.hmmlayer_params(logits, init, first_call=True)
+    lP2, lp02 = O.hmmlayer_params(logits, init, first_call=False)
+    assert eq(lP1, g["log_P1"]) and eq(lp01, g["log_p01"])
+    assert eq(lP2, g["log_P2"]) and eq(lp02, g["log_p02"])
+    assert not eq(lP1, lP2)  # the quirk: bits differ between call 1 and call 2+
+    x = torch.from_numpy(g["x"])
+    post, _, _, la, lb = O.forward_backward(torch.sigmoid(x), lP1, lp01)
+    assert eq(post, g["posterior1"]) and eq(la, g["log_alpha1"])
+    s, d = O.viterbi_decode(torch.sigmoid(x), lP2, lp02)
+    assert eq(s, g["align2"]) and eq(s, g["states3"]) and eq(d, g["log_delta3"])
+
+
+@pytest.mark.parametrize("name", ["gaussian_c2", "gaussian_small"])
+def test_gaussian_log_probs(name):
+    g = golden(name)
+    lp = O.gaussian_log_probs(torch.from_numpy(g["x"]), torch.from_numpy(g["means"]), torch.from_numpy(g["log_scales"]))
+    assert eq(lp, g["log_probs"])
+    if name == "gaussian_c2":
+        assert np.all(g["probs"] == 0.0)  # D=80: exp underflows everywhere
+
+
+@pytest.mark.parametrize("name", ["mixture_s16", "mixture_s128", "mixture_single"])
+def test_mixture_oracle(name):
+    g = golden(name)
+    lp = O.mixture_log_probs(torch.from_numpy(g["x"]), torch.from_numpy(g["mixture_weights_logits"]),
+                             torch.from_numpy(g["means"]), torch.from_numpy(g["log_vars"]))
+    assert eq(lp, g["log_probs"])
+    assert eq(O.mixture_log_transitions(torch.from_numpy(g["transition_logits"])), g["log_T"])
+    s, sc = O.mixture_viterbi(lp, torch.from_numpy(g["log_T"]))
+    assert eq(s, g["states"]) and eq(sc, g["scores"])
+    init = O.mixture_init_vector(lp.shape[-1]).numpy()
+    cs, cd, _ = O.c_viterbi(g["log_probs"], g["log_T"], init)
+    assert eq(cs, g["states"]) and eq(cd[:, -1].max(-1), g["scores"])
+
+
+def test_mixture_chunked_emission_identical():
+    g = golden("mixture_s16")
+    args = [torch.from_numpy(g[k]) for k in ("x", "mixture_weights_logits", "means", "log_vars")]
+    assert eq(O.mixture_log_probs(*args, t_chunk=37), g["log_probs"])
+
+
+@pytest.mark.parametrize("name", ["hsmm_s5", "hsmm_s2", "hsmm_s8"])
+def test_hsmm_oracle(name):
+    g = golden(name)
+    x = torch.from_numpy(g["x"])
+    lp = O.hsmm_log_probs(x, torch.from_numpy(g["observation_means"]), torch.from_numpy(g["observation_log_vars"]))
+    assert eq(lp, g["log_probs"])
+    Dm = g["dur_log_probs"].shape[1]
+    du = O.hsmm_duration_log_probs(torch.from_numpy(g["duration_shape"]), torch.from_numpy(g["duration_rate"]), 1, Dm)
+    assert eq(du, g["dur_log_probs"])
+    assert eq(O.hsmm_log_transitions(torch.from_numpy(g["transition_logits"])), g["log_T"])
+    for literal in (True, False):
+        s, sc = O.c_hsmm(g["log_probs"], g["dur_log_probs"], g["log_T"], literal=literal)
+        assert eq(s, g["states"]) and eq(sc, g["scores"])
+
+
+@pytest.mark.parametrize("seed,T,S,Dm", [(1, 60, 6, 9), (2, 45, 4, 20), (3, 80, 9, 7)])
+def test_hsmm_fast_equals_literal(seed, T, S, Dm):
+    """The reorganised recursion (max over d' hoisted, exact tie re-resolution) is
+    bit-identical to the literal 5-deep loop, including on near-tie inputs."""
+    rng = np.random.default_rng(seed)
+    lp = np.round(-(rng.random((2, T, S)) * 8 + 4), 1).astype(np.float32)   # coarse -> many ties
+    dur = np.round(np.log(rng.random((S, Dm)) + 1e-3), 1).astype(np.float32)
+    logT = np.round(np.log(rng.random((S, S)) + 1e-3), 1).astype(np.float32)
+    a = O.c_hsmm(lp, dur, logT, literal=True)
+    b = O.c_hsmm(lp, dur, logT, literal=False)
+    assert eq(a[0], b[0]) and eq(a[1], b[1])
+
+
+def test_fullsize_ns_digest():
+    """North-star shape: the oracle reproduces the reference's stored states/loglik."""
+    g = golden("fullsize_ns")
+    B, T, N = g["shape"]
+    obs = O.uniform_obs(int(g["seed"]), (B, T, N))
+    import hashlib
+    assert hashlib.sha256(obs.tobytes()).hexdigest() == str(g["input_sha256"])
+    lo = np.log(obs + np.float32(1e-8))
+    s, d, _ = O.c_viterbi(lo, g["log_P"], g["log_p0"])
+    lo_t = torch.log(torch.from_numpy(obs) + 1e-8).numpy()
+    if np.array_equal(lo, lo_t):
+        assert eq(s.astype(np.uint8), g["states"])
+        assert eq(d[:, -1], g["delta_last"])
+
+
+@pytest.mark.parametrize("tt", ["ergodic", "left_to_right", "left_to_right_skip", "circular"])
+@pytest.mark.parametrize("K", [1, 2, 3, 5, 128])
+def test_transition_factories_match(tt, K):
+    from pytorch_hmm_amd.utils import create_transition_matrix
+    assert eq(create_transition_matrix(K, tt), O.transition_matrix(K, tt))
