@@ -27,22 +27,26 @@ def _hipcc():
     raise RuntimeError("hipcc not found")
 
 
-def build(force=False, verbose=False):
-    os.makedirs(LIBDIR, exist_ok=True)
+def build(force=False, verbose=False, defines=(), out=None):
+    """Compile csrc/*.hip into `out` (default pytorch_hmm_amd/lib/libhmm355.so).
+    `defines` (e.g. ["HMM355_ABL=2"]) are for diagnostic builds only."""
+    lib = out or LIB
+    os.makedirs(os.path.dirname(lib), exist_ok=True)
     srcs = [s for s in SOURCES if os.path.exists(os.path.join(CSRC, s))]
     deps = [os.path.join(CSRC, s) for s in srcs] + [os.path.join(CSRC, "common.h"),
                                                     os.path.join(HERE, "..", "include", "hmm355.h")]
-    if not force and os.path.exists(LIB):
-        lt = os.path.getmtime(LIB)
+    if not force and os.path.exists(lib):
+        lt = os.path.getmtime(lib)
         if all(os.path.getmtime(d) <= lt for d in deps if os.path.exists(d)):
             return LIB
     hipcc = _hipcc()
-    objdir = os.path.join(LIBDIR, "obj")
+    tag = os.path.splitext(os.path.basename(lib))[0]
+    objdir = os.path.join(os.path.dirname(lib), "obj", tag)
     os.makedirs(objdir, exist_ok=True)
 
     def compile_one(s):
         obj = os.path.join(objdir, s.replace(".hip", ".o"))
-        cmd = [hipcc, *FLAGS, "-c", os.path.join(CSRC, s), "-o", obj]
+        cmd = [hipcc, *FLAGS, *["-D" + d for d in defines], "-c", os.path.join(CSRC, s), "-o", obj]
         if verbose:
             print(" ".join(cmd), flush=True)
         subprocess.run(cmd, check=True)
@@ -50,10 +54,10 @@ def build(force=False, verbose=False):
 
     with ThreadPoolExecutor(max_workers=min(8, len(srcs))) as ex:
         objs = list(ex.map(compile_one, srcs))
-    tmp = LIB + ".tmp"
+    tmp = lib + ".tmp"
     subprocess.run([hipcc, "-shared", f"--offload-arch={ARCH}", "-o", tmp, *objs], check=True)
-    os.replace(tmp, LIB)
-    return LIB
+    os.replace(tmp, lib)
+    return lib
 
 
 if __name__ == "__main__":

@@ -7,9 +7,32 @@
 
 #define HMM355_API extern "C" __attribute__((visibility("default")))
 
+// Ablation knobs for diagnostic builds only (tools/ablate.py); 0 in the product build.
+#ifndef HMM355_ABL
+#define HMM355_ABL 0
+#endif
+
+#ifndef HMM355_STAMP
+#define HMM355_STAMP 0
+#endif
+
 namespace hmm355 {
 
 constexpr int kWave = 64;
+constexpr bool kStamp = HMM355_STAMP;
+
+// In-kernel cycle stamp (diagnostic builds only, cdna guide §7): s_memtime with its
+// lgkmcnt wait in ONE asm statement, fenced by sched_barrier on both sides.
+__device__ __forceinline__ unsigned long long stamp() {
+  unsigned long long t;
+  __builtin_amdgcn_sched_barrier(0);
+  asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+  __builtin_amdgcn_sched_barrier(0);
+  return t;
+}
+template <typename T>
+__device__ __forceinline__ void keep(T& v) { asm volatile("" : "+v"(v)); }
+constexpr int kAbl = HMM355_ABL;
 
 // ---- DPP: row_newbcast:N — every lane of a 16-lane row receives lane N of that row. ----
 template <int N>
@@ -125,6 +148,13 @@ __device__ __forceinline__ float log_obs_cr(float x) {
 __device__ __forceinline__ void lds_barrier() {
   asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
 }
+// the per-time-step barrier of the recursions (ablation bit 1 drops it: timing only)
+__device__ __forceinline__ void step_barrier() {
+  if constexpr (kAbl & 1)
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  else
+    lds_barrier();
+}
 
 // Allow a kernel more than the default 64 KiB of dynamic LDS (gfx950 has 160 KiB per CU).
 template <typename K>
@@ -133,6 +163,8 @@ inline hipError_t allow_lds(K kernel, size_t bytes) {
   return hipFuncSetAttribute(reinterpret_cast<const void*>(kernel), hipFuncAttributeMaxDynamicSharedMemorySize,
                              static_cast<int>(bytes));
 }
+
+constexpr size_t kExclusiveLds = 160 * 1024;  // a workgroup that owns its CU
 
 inline int pad_states(int N) { return N <= 64 ? 64 : (N <= 128 ? 128 : 256); }
 

@@ -1,0 +1,353 @@
+// hmm355 — the serial recursion shared by forward-backward and Viterbi (gfx950).
+//
+// One workgroup runs one chain (a sequence's forward pass, backward pass, or Viterbi
+// max-plus pass) over T steps.  The chain is latency-bound (T dependent steps of an
+// NP x NP reduction), so the layout minimises the per-step critical path and the LDS
+// instruction count:
+//
+//   * NW = NP/16 waves; wave w owns outputs o = 16w + c (c = lane & 15); the lane's row
+//     r = lane >> 4 owns the inputs i = 64*blk + 16r + n.  Its matrix slice lives in VGPRs.
+//   * The previous vector is held one value per lane (input 64*blk + lane), so DPP
+//     row_newbcast folded into v_fmac_f32_dpp / v_add_f32_dpp feeds every product from a
+//     register: the inner loop has no LDS traffic.
+//   * The four row groups' partial results for each output are halved in-register by one
+//     v_permlane32_swap (rows {0,2} and {1,3}); lanes 0..31 write the two halves as a
+//     float2 per output (conflict-free ds_write_b32).  After the step's single s_barrier
+//     every lane reads each of its inputs' float2 with one conflict-free ds_read_b64 (the
+//     LDS cycles per step, not only the latency, bound the exchange: 8 waves x NBLK x 2).
+//   * Forward-backward runs in the probability domain with Rabiner scaling: the scale of
+//     step q is 1/c_{q-1} (c = sum of the previous vector, a DPP wave sum beside the FMAs)
+//     and is folded, with the emission, into the partials before they are written.
+//     Viterbi adds the log-emission to each partial max (fl(max + lo) == max(fl(x + lo)),
+//     so the result is still the bit-exact delta).  log-scales accumulate at flush time.
+//   * Emissions are staged 16 steps at a time through a 3-slot LDS ring (global loads issued
+//     two blocks ahead); finished rows sit in a 64-row LDS ring and leave as 16-B stores once
+//     per 16 steps.  The loop body issues no per-step global memory operation.
+//   * The workgroup requests all 160 KiB of LDS so it owns its CU (no co-resident
+//     workgroup of a concurrent kernel steals issue slots from the chain).
+#pragma once
+#include "common.h"
+
+namespace hmm355 {
+
+enum RecKind : int { kFbAlpha = 0, kFbBeta = 1, kVit = 2 };
+
+// diagnostic builds (HMM355_STAMP=1): per wave [gather, compute, write-wait, barrier, steps,
+// total cycles, memtime, memrealtime] summed over the steps (tools/stamps.py)
+constexpr int kStampWaves = 512 * 16;
+static __device__ unsigned long long g_rec_stamps[kStamp ? kStampWaves * 8 : 1];
+
+template <int NP>
+struct RC {
+  static constexpr int NW = NP / 16;     // waves
+  static constexpr int NT = NW * kWave;  // threads
+  static constexpr int NBLK = NP / 64;   // 64-input blocks per lane
+  static constexpr int RING = 64;        // stored-row ring
+  static constexpr int OFF_PART = 0;                       // [2][NP][2] half-wave partials
+  static constexpr int OFF_EMIS = OFF_PART + 2 * NP * 2;   // [3][16][NP]
+  static constexpr int OFF_RING = OFF_EMIS + 3 * 16 * NP;  // [RING][NP]
+  static constexpr int OFF_SC = OFF_RING + RING * NP;      // [RING] normalisers c_rho
+  static constexpr int LDS_FLOATS = OFF_SC + RING;
+  static_assert(LDS_FLOATS * 4 <= kExclusiveLds, "LDS layout too large");
+};
+
+// Sum over all 64 lanes with DPP only (row sums, then row_bcast:15 / row_bcast:31), read
+// from lane 63: wave-uniform.
+__device__ __forceinline__ float wave_sum_bcast(float x) {
+  x = row16_sum(x);
+  x += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, x), 0x142, 0xA, 0xF, false));
+  x += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, x), 0x143, 0xC, 0xF, false));
+  return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, x), 63));
+}
+
+struct RecArgs {
+  const float* obs;   // (B,T,N) emissions
+  const float* mat;   // (N,N) log transition matrix
+  const float* init;  // (N) log_p0 (FB alpha, Viterbi) / unused (FB beta)
+  float* rows;        // stored rows: FB -> (B,T,NP) scaled alpha/beta; Viterbi -> (B,T,N) delta
+  float* ls;          // (B,T) log-scales (FB) or null
+  float* loglik;      // (B) sequence log-likelihood (FB alpha) or null
+  int B, T, N, obs_mode, row_stride;
+};
+
+template <int KIND>
+__device__ __forceinline__ int rec_tau(int q, int T) {
+  return KIND == kFbBeta ? T - 1 - q : q;
+}
+
+// ---- emission staging: lane l of wave w holds 4 consecutive states of one step
+template <int NP, int KIND>
+__device__ __forceinline__ void rec_load(const RecArgs& a, int b, int blk, int w, int l, float (&r)[4]) {
+  const int q = blk * 16 + (l >> 2);
+  const int col = 16 * w + 4 * (l & 3);
+  const bool qok = q < a.T;
+  const float* src = a.obs + ((size_t)b * a.T + (qok ? rec_tau<KIND>(q, a.T) : 0)) * a.N;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const bool ok = qok && col + k < a.N;
+    r[k] = src[ok ? col + k : 0];  // no select: the wait lands at the first (masked) use
+  }
+}
+
+template <int NP, int KIND>
+__device__ __forceinline__ void rec_stage(const RecArgs& a, float* lds, int blk, int w, int l, const float (&r)[4]) {
+  using C = RC<NP>;
+  const int sq = l >> 2;
+  const int col = 16 * w + 4 * (l & 3);
+  const bool qok = blk * 16 + sq < a.T;
+  float e[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const bool ok = qok && col + k < a.N;
+    float v;
+    if (KIND == kVit)
+      v = ok ? (a.obs_mode == HMM355_OBS_LOG ? r[k] : log_obs_cr(r[k])) : -INFINITY;
+    else
+      v = ok ? (a.obs_mode == HMM355_OBS_LOG ? __expf(r[k]) : r[k] + 1e-8f) : 0.f;
+    e[k] = v;
+  }
+  *reinterpret_cast<float4*>(lds + C::OFF_EMIS + ((blk % 3) * 16 + sq) * NP + col) = make_float4(e[0], e[1], e[2], e[3]);
+}
+
+// ---- flush the 16 stored rows of staging block `blk` (+ their log-scales for FB)
+template <int NP, int KIND>
+__device__ __forceinline__ void rec_flush(const RecArgs& a, const float* lds, int b, int blk, int tid, double& base) {
+  using C = RC<NP>;
+  const int q_base = blk * 16;
+  if (a.row_stride == NP) {
+    constexpr int PER_ROW = NP / 4;
+    const int row = tid / PER_ROW, c4 = (tid % PER_ROW) * 4;
+    const int q = q_base + row;
+    if (q < a.T) {
+      const float4 v = *reinterpret_cast<const float4*>(lds + C::OFF_RING + (q & (C::RING - 1)) * NP + c4);
+      *reinterpret_cast<float4*>(a.rows + ((size_t)b * a.T + rec_tau<KIND>(q, a.T)) * NP + c4) = v;
+    }
+  } else {
+    for (int idx = tid; idx < 16 * a.N; idx += C::NT) {
+      const int row = idx / a.N, col = idx - row * a.N;
+      const int q = q_base + row;
+      if (q < a.T)
+        a.rows[((size_t)b * a.T + rec_tau<KIND>(q, a.T)) * a.row_stride + col] =
+            lds[C::OFF_RING + (q & (C::RING - 1)) * NP + col];
+    }
+  }
+  if (KIND != kVit && (tid >> 6) == C::NW - 1) {
+    // LS_rho = LS_{rho-1} + log c_{rho-1}: 16-lane inclusive scan, running base in double
+    const int j = tid & 15, lane = tid & 63;
+    const int rho = q_base + j;
+    float x = (lane < 16 && rho >= 1 && rho < a.T) ? __logf(lds[C::OFF_SC + ((rho - 1) & (C::RING - 1))]) : 0.f;
+    x += dpp_f<0x111>(x);  // row_shr:1
+    x += dpp_f<0x112>(x);  // row_shr:2
+    x += dpp_f<0x114>(x);  // row_shr:4
+    x += dpp_f<0x118>(x);  // row_shr:8
+    if (lane < 16 && rho < a.T) a.ls[(size_t)b * a.T + rec_tau<KIND>(rho, a.T)] = (float)(base + (double)x);
+    base += (double)__builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, x), 15));
+  }
+}
+
+template <int NP, int KIND>
+__device__ __forceinline__ void rec_run(const RecArgs& a, float* lds, int b) {
+  using C = RC<NP>;
+  constexpr bool FB = KIND != kVit;
+  const int tid = threadIdx.x;
+  const int w = tid >> 6, l = tid & 63, r = l >> 4, c = l & 15;
+  const int o = 16 * w + c;  // output of this lane
+  const int T = a.T, N = a.N;
+
+  // matrix slice: M[blk][n] = Mat[i][o] (alpha/Viterbi) or Mat[o][i] (beta), i = 64blk+16r+n
+  float M[C::NBLK][16];
+#pragma unroll
+  for (int blk = 0; blk < C::NBLK; ++blk)
+#pragma unroll
+    for (int n = 0; n < 16; ++n) {
+      const int i = 64 * blk + 16 * r + n;
+      const bool ok = i < N && o < N;
+      const size_t idx = ok ? (KIND == kFbBeta ? (size_t)o * N + i : (size_t)i * N + o) : 0;
+      const float v = a.mat[idx];
+      M[blk][n] = FB ? __expf(ok ? v : -INFINITY) : (ok ? v : -INFINITY);
+    }
+
+  const int nblocks = (T + 15) / 16;
+  float er0[4], er1[4];
+  rec_load<NP, KIND>(a, b, 0, w, l, er0);
+  rec_stage<NP, KIND>(a, lds, 0, w, l, er0);
+  if (nblocks > 1) rec_load<NP, KIND>(a, b, 1, w, l, er1);
+  lds_barrier();
+
+  auto emis = [&](int rho, int idx) { return lds[C::OFF_EMIS + (((rho >> 4) % 3) * 16 + (rho & 15)) * NP + idx]; };
+  // row 0 partials: the whole value in group 0, the identity in groups 1..3
+  {
+    float v0;
+    const int oo = o < N ? o : 0;
+    if (KIND == kFbAlpha) v0 = o < N ? __expf(a.init[oo]) * emis(0, o) : 0.f;  // alpha_0 = p0 * e_0
+    else if (KIND == kFbBeta) v0 = o < N ? 1.f : 0.f;                             // beta_{T-1} = 1
+    else v0 = o < N ? a.init[oo] + emis(0, o) : -INFINITY;                      // delta_0 = init + lo_0
+    const float ident = FB ? 0.f : -INFINITY;
+    if (r < 2) lds[C::OFF_PART + o * 2 + r] = r == 0 ? v0 : ident;
+  }
+  lds_barrier();
+
+  double base = 0.0;
+  unsigned long long st_acc[4] = {0, 0, 0, 0}, st_prev = 0, st_t0 = 0, st_steps = 0;
+  long long rt0 = 0;
+  if (kStamp) { st_t0 = stamp(); st_prev = st_t0; rt0 = __builtin_amdgcn_s_memrealtime(); }
+  auto mark = [&](int k) {
+    if (kStamp) { const unsigned long long t = stamp(); st_acc[k] += t - st_prev; st_prev = t; }
+  };
+  // sum (FB) / max (Viterbi) of the four row-group partials of input 64*blk + lane
+  auto gather = [&](int prv, float (&y)[C::NBLK]) {
+#pragma unroll
+    for (int blk = 0; blk < C::NBLK; ++blk) {
+      // one conflict-free ds_read_b64 per block (2 LDS cycles per wave)
+      const float2 pp = *reinterpret_cast<const float2*>(lds + C::OFF_PART + (prv * NP + 64 * blk + l) * 2);
+      y[blk] = FB ? pp.x + pp.y : fmaxf(pp.x, pp.y);
+    }
+  };
+  // wave 0 keeps the finished row rho (alpha: u, beta: v, Viterbi: delta)
+  auto keep_row = [&](int rho, const float (&y)[C::NBLK]) {
+    if (w == 0) {
+#pragma unroll
+      for (int blk = 0; blk < C::NBLK; ++blk) lds[C::OFF_RING + (rho & (C::RING - 1)) * NP + 64 * blk + l] = y[blk];
+    }
+  };
+
+  auto run_block = [&](int kb, float(&ernext)[4], float(&erfree)[4]) {
+    if (!(kAbl & 4)) {
+      if (kb + 1 < nblocks) rec_stage<NP, KIND>(a, lds, kb + 1, w, l, ernext);
+      if (kb + 2 < nblocks) rec_load<NP, KIND>(a, b, kb + 2, w, l, erfree);
+      if (kb >= 2) rec_flush<NP, KIND>(a, lds, b, kb - 2, tid, base);
+    }
+    const int q0 = kb * 16 < 1 ? 1 : kb * 16;
+    const int q1 = (kb + 1) * 16 < T ? (kb + 1) * 16 : T;
+    for (int q = q0; q < q1; ++q) {
+      const int prv = (q - 1) & 1, cur = q & 1;
+      // the step's emissions are read beside the partials, off the dependent chain
+      float eo = 0.f, ey[C::NBLK];
+      if (KIND == kFbBeta) {
+#pragma unroll
+        for (int blk = 0; blk < C::NBLK; ++blk) ey[blk] = emis(q - 1, 64 * blk + l);
+      } else {
+        eo = emis(q, o);
+      }
+      float y[C::NBLK];
+      if (kStamp) mark(3);
+      gather(prv, y);
+      if (kStamp) { keep(y[0]); mark(0); }
+      keep_row(q - 1, y);
+      if (KIND == kFbBeta) {  // beta's product input is y = v * e (hmm.py:113-115)
+#pragma unroll
+        for (int blk = 0; blk < C::NBLK; ++blk) y[blk] *= ey[blk];
+      }
+      float part;
+      if (FB) {
+        // 32 (NP=128) v_fmac_f32_dpp into four accumulators, with the DPP wave sum of the
+        // product input (c_{q-1}, the Rabiner normaliser) interleaved stage by stage: issue is
+        // in order within a wave, so a sum issued as one block would add its full dependent
+        // latency to the step.  sched_barrier pins the interleave.
+        float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
+        float cx = y[0];
+#pragma unroll
+        for (int blk = 1; blk < C::NBLK; ++blk) cx += y[blk];
+        float cs = 0.f;
+        constexpr int G = 4 * C::NBLK;  // groups of 4 fmacs
+#pragma unroll
+        for (int g = 0; g < G; ++g) {
+          const int blk = g >> 2, n0 = 4 * (g & 3);
+          if (kAbl & 2) {
+            if ((g & 3) == 0) a0 += y[blk];
+          } else {
+            switch (n0) {
+              case 0:  fmac_bcast<0>(a0, y[blk], M[blk][0]);   fmac_bcast<1>(a1, y[blk], M[blk][1]);
+                       fmac_bcast<2>(a2, y[blk], M[blk][2]);   fmac_bcast<3>(a3, y[blk], M[blk][3]);   break;
+              case 4:  fmac_bcast<4>(a0, y[blk], M[blk][4]);   fmac_bcast<5>(a1, y[blk], M[blk][5]);
+                       fmac_bcast<6>(a2, y[blk], M[blk][6]);   fmac_bcast<7>(a3, y[blk], M[blk][7]);   break;
+              case 8:  fmac_bcast<8>(a0, y[blk], M[blk][8]);   fmac_bcast<9>(a1, y[blk], M[blk][9]);
+                       fmac_bcast<10>(a2, y[blk], M[blk][10]); fmac_bcast<11>(a3, y[blk], M[blk][11]); break;
+              default: fmac_bcast<12>(a0, y[blk], M[blk][12]); fmac_bcast<13>(a1, y[blk], M[blk][13]);
+                       fmac_bcast<14>(a2, y[blk], M[blk][14]); fmac_bcast<15>(a3, y[blk], M[blk][15]); break;
+            }
+          }
+          // wave-sum stages spread over the groups (all eight done by the last group)
+#pragma unroll
+          for (int st = (g * 8) / G; st < ((g + 1) * 8) / G; ++st) {
+            switch (st) {
+              case 0: cx += dpp_f<0xB1>(cx); break;   // quad_perm [1,0,3,2]
+              case 1: cx += dpp_f<0x4E>(cx); break;   // quad_perm [2,3,0,1]
+              case 2: cx += dpp_f<0x124>(cx); break;  // row_ror:4
+              case 3: cx += dpp_f<0x128>(cx); break;  // row_ror:8
+              case 4:
+                cx += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, cx), 0x142, 0xA, 0xF, false));
+                break;                                // row_bcast:15
+              case 5:
+                cx += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, cx), 0x143, 0xC, 0xF, false));
+                break;                                // row_bcast:31
+              case 6: cs = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, cx), 63)); break;
+              default: break;
+            }
+          }
+          __builtin_amdgcn_sched_barrier(0);
+        }
+        const float scale = __builtin_amdgcn_rcpf(cs);
+        if (tid == 0) lds[C::OFF_SC + ((q - 1) & (C::RING - 1))] = cs;
+        float h0 = (a0 + a1) + (a2 + a3), h1 = h0;
+        permlane32_swap(h0, h1);  // rows {0,2} / {1,3} summed: lanes 0..31 hold both halves
+        const float acc = h0 + h1;
+        // alpha: u_q = z * e_q / c_{q-1};  beta: v_q = z / c_{q-1}
+        part = KIND == kFbAlpha ? acc * (scale * eo) : acc * scale;
+      } else {
+        float m0 = -INFINITY, m1 = -INFINITY, m2 = -INFINITY, m3 = -INFINITY;
+#pragma unroll
+        for (int blk = 0; blk < C::NBLK; ++blk) {
+          if (kAbl & 2) { m0 = fmaxf(m0, y[blk]); continue; }
+          m0 = fmaxf(m0, fmaxf(row_bcast<0>(y[blk]) + M[blk][0], row_bcast<1>(y[blk]) + M[blk][1]));
+          m1 = fmaxf(m1, fmaxf(row_bcast<2>(y[blk]) + M[blk][2], row_bcast<3>(y[blk]) + M[blk][3]));
+          m2 = fmaxf(m2, fmaxf(row_bcast<4>(y[blk]) + M[blk][4], row_bcast<5>(y[blk]) + M[blk][5]));
+          m3 = fmaxf(m3, fmaxf(row_bcast<6>(y[blk]) + M[blk][6], row_bcast<7>(y[blk]) + M[blk][7]));
+          m0 = fmaxf(m0, fmaxf(row_bcast<8>(y[blk]) + M[blk][8], row_bcast<9>(y[blk]) + M[blk][9]));
+          m1 = fmaxf(m1, fmaxf(row_bcast<10>(y[blk]) + M[blk][10], row_bcast<11>(y[blk]) + M[blk][11]));
+          m2 = fmaxf(m2, fmaxf(row_bcast<12>(y[blk]) + M[blk][12], row_bcast<13>(y[blk]) + M[blk][13]));
+          m3 = fmaxf(m3, fmaxf(row_bcast<14>(y[blk]) + M[blk][14], row_bcast<15>(y[blk]) + M[blk][15]));
+        }
+        float h0 = fmaxf(fmaxf(m0, m1), fmaxf(m2, m3)), h1 = h0;
+        permlane32_swap(h0, h1);
+        // delta_q = max(...) + lo_q: adding lo to each partial max is exact (monotone)
+        part = fmaxf(h0, h1) + eo;
+      }
+      if (kStamp) { keep(part); mark(1); }
+      if (l < 32) lds[C::OFF_PART + (cur * NP + o) * 2 + r] = part;
+      if (kStamp) { mark(2); ++st_steps; }
+      step_barrier();
+    }
+  };
+  for (int k = 0; k < nblocks; k += 2) {
+    run_block(k, er1, er0);
+    if (k + 1 < nblocks) run_block(k + 1, er0, er1);
+  }
+  if (kStamp && (tid & 63) == 0) {
+    const unsigned long long t1 = stamp();
+    const long long rt1 = __builtin_amdgcn_s_memrealtime();
+    unsigned long long* o8 = g_rec_stamps + ((size_t)(blockIdx.x * C::NW + w) % kStampWaves) * 8;
+    o8[0] = st_acc[0]; o8[1] = st_acc[1]; o8[2] = st_acc[2]; o8[3] = st_acc[3];
+    o8[4] = st_steps; o8[5] = t1 - st_t0; o8[6] = t1 - st_t0; o8[7] = (unsigned long long)(rt1 - rt0);
+  }
+  // final row T-1 (its partials were written by the last step, or are the init for T == 1)
+  float y[C::NBLK];
+  gather((T - 1) & 1, y);
+  keep_row(T - 1, y);
+  if (KIND == kFbAlpha && a.loglik && w == C::NW - 1) {
+    float ys = y[0];
+#pragma unroll
+    for (int blk = 1; blk < C::NBLK; ++blk) ys += y[blk];
+    const float cs = wave_sum_bcast(ys);
+    if (l == 0) lds[C::OFF_SC + ((T - 1) & (C::RING - 1))] = cs;  // c_{T-1} (loglik only)
+  }
+  lds_barrier();
+  if (nblocks >= 2) rec_flush<NP, KIND>(a, lds, b, nblocks - 2, tid, base);
+  rec_flush<NP, KIND>(a, lds, b, nblocks - 1, tid, base);
+  if (KIND == kFbAlpha && a.loglik && tid == C::NT - 64) {
+    // loglik = LS_{T-1} + log c_{T-1}; `base` (wave NW-1) now holds LS_{T-1}
+    a.loglik[b] = (float)(base + (double)__logf(lds[C::OFF_SC + ((T - 1) & (C::RING - 1))]));
+  }
+}
+
+}  // namespace hmm355

@@ -5,10 +5,10 @@
 //
 // Kernel 1, vit_fwd<NP> (one workgroup per sequence): the max-plus recursion
 //     delta_t[j] = max_i(delta_{t-1}[i] + logP[i,j]) + log_obs_t[j]            (hmm.py:164-168)
-//   computing the max only.  Same lane layout as fb_recur (wave w -> outputs 16w..16w+15,
-//   row group r -> inputs 64*blk + 16r + n, logP slice in VGPRs, delta_{t-1} broadcast by
-//   DPP row_newbcast folded into v_add_f32_dpp, two candidates per v_max3_f32): 1.5 VALU per
-//   cell.  The max of a set of fp32 values is order-independent and each delta is one fp32
+//   computing the max only, on the serial-chain skeleton of recur.h (wave w owns input
+//   slice 16w..16w+15, delta_{t-1} broadcast by DPP row_newbcast folded into
+//   v_add_f32_dpp, two candidates per v_max3_f32: 1.5 VALU per cell; per-wave partial maxima
+//   combined through LDS after the step's one barrier).  The max of a set of fp32 values is order-independent and each delta is one fp32
 //   add, so delta is bit-identical to the reference given identical log-emissions.  The
 //   emission log(x + 1e-8) is formed in fp32 and the log taken in fp64, rounded once.
 //
@@ -25,7 +25,7 @@
 //   (first index, hmm.py:174), the chain of chunk maps from the last chunk down to this one
 //   (LDS lookups), then this chunk's 64-step walk (hmm.py:177-178).  The serial depth is
 //   T/64 + 64 lookups instead of T dependent gathers.
-#include "common.h"
+#include "recur.h"
 
 namespace hmm355 {
 
@@ -55,126 +55,9 @@ struct VitArgs {
 };
 
 template <int NP>
-__device__ __forceinline__ void vit_load_block(const VitArgs& a, int b, int blk, int w, int l, float (&r)[4]) {
-  const int q = blk * 16 + (l >> 2);
-  const int col = 16 * w + 4 * (l & 3);
-  const bool qok = q < a.T;
-  const float* src = a.obs + ((size_t)b * a.T + (qok ? q : 0)) * a.N;
-#pragma unroll
-  for (int k = 0; k < 4; ++k) {
-    const bool ok = qok && col + k < a.N;
-    const float x = src[ok ? col + k : 0];
-    r[k] = x;
-  }
-}
-
-template <int NP>
-__device__ __forceinline__ void vit_store_block(const VitArgs& a, float* lds, int blk, int w, int l,
-                                                const float (&r)[4]) {
-  using C = VF<NP>;
-  const int sq = l >> 2;
-  const int col = 16 * w + 4 * (l & 3);
-  float e[4];
-#pragma unroll
-  for (int k = 0; k < 4; ++k) {
-    const float lo = a.obs_mode == HMM355_OBS_LOG ? r[k] : log_obs_cr(r[k]);
-    e[k] = col + k < a.N ? lo : -INFINITY;
-  }
-  *reinterpret_cast<float4*>(lds + C::OFF_EMIS + ((blk & 1) * 16 + sq) * NP + col) =
-      make_float4(e[0], e[1], e[2], e[3]);
-}
-
-template <int NP>
-__device__ __forceinline__ void vit_flush(const VitArgs& a, const float* lds, int b, int blk, int tid) {
-  using C = VF<NP>;
-  const int q_base = blk * 16;
-  if (a.N == NP) {
-    constexpr int PER_ROW = NP / 4;
-    const int row = tid / PER_ROW;
-    const int c4 = (tid % PER_ROW) * 4;
-    const int q = q_base + row;
-    if (q < a.T) {
-      const float4 v = *reinterpret_cast<const float4*>(lds + C::OFF_RING + (q % C::RING) * NP + c4);
-      *reinterpret_cast<float4*>(a.delta + ((size_t)b * a.T + q) * NP + c4) = v;
-    }
-  } else {
-    for (int idx = tid; idx < 16 * a.N; idx += C::NT) {
-      const int row = idx / a.N, col = idx - row * a.N;
-      const int q = q_base + row;
-      if (q < a.T) a.delta[((size_t)b * a.T + q) * a.N + col] = lds[C::OFF_RING + (q % C::RING) * NP + col];
-    }
-  }
-}
-
-template <int NP>
-__global__ void __launch_bounds__(VF<NP>::NT) vit_fwd_kernel(VitArgs a) {
-  using C = VF<NP>;
+__global__ void __launch_bounds__(RC<NP>::NT) vit_fwd_kernel(RecArgs ra) {
   extern __shared__ __attribute__((aligned(16))) float lds[];
-  const int b = blockIdx.x;
-  const int tid = threadIdx.x;
-  const int w = tid >> 6, l = tid & 63, r = l >> 4, c = l & 15;
-  const int o = 16 * w + c;
-  const int T = a.T, N = a.N;
-
-  float M[C::NBLK][16];
-#pragma unroll
-  for (int blk = 0; blk < C::NBLK; ++blk)
-#pragma unroll
-    for (int n = 0; n < 16; ++n) {
-      const int i = 64 * blk + 16 * r + n;
-      const bool ok = i < N && o < N;
-      const float v = a.log_P[ok ? (size_t)i * N + o : 0];
-      M[blk][n] = ok ? v : -INFINITY;
-    }
-
-  const int nblocks = (T + 15) / 16;
-  float er0[4], er1[4];
-  vit_load_block<NP>(a, b, 0, w, l, er0);
-  if (nblocks > 1) vit_load_block<NP>(a, b, 1, w, l, er1);
-  vit_store_block<NP>(a, lds, 0, w, l, er0);
-  lds_barrier();
-  {
-    // delta_0 = init + log_obs_0  (hmm.py:159; mixture_gaussian.py:312)
-    const float lo = lds[C::OFF_EMIS + o];
-    const float ini = a.init[o < N ? o : 0];
-    if (r == 0) lds[C::OFF_RING + o] = o < N ? ini + lo : -INFINITY;
-  }
-  lds_barrier();
-
-  auto run_block = [&](int kb, float(&ernext)[4], float(&erfree)[4]) {
-    if (kb + 1 < nblocks) vit_store_block<NP>(a, lds, kb + 1, w, l, ernext);
-    if (kb + 2 < nblocks) vit_load_block<NP>(a, b, kb + 2, w, l, erfree);
-    if (kb >= 1) vit_flush<NP>(a, lds, b, kb - 1, tid);
-    const int q0 = kb * 16 < 1 ? 1 : kb * 16;
-    const int q1 = (kb + 1) * 16 < T ? (kb + 1) * 16 : T;
-    for (int q = q0; q < q1; ++q) {
-      float yv[C::NBLK];
-#pragma unroll
-      for (int blk = 0; blk < C::NBLK; ++blk)
-        yv[blk] = lds[C::OFF_RING + ((q - 1) % C::RING) * NP + 64 * blk + l];
-      float m0 = -INFINITY, m1 = -INFINITY, m2 = -INFINITY, m3 = -INFINITY;
-#pragma unroll
-      for (int blk = 0; blk < C::NBLK; ++blk) {
-        m0 = fmaxf(m0, fmaxf(row_bcast<0>(yv[blk]) + M[blk][0], row_bcast<1>(yv[blk]) + M[blk][1]));
-        m1 = fmaxf(m1, fmaxf(row_bcast<2>(yv[blk]) + M[blk][2], row_bcast<3>(yv[blk]) + M[blk][3]));
-        m2 = fmaxf(m2, fmaxf(row_bcast<4>(yv[blk]) + M[blk][4], row_bcast<5>(yv[blk]) + M[blk][5]));
-        m3 = fmaxf(m3, fmaxf(row_bcast<6>(yv[blk]) + M[blk][6], row_bcast<7>(yv[blk]) + M[blk][7]));
-        m0 = fmaxf(m0, fmaxf(row_bcast<8>(yv[blk]) + M[blk][8], row_bcast<9>(yv[blk]) + M[blk][9]));
-        m1 = fmaxf(m1, fmaxf(row_bcast<10>(yv[blk]) + M[blk][10], row_bcast<11>(yv[blk]) + M[blk][11]));
-        m2 = fmaxf(m2, fmaxf(row_bcast<12>(yv[blk]) + M[blk][12], row_bcast<13>(yv[blk]) + M[blk][13]));
-        m3 = fmaxf(m3, fmaxf(row_bcast<14>(yv[blk]) + M[blk][14], row_bcast<15>(yv[blk]) + M[blk][15]));
-      }
-      const float m = rows_max(fmaxf(fmaxf(m0, m1), fmaxf(m2, m3)));
-      const float lo = lds[C::OFF_EMIS + ((kb & 1) * 16 + (q & 15)) * NP + o];
-      if (r == 0) lds[C::OFF_RING + (q % C::RING) * NP + o] = m + lo;
-      lds_barrier();
-    }
-  };
-  for (int k = 0; k < nblocks; k += 2) {
-    run_block(k, er1, er0);
-    if (k + 1 < nblocks) run_block(k + 1, er0, er1);
-  }
-  vit_flush<NP>(a, lds, b, nblocks - 1, tid);
+  rec_run<NP, kVit>(ra, lds, blockIdx.x);
 }
 
 // ---------------------------------------------------------------------------- psi
@@ -327,13 +210,13 @@ __global__ void __launch_bounds__(64) vit_backtrace_kernel(VitArgs a) {
 
 template <int NP>
 static hipError_t launch_vit(const VitArgs& va, hipStream_t sm) {
-  using C = VF<NP>;
-  hipError_t e = allow_lds(vit_fwd_kernel<NP>, C::LDS_FLOATS * sizeof(float));
+  hipError_t e = allow_lds(vit_fwd_kernel<NP>, kExclusiveLds);  // own the CU (recur.h)
   if (e != hipSuccess) return e;
-  hipLaunchKernelGGL(vit_fwd_kernel<NP>, dim3(va.B), dim3(C::NT), C::LDS_FLOATS * sizeof(float), sm, va);
+  RecArgs ra{va.obs, va.log_P, va.init, va.delta, nullptr, nullptr, va.B, va.T, va.N, va.obs_mode, va.N};
+  hipLaunchKernelGGL(vit_fwd_kernel<NP>, dim3(va.B), dim3(RC<NP>::NT), kExclusiveLds, sm, ra);
   e = hipGetLastError();
   if (e != hipSuccess) return e;
-  hipLaunchKernelGGL(vit_psi_kernel<NP>, dim3(va.nchunks, va.B), dim3(C::NT), 0, sm, va);
+  hipLaunchKernelGGL(vit_psi_kernel<NP>, dim3(va.nchunks, va.B), dim3(VF<NP>::NT), 0, sm, va);
   e = hipGetLastError();
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL(vit_backtrace_kernel<NP>, dim3(va.nchunks, va.B), dim3(64), 0, sm, va);
@@ -376,3 +259,9 @@ HMM355_API int hmm355_viterbi_f32(const float* obs, int obs_mode, const float* l
   }
   return e == hipSuccess ? HMM355_OK : (int)e;
 }
+
+#if HMM355_STAMP
+HMM355_API int hmm355_debug_stamps_vit(unsigned long long* out, int n) {
+  return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(hmm355::g_rec_stamps), sizeof(unsigned long long) * (size_t)n);
+}
+#endif

@@ -65,7 +65,7 @@ def test_hmmlayer_first_call_renormalises():
     lP2, lp02 = O.hmmlayer_params(logits, init, first_call=False)
     assert eq(lP1, g["log_P1"]) and eq(lp01, g["log_p01"])
     assert eq(lP2, g["log_P2"]) and eq(lp02, g["log_p02"])
-    assert not eq(lP1, lP2)  # the quirk: bits differ between call 1 and call 2+
+    # call 1 renormalises (HMM.__init__), later calls do not: the bits may differ (data-dependent)
     x = torch.from_numpy(g["x"])
     post, _, _, la, lb = O.forward_backward(torch.sigmoid(x), lP1, lp01)
     assert eq(post, g["posterior1"]) and eq(la, g["log_alpha1"])
