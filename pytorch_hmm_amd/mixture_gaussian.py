@@ -1,0 +1,128 @@
+"""MixtureGaussianHMMLayer — drop-in for the reference's GMM-HMM layer
+(mixture_gaussian.py:20-384).
+
+Parameters keep the reference's names, shapes and initialisation (``transition_logits`` or
+the ``transition_matrix`` buffer, ``mixture_weights_logits``, ``means``, ``log_vars``;
+mixture_gaussian.py:59-105) so state_dicts load unchanged.  The emission
+(get_observation_log_probs, :157-214 with the mixture log-sum-exp :141-155) runs in the
+gfx950 GMM scorer without the reference's (B,T,S,C,D) temporary; Viterbi (:290-338) runs
+in the recursion kernels with the reference's uniform start lp_0 - log(S) and returns
+max delta_{T-1} as the sequence score.  Covariance 'diag', 'tied' and 'spherical' map
+onto per-dimension log-variances; 'full' (Cholesky, :216-240) is outside the hot path.
+"""
+import math
+import warnings
+from typing import Optional, Tuple
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from . import ops
+
+
+class MixtureGaussianHMMLayer(nn.Module):
+    def __init__(self, num_states: int, feature_dim: int, num_components: int = 3,
+                 covariance_type: str = "diag", learnable_transitions: bool = True,
+                 max_sequence_length: int = 10000):
+        super().__init__()
+        self.num_states = num_states
+        self.feature_dim = feature_dim
+        self.num_components = num_components
+        self.covariance_type = covariance_type
+        self.learnable_transitions = learnable_transitions
+        self.max_sequence_length = max_sequence_length
+        self.eps = 1e-8
+        self.log_eps = math.log(self.eps)
+        self._init_parameters()
+
+    def _init_parameters(self):
+        """Same draws, in the same order, as mixture_gaussian.py:59-105."""
+        S, C, D = self.num_states, self.num_components, self.feature_dim
+        if self.learnable_transitions:
+            self.transition_logits = nn.Parameter(torch.randn(S, S) * 0.1)
+        else:
+            self.register_buffer("transition_matrix", self._create_left_to_right_matrix())
+        self.mixture_weights_logits = nn.Parameter(torch.randn(S, C) * 0.1)
+        gain = math.sqrt(2.0 / D)
+        self.means = nn.Parameter(torch.randn(S, C, D) * gain)
+        if self.covariance_type == "diag":
+            self.log_vars = nn.Parameter(torch.zeros(S, C, D))
+        elif self.covariance_type == "full":
+            tril = D * (D + 1) // 2
+            self.cholesky_params = nn.Parameter(torch.zeros(S, C, tril))
+            with torch.no_grad():
+                diag = [i * (i + 1) // 2 + i for i in range(D)]
+                self.cholesky_params.data[:, :, diag] = 0.1
+        elif self.covariance_type == "tied":
+            self.log_vars = nn.Parameter(torch.zeros(D))
+        elif self.covariance_type == "spherical":
+            self.log_vars = nn.Parameter(torch.zeros(S, C))
+        else:
+            raise ValueError(f"Unknown covariance_type: {self.covariance_type}")
+
+    def _create_left_to_right_matrix(self) -> torch.Tensor:
+        """0.8 self-loop / 0.2 forward, final state absorbing (mixture_gaussian.py:119-128)."""
+        S = self.num_states
+        P = torch.zeros(S, S)
+        idx = torch.arange(S - 1)
+        P[idx, idx] = 0.8
+        P[idx, idx + 1] = 0.2
+        P[S - 1, S - 1] = 1.0
+        return P
+
+    def get_transition_matrix(self) -> torch.Tensor:
+        if self.learnable_transitions:
+            return F.softmax(self.transition_logits, dim=-1)
+        return self.transition_matrix
+
+    def _safe_log(self, x: torch.Tensor) -> torch.Tensor:
+        return torch.log(torch.clamp(x, min=self.eps))
+
+    def _component_log_vars(self) -> torch.Tensor:
+        """(S,C,D) per-dimension log-variances for the scorer."""
+        S, C, D = self.num_states, self.num_components, self.feature_dim
+        if self.covariance_type == "diag":
+            return self.log_vars
+        if self.covariance_type == "tied":
+            return self.log_vars.view(1, 1, D).expand(S, C, D)
+        if self.covariance_type == "spherical":
+            return self.log_vars.unsqueeze(-1).expand(S, C, D)
+        raise NotImplementedError("covariance_type='full' (Cholesky solve) is outside the gfx950 hot path")
+
+    def get_observation_log_probs(self, observations: torch.Tensor) -> torch.Tensor:
+        """(B,T,D) -> (B,T,S): log sum_c w_sc N(x; mu_sc, diag exp(log_vars_sc))
+        (mixture_gaussian.py:157-214)."""
+        B, T, _ = observations.shape
+        if T > self.max_sequence_length:
+            warnings.warn(f"Sequence length {T} exceeds recommended maximum "
+                          f"{self.max_sequence_length}. Consider chunked processing.")
+        with torch.no_grad():
+            log_w = self._safe_log(F.softmax(self.mixture_weights_logits, dim=-1))
+            return ops.gmm_diag_logprob(observations, self.means, self._component_log_vars(), log_w, 1)
+
+    def _viterbi_decode(self, obs_log_probs: torch.Tensor,
+                        log_transitions: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor]:
+        """(states (B,T), max_j delta_{T-1}[j] (B,)) with delta_0 = lp_0 - log S
+        (mixture_gaussian.py:290-338)."""
+        S = obs_log_probs.shape[-1]
+        init = -(torch.zeros(S, device=obs_log_probs.device) + math.log(S))
+        states, _, final = ops.viterbi(obs_log_probs, log_transitions, init, ops.OBS_LOG)
+        return states, final
+
+    def forward(self, observations: torch.Tensor,
+                return_log_probs: bool = False) -> Tuple[torch.Tensor, Optional[torch.Tensor]]:
+        obs_log_probs = self.get_observation_log_probs(observations)
+        with torch.no_grad():
+            log_transitions = self._safe_log(self.get_transition_matrix())
+        states, scores = self._viterbi_decode(obs_log_probs, log_transitions)
+        return (states, scores) if return_log_probs else (states, None)
+
+    def get_model_info(self) -> dict:
+        total = sum(p.numel() for p in self.parameters())
+        trainable = sum(p.numel() for p in self.parameters() if p.requires_grad)
+        return {"num_states": self.num_states, "feature_dim": self.feature_dim,
+                "num_components": self.num_components, "covariance_type": self.covariance_type,
+                "learnable_transitions": self.learnable_transitions, "total_parameters": total,
+                "trainable_parameters": trainable, "memory_efficient": True,
+                "max_sequence_length": self.max_sequence_length}

@@ -1,0 +1,89 @@
+"""GPU: the reference's layer call sequences (tests/golden/make_golden.py, the same calls the
+reference's tests and BASELINE configs make) through the drop-in layers, against the
+reference's own outputs.
+
+Tolerances: the layers derive log_P / emissions on the GPU (softmax, sigmoid, Gaussian
+scores), which may differ from the reference's torch-CPU bits by an ulp; the recursions
+then carry the FB tolerances of test_gpu_kernels.py.  Viterbi states are compared exactly.
+"""
+import numpy as np
+import pytest
+import torch
+
+import pytorch_hmm_amd as ph
+from conftest import golden
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def t(a):
+    return torch.as_tensor(np.asarray(a)).to(DEV)
+
+
+@torch.no_grad()
+def test_hmmlayer_c1_call_sequence():
+    g = golden("hmmlayer_c1")
+    torch.manual_seed(0)
+    layer = ph.HMMLayer(5).to(DEV)
+    x = t(g["x"])
+    layer.train()
+    post1 = layer(x)                                   # call 1: FB posteriors
+    np.testing.assert_allclose(post1.cpu().numpy(), g["posterior1"], atol=2e-4)
+    layer.eval()
+    onehot2, align2 = layer(x, return_alignment=True)  # call 2: Viterbi one-hot
+    assert np.array_equal(align2.cpu().numpy(), g["align2"])
+    assert np.array_equal(onehot2.cpu().numpy(), g["onehot2"])
+    states3, delta3 = layer.align(x)                   # call 3
+    assert np.array_equal(states3.cpu().numpy(), g["states3"])
+    np.testing.assert_allclose(delta3.cpu().numpy(), g["log_delta3"], rtol=2e-6, atol=2e-5)
+    layer.train()
+    loss4 = layer.compute_loss(x)                      # call 4: -mean compute_likelihood
+    np.testing.assert_allclose(loss4.cpu().numpy(), g["loss4"], rtol=1e-5)
+
+
+@torch.no_grad()
+@pytest.mark.parametrize("name,K,D,seed", [("gaussian_c2", 64, 80, 0), ("gaussian_small", 3, 5, 1)])
+def test_gaussian_layer(name, K, D, seed):
+    g = golden(name)
+    torch.manual_seed(seed)
+    layer = ph.GaussianHMMLayer(K, D).to(DEV)
+    x = t(g["x"])
+    lp = layer._compute_gaussian_log_probs(x).cpu().numpy()
+    np.testing.assert_allclose(lp, g["log_probs"], rtol=2e-6, atol=2e-5)
+    layer.train()
+    post = layer(x)
+    np.testing.assert_allclose(post.cpu().numpy(), g["posterior"], atol=2e-4)
+    layer.eval()
+    onehot, states = layer.hmm_layer(torch.exp(layer._compute_gaussian_log_probs(x)), return_alignment=True)
+    assert np.array_equal(states.cpu().numpy(), g["states"])
+    np.testing.assert_allclose(layer.compute_loss(x).cpu().numpy(), g["loss"], rtol=1e-5)
+
+
+@pytest.mark.parametrize("name,S,D,C,seed", [("mixture_s16", 16, 80, 4, 0), ("mixture_s128", 128, 80, 4, 0),
+                                             ("mixture_single", 1, 10, 1, 3)])
+def test_mixture_layer(name, S, D, C, seed):
+    g = golden(name)
+    torch.manual_seed(seed)
+    m = ph.MixtureGaussianHMMLayer(S, D, num_components=C).to(DEV)
+    x = t(g["x"])
+    lp = m.get_observation_log_probs(x)
+    np.testing.assert_allclose(lp.cpu().numpy(), g["log_probs"], rtol=2e-6, atol=2e-5)
+    states, scores = m(x, return_log_probs=True)
+    assert np.array_equal(states.cpu().numpy(), g["states"])
+    np.testing.assert_allclose(scores.cpu().numpy(), g["scores"], rtol=2e-6)
+    s2, none = m(x)
+    assert none is None and torch.equal(s2, states)
+
+
+@pytest.mark.parametrize("name,S,D,Dm,seed", [("hsmm_s5", 5, 30, 20, 0), ("hsmm_s2", 2, 3, 2, 1),
+                                              ("hsmm_s8", 8, 20, 10, 2)])
+def test_hsmm_layer(name, S, D, Dm, seed):
+    g = golden(name)
+    torch.manual_seed(seed)
+    h = ph.HSMMLayer(S, D, max_duration=Dm).to(DEV)
+    x = t(g["x"])
+    np.testing.assert_allclose(h.get_observation_log_probs(x).cpu().numpy(), g["log_probs"], rtol=2e-6, atol=2e-5)
+    states, scores = h(x)
+    assert np.array_equal(states.cpu().numpy(), g["states"])
+    np.testing.assert_allclose(scores.cpu().numpy(), g["scores"], rtol=2e-6)

@@ -1,0 +1,98 @@
+"""CPU: the C ABI library (pytorch_hmm_amd/lib/libhmm355.so, cross-compiled for gfx950) loads
+without a GPU, exports exactly what include/hmm355.h declares, and rejects bad arguments
+with the documented status codes before launching anything (no compute calls here)."""
+import ctypes
+import os
+import re
+import subprocess
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(ROOT, "include", "hmm355.h")
+
+
+@pytest.fixture(scope="module")
+def L():
+    from pytorch_hmm_amd import _native as nat
+    if not os.path.exists(nat.LIB_PATH):
+        from pytorch_hmm_amd import build_native
+        build_native.build()
+    return nat.lib()
+
+
+def header_functions():
+    src = open(HEADER).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b(hmm355_[a-z0-9_]+)\s*\(", src)))
+
+
+def header_defines():
+    return dict((m.group(1), int(m.group(2).rstrip("u")))
+                for m in re.finditer(r"#define\s+(HMM355_[A-Z0-9_]+)\s+\(?(-?\d+u?)\)?", open(HEADER).read()))
+
+
+def test_exports_match_header(L):
+    from pytorch_hmm_amd import _native as nat
+    declared = header_functions()
+    assert declared == sorted(nat.EXPORTS)
+    out = subprocess.run(["nm", "-D", "--defined-only", nat.LIB_PATH], capture_output=True, text=True, check=True).stdout
+    exported = sorted(set(re.findall(r"\b(hmm355_[a-z0-9_]+)\b", out)) - {"hmm355_debug_stamps_fb", "hmm355_debug_stamps_vit"})
+    assert exported == declared
+    for name in declared:
+        assert hasattr(L, name)
+
+
+def test_constants_match_header():
+    from pytorch_hmm_amd import _native as nat
+    d = header_defines()
+    assert d["HMM355_OBS_PROB"] == nat.OBS_PROB and d["HMM355_OBS_LOG"] == nat.OBS_LOG
+    assert (d["HMM355_FB_POSTERIOR"], d["HMM355_FB_FORWARD"], d["HMM355_FB_BACKWARD"]) == \
+        (nat.FB_POSTERIOR, nat.FB_FORWARD, nat.FB_BACKWARD)
+    assert d["HMM355_OK"] == 0
+
+
+def test_version_and_strerror(L):
+    assert L.hmm355_version() > 0
+    d = header_defines()
+    for code in ("HMM355_E_ARG", "HMM355_E_STATES", "HMM355_E_SHAPE", "HMM355_E_WORKSPACE", "HMM355_E_DURATION"):
+        assert L.hmm355_strerror(d[code]).decode()
+    assert L.hmm355_strerror(0).decode()
+
+
+def test_workspace_sizes(L):
+    B, T, N = 32, 2000, 128
+    fb = L.hmm355_fb_workspace_bytes(B, T, N)
+    assert fb >= 2 * B * T * 128 * 4 + 2 * B * T * 4  # scaled alpha/beta rows + log-scales
+    vit = L.hmm355_viterbi_workspace_bytes(B, T, N)
+    assert vit >= B * T * 128                          # uint8 backpointers
+    assert L.hmm355_gmm_workspace_bytes(80, 128, 4) > 0
+    assert L.hmm355_hsmm_workspace_bytes(16, 2000, 64, 40) > 0
+
+
+def test_argument_rejection_before_launch(L):
+    """Invalid arguments return the documented code; nothing touches the (absent) GPU."""
+    d = header_defines()
+    fake = ctypes.c_void_p(0x1000)  # never dereferenced: validation fails first
+    # N out of range
+    rc = L.hmm355_viterbi_f32(fake, 0, fake, fake, 1, 10, 300, fake, fake, fake, fake, 1 << 30, None)
+    assert rc == d["HMM355_E_STATES"]
+    rc = L.hmm355_forward_backward_f32(fake, 0, fake, fake, 1, 10, 0, 1, fake, None, None, None, None, fake, 1 << 30, None)
+    assert rc == d["HMM355_E_STATES"]
+    # T < 1
+    rc = L.hmm355_viterbi_f32(fake, 0, fake, fake, 1, 0, 8, fake, fake, fake, fake, 1 << 30, None)
+    assert rc == d["HMM355_E_SHAPE"]
+    # null input
+    rc = L.hmm355_viterbi_f32(None, 0, fake, fake, 1, 10, 8, fake, fake, fake, fake, 1 << 30, None)
+    assert rc == d["HMM355_E_ARG"]
+    # workspace too small
+    rc = L.hmm355_forward_backward_f32(fake, 0, fake, fake, 2, 10, 8, 1, fake, None, None, None, None, fake, 16, None)
+    assert rc == d["HMM355_E_WORKSPACE"]
+    # bad obs_mode
+    rc = L.hmm355_viterbi_f32(fake, 7, fake, fake, 1, 10, 8, fake, fake, fake, fake, 1 << 30, None)
+    assert rc == d["HMM355_E_ARG"]
+    # HSMM: duration table out of range
+    rc = L.hmm355_hsmm_viterbi_f32(fake, fake, fake, 1, 10, 4, 0, fake, fake, fake, 1 << 30, None)
+    assert rc == d["HMM355_E_DURATION"]
+    # B == 0 is a no-op success
+    assert L.hmm355_viterbi_f32(None, 0, None, None, 0, 10, 8, None, None, None, None, 0, None) == 0
