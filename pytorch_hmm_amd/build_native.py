@@ -16,7 +16,7 @@ LIBDIR = os.path.join(HERE, "lib")
 LIB = os.path.join(LIBDIR, "libhmm355.so")
 SOURCES = ["capi.hip", "fb.hip", "viterbi.hip", "gmm.hip", "hsmm.hip"]
 ARCH = os.environ.get("HMM355_ARCH", "gfx950")
-FLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-fno-slp-vectorize",
+FLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-fno-slp-vectorize", "-fno-honor-nans",
          "-Wno-unused-result", "-I" + os.path.join(HERE, "..", "include")]
 
 

@@ -26,10 +26,21 @@ template <int NP>
 __global__ void __launch_bounds__(RC<NP>::NT) fb_recur_kernel(RecArgs fa, RecArgs fb) {
   extern __shared__ __attribute__((aligned(16))) float lds[];
   const int b = blockIdx.x >> 1;
-  if (blockIdx.x & 1)
-    rec_run<NP, kFbBeta>(fb, lds, b);
-  else
-    rec_run<NP, kFbAlpha>(fa, lds, b);
+  if (blockIdx.x & 1) {
+    switch (rec_band_width<kFbBeta>(fb)) {
+      case 2: rec_band<NP, kFbBeta, 2>(fb, lds, b, fb.band); break;
+      case 4: rec_band<NP, kFbBeta, 4>(fb, lds, b, fb.band); break;
+      case 8: rec_band<NP, kFbBeta, 8>(fb, lds, b, fb.band); break;
+      default: rec_run<NP, kFbBeta>(fb, lds, b); break;
+    }
+  } else {
+    switch (rec_band_width<kFbAlpha>(fa)) {
+      case 2: rec_band<NP, kFbAlpha, 2>(fa, lds, b, fa.band); break;
+      case 4: rec_band<NP, kFbAlpha, 4>(fa, lds, b, fa.band); break;
+      case 8: rec_band<NP, kFbAlpha, 8>(fa, lds, b, fa.band); break;
+      default: rec_run<NP, kFbAlpha>(fa, lds, b); break;
+    }
+  }
 }
 
 struct PostArgs {
@@ -107,6 +118,10 @@ template <int NP>
 static hipError_t launch_fb(const RecArgs& fa, const RecArgs& fb, const PostArgs& pa, hipStream_t st) {
   hipError_t e = allow_lds(fb_recur_kernel<NP>, kExclusiveLds);  // own the CU (recur.h)
   if (e != hipSuccess) return e;
+  if (fa.band) {
+    e = launch_band_prep(fa.mat, fa.N, const_cast<BandDesc*>(fa.band), st);
+    if (e != hipSuccess) return e;
+  }
   hipLaunchKernelGGL(fb_recur_kernel<NP>, dim3(2 * fa.B), dim3(RC<NP>::NT), kExclusiveLds, st, fa, fb);
   e = hipGetLastError();
   if (e != hipSuccess) return e;
@@ -125,7 +140,8 @@ HMM355_API size_t hmm355_fb_workspace_bytes(int B, int T, int N) {
   if (B < 0 || T < 1 || N < 1 || N > 256) return 0;
   const size_t NP = pad_states(N);
   const size_t rows = (size_t)B * T;
-  return align_up(2 * rows * NP * sizeof(float), 256) + align_up(2 * rows * sizeof(float), 256);
+  return align_up(2 * rows * NP * sizeof(float), 256) + align_up(2 * rows * sizeof(float), 256) +
+         align_up(sizeof(BandDesc), 256);
 }
 
 HMM355_API int hmm355_forward_backward_f32(const float* obs, int obs_mode, const float* log_P,
@@ -151,8 +167,11 @@ HMM355_API int hmm355_forward_backward_f32(const float* obs, int obs_mode, const
   float* V = U + rows * NP;
   float* LA = reinterpret_cast<float*>(ws + align_up(2 * rows * NP * sizeof(float), 256));
   float* LB = LA + rows;
-  RecArgs fa{obs, log_P, log_p0, U, LA, loglik, B, T, N, obs_mode, NP};
-  RecArgs fb{obs, log_P, log_p0, V, LB, nullptr, B, T, N, obs_mode, NP};
+  BandDesc* band = use_band() ? reinterpret_cast<BandDesc*>(ws + align_up(2 * rows * NP * sizeof(float), 256) +
+                                                           align_up(2 * rows * sizeof(float), 256))
+                              : nullptr;
+  RecArgs fa{obs, log_P, log_p0, U, LA, loglik, B, T, N, obs_mode, NP, band};
+  RecArgs fb{obs, log_P, log_p0, V, LB, nullptr, B, T, N, obs_mode, NP, band};
   PostArgs pa{U, V, LA, LB, posterior, forward, backward, lik_ref, B, T, N, out_mask};
   hipStream_t st = static_cast<hipStream_t>(stream);
   hipError_t e;

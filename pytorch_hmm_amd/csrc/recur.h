@@ -26,6 +26,7 @@
 //   * The workgroup requests all 160 KiB of LDS so it owns its CU (no co-resident
 //     workgroup of a concurrent kernel steals issue slots from the chain).
 #pragma once
+#include "band.h"
 #include "common.h"
 
 namespace hmm355 {
@@ -60,6 +61,18 @@ __device__ __forceinline__ float wave_sum_bcast(float x) {
   return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, x), 63));
 }
 
+// Max over all 64 lanes with DPP only, read from lane 63: wave-uniform.
+__device__ __forceinline__ float wave_max_bcast(float x) {
+  x = fmaxf(x, dpp_f<0xB1>(x));
+  x = fmaxf(x, dpp_f<0x4E>(x));
+  x = fmaxf(x, dpp_f<0x124>(x));
+  x = fmaxf(x, dpp_f<0x128>(x));
+  const int ninf = __builtin_bit_cast(int, -INFINITY);
+  x = fmaxf(x, __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(ninf, __builtin_bit_cast(int, x), 0x142, 0xA, 0xF, false)));
+  x = fmaxf(x, __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(ninf, __builtin_bit_cast(int, x), 0x143, 0xC, 0xF, false)));
+  return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, x), 63));
+}
+
 struct RecArgs {
   const float* obs;   // (B,T,N) emissions
   const float* mat;   // (N,N) log transition matrix
@@ -68,7 +81,17 @@ struct RecArgs {
   float* ls;          // (B,T) log-scales (FB) or null
   float* loglik;      // (B) sequence log-likelihood (FB alpha) or null
   int B, T, N, obs_mode, row_stride;
+  const BandDesc* band;  // banded decomposition (band.h) or null: dense chain
 };
+
+// the banded chain serves a chain iff band_prep measured a narrow enough window; returns
+// the padded window width (2 / 4 / 8) or 0 for the dense chain
+template <int KIND>
+__device__ __forceinline__ int rec_band_width(const RecArgs& a) {
+  if (!a.band) return 0;
+  const int W = KIND == kFbBeta ? a.band->wr : a.band->wc;
+  return W <= kBandMax ? (KIND == kFbBeta ? a.band->wrp : a.band->wcp) : 0;
+}
 
 template <int KIND>
 __device__ __forceinline__ int rec_tau(int q, int T) {
@@ -347,6 +370,182 @@ __device__ __forceinline__ void rec_run(const RecArgs& a, float* lds, int b) {
   if (KIND == kFbAlpha && a.loglik && tid == C::NT - 64) {
     // loglik = LS_{T-1} + log c_{T-1}; `base` (wave NW-1) now holds LS_{T-1}
     a.loglik[b] = (float)(base + (double)__logf(lds[C::OFF_SC + ((T - 1) & (C::RING - 1))]));
+  }
+}
+
+// ---------------------------------------------------------------------------------------
+// Banded chain (band.h).  Wave 0 runs the whole recursion; lane l owns states
+// s = 64*blk + l.  Per step: the previous row goes to the LDS ring (it is both the window
+// source and the row that is flushed), one DPP wave reduction (sum / weighted sum / max)
+// runs beside the W window reads, then W fma / add+max per state.  No s_barrier inside the
+// 16-step block: LDS accesses of one wave complete in order.  Waves 1..NW-1 are helpers:
+// during block kb they stage the emissions of block kb+1 (log / +1e-8 transform included),
+// issue the global loads of block kb+2 and flush the rows and log-scales of block kb-2, so
+// the chain wave issues no global memory operation and no transcendental of the staging.
+// All waves meet at one s_barrier per 16 steps.
+template <int NP, int KIND, int WP>
+__device__ __forceinline__ void rec_band(const RecArgs& a, float* lds, int b, const BandDesc* __restrict__ d) {
+  using C = RC<NP>;
+  constexpr int NB = C::NBLK;
+  constexpr int NH = C::NW - 1;  // helper waves
+  constexpr int HV = (C::NW + NH - 1) / NH;  // virtual staging waves per helper
+  constexpr bool FB = KIND != kVit;
+  const int tid = threadIdx.x;
+  const int w = tid >> 6, l = tid & 63;
+  const int T = a.T, N = a.N;
+  const int nblocks = (T + 15) / 16;
+  double base = 0.0;
+
+  // prologue: every wave stages its column group of block 0 and loads block 1
+  {
+    float er[4];
+    rec_load<NP, KIND>(a, b, 0, w, l, er);
+    rec_stage<NP, KIND>(a, lds, 0, w, l, er);
+  }
+  float er0[HV][4], er1[HV][4];
+  if (w > 0) {
+#pragma unroll
+    for (int h = 0; h < HV; ++h) {
+      const int vw = (w - 1) + h * NH;
+      if (vw < C::NW && nblocks > 1) rec_load<NP, KIND>(a, b, 1, vw, l, er1[h]);
+    }
+  }
+  lds_barrier();
+
+  if (w == 0) {
+    // ------------------------------------------------------------------ chain wave
+    int lo[NB];
+    float wv[NB][WP], fl[NB];
+#pragma unroll
+    for (int blk = 0; blk < NB; ++blk) {
+      const int s = 64 * blk + l;
+      lo[blk] = KIND == kFbBeta ? d->rlo[s] : d->clo[s];
+#pragma unroll
+      for (int k = 0; k < WP; ++k)
+        wv[blk][k] = KIND == kVit ? d->cL[s][k] : (KIND == kFbAlpha ? d->cD[s][k] : d->rD[s][k]);
+      fl[blk] = KIND == kVit ? d->rfl[s] : d->afl[s];
+    }
+    auto emis = [&](int rho, int idx) { return lds[C::OFF_EMIS + (((rho >> 4) % 3) * 16 + (rho & 15)) * NP + idx]; };
+    float y[NB];
+#pragma unroll
+    for (int blk = 0; blk < NB; ++blk) {
+      const int s = 64 * blk + l;
+      const int ss = s < N ? s : 0;
+      if (KIND == kFbAlpha) y[blk] = s < N ? __expf(a.init[ss]) * emis(0, s) : 0.f;
+      else if (KIND == kFbBeta) y[blk] = s < N ? 1.f : 0.f;
+      else y[blk] = s < N ? a.init[ss] + emis(0, s) : -INFINITY;
+    }
+    float* ybuf = lds + C::OFF_PART;  // beta's window source [2][NP]
+    for (int kb = 0; kb < nblocks; ++kb) {
+      const int q0 = kb * 16 < 1 ? 1 : kb * 16;
+      const int q1 = (kb + 1) * 16 < T ? (kb + 1) * 16 : T;
+      for (int q = q0; q < q1; ++q) {
+        float* row = lds + C::OFF_RING + ((q - 1) & (C::RING - 1)) * NP;
+#pragma unroll
+        for (int blk = 0; blk < NB; ++blk) row[64 * blk + l] = y[blk];
+        float eo[NB];
+#pragma unroll
+        for (int blk = 0; blk < NB; ++blk) eo[blk] = emis(q, 64 * blk + l);
+        const float* src = row;
+        float red, cs = 0.f;
+        float win[NB][WP];
+        if (KIND == kFbBeta) {  // y = v * e_{q-1} is the product input (hmm.py:113-115)
+          float* yb = ybuf + ((q - 1) & 1) * NP;
+          float t = 0.f;
+#pragma unroll
+          for (int blk = 0; blk < NB; ++blk) {
+            const float yy = y[blk] * emis(q - 1, 64 * blk + l);
+            yb[64 * blk + l] = yy;
+            t += yy;
+          }
+          src = yb;
+#pragma unroll
+          for (int blk = 0; blk < NB; ++blk)
+#pragma unroll
+            for (int k = 0; k < WP; ++k) win[blk][k] = src[lo[blk] + k];
+          cs = wave_sum_bcast(t);
+          red = cs;
+        } else if (KIND == kFbAlpha) {
+#pragma unroll
+          for (int blk = 0; blk < NB; ++blk)
+#pragma unroll
+            for (int k = 0; k < WP; ++k) win[blk][k] = src[lo[blk] + k];
+          float t = 0.f, tw = 0.f;
+#pragma unroll
+          for (int blk = 0; blk < NB; ++blk) { t += y[blk]; tw = fmaf(y[blk], fl[blk], tw); }
+          cs = wave_sum_bcast(t);
+          red = wave_sum_bcast(tw);
+        } else {
+#pragma unroll
+          for (int blk = 0; blk < NB; ++blk)
+#pragma unroll
+            for (int k = 0; k < WP; ++k) win[blk][k] = src[lo[blk] + k];
+          float g = -INFINITY;
+#pragma unroll
+          for (int blk = 0; blk < NB; ++blk) g = fmaxf(g, y[blk] + fl[blk]);
+          red = wave_max_bcast(g);
+        }
+        float scale = 1.f;
+        if (FB) {
+          scale = __builtin_amdgcn_rcpf(cs);
+          if (l == 0) lds[C::OFF_SC + ((q - 1) & (C::RING - 1))] = cs;
+        }
+#pragma unroll
+        for (int blk = 0; blk < NB; ++blk) {
+          const int s = 64 * blk + l;
+          float acc = KIND == kFbBeta ? fl[blk] * red : red;
+#pragma unroll
+          for (int k = 0; k < WP; ++k) {
+            if (FB) acc = fmaf(win[blk][k], wv[blk][k], acc);
+            else acc = fmaxf(acc, win[blk][k] + wv[blk][k]);
+          }
+          if (KIND == kFbAlpha) y[blk] = s < N ? acc * (scale * eo[blk]) : 0.f;
+          else if (KIND == kFbBeta) y[blk] = s < N ? acc * scale : 0.f;
+          else y[blk] = acc + eo[blk];  // eo = -inf on padded states
+        }
+      }
+      lds_barrier();  // B_{kb+1}: block kb+1 staged by the helpers, rows of block kb-1 written
+    }
+    float* row = lds + C::OFF_RING + ((T - 1) & (C::RING - 1)) * NP;
+#pragma unroll
+    for (int blk = 0; blk < NB; ++blk) row[64 * blk + l] = y[blk];
+    if (KIND == kFbAlpha && a.loglik) {
+      float t = 0.f;
+#pragma unroll
+      for (int blk = 0; blk < NB; ++blk) t += y[blk];
+      const float cs = wave_sum_bcast(t);
+      if (l == 0) lds[C::OFF_SC + ((T - 1) & (C::RING - 1))] = cs;
+    }
+    lds_barrier();
+  } else {
+    // ---------------------------------------------------------------- helper waves
+    auto block_work = [&](int kb, float(&ernext)[HV][4], float(&erfree)[HV][4]) {
+#pragma unroll
+      for (int h = 0; h < HV; ++h) {
+        const int vw = (w - 1) + h * NH;
+        if (vw < C::NW) {
+          if (kb + 1 < nblocks) rec_stage<NP, KIND>(a, lds, kb + 1, vw, l, ernext[h]);
+          if (kb + 2 < nblocks) rec_load<NP, KIND>(a, b, kb + 2, vw, l, erfree[h]);
+          if (kb >= 2) rec_flush<NP, KIND>(a, lds, b, kb - 2, l + 64 * vw, base);
+        }
+      }
+      lds_barrier();
+    };
+    for (int kb = 0; kb < nblocks; kb += 2) {
+      block_work(kb, er1, er0);
+      if (kb + 1 < nblocks) block_work(kb + 1, er0, er1);
+    }
+    lds_barrier();  // the chain's last row and c_{T-1}
+#pragma unroll
+    for (int h = 0; h < HV; ++h) {
+      const int vw = (w - 1) + h * NH;
+      if (vw < C::NW) {
+        if (nblocks >= 2) rec_flush<NP, KIND>(a, lds, b, nblocks - 2, l + 64 * vw, base);
+        rec_flush<NP, KIND>(a, lds, b, nblocks - 1, l + 64 * vw, base);
+        if (KIND == kFbAlpha && a.loglik && vw == C::NW - 1 && l == 0)
+          a.loglik[b] = (float)(base + (double)__logf(lds[C::OFF_SC + ((T - 1) & (C::RING - 1))]));
+      }
+    }
   }
 }
 

@@ -52,12 +52,91 @@ struct VitArgs {
   uint8_t* psi;          // (B,T,NP) workspace
   uint8_t* G;            // (B,nchunks,NP) workspace
   int B, T, N, obs_mode, nchunks;
+  const BandDesc* band;  // banded decomposition (band.h) or null
 };
 
 template <int NP>
 __global__ void __launch_bounds__(RC<NP>::NT) vit_fwd_kernel(RecArgs ra) {
   extern __shared__ __attribute__((aligned(16))) float lds[];
-  rec_run<NP, kVit>(ra, lds, blockIdx.x);
+  switch (rec_band_width<kVit>(ra)) {
+    case 2: rec_band<NP, kVit, 2>(ra, lds, blockIdx.x, ra.band); break;
+    case 4: rec_band<NP, kVit, 4>(ra, lds, blockIdx.x, ra.band); break;
+    case 8: rec_band<NP, kVit, 8>(ra, lds, blockIdx.x, ra.band); break;
+    default: rec_run<NP, kVit>(ra, lds, blockIdx.x); break;
+  }
+}
+
+// psi rows of one chunk -> HBM, and the chunk map G[j] = state at t_lo - 1 given j at t_hi
+template <int NP>
+__device__ __forceinline__ void psi_write_rows(const VitArgs& a, uint8_t (*prow)[NP], int b, int chunk, int t_lo,
+                                               int t_hi) {
+  using C = VF<NP>;
+  const int tid = threadIdx.x;
+  const int T = a.T, N = a.N;
+  const int rows = t_hi - t_lo + 1;
+  uint8_t* pdst = a.psi + ((size_t)b * T + t_lo) * NP;
+  for (int idx = tid; idx < rows * NP / 16; idx += C::NT) {
+    const int row = idx / (NP / 16), c16 = (idx % (NP / 16)) * 16;
+    *reinterpret_cast<uint4*>(pdst + (size_t)row * NP + c16) = *reinterpret_cast<const uint4*>(&prow[row][c16]);
+  }
+  // chunk map: G[j] = state at t_lo - 1 given state j at t_hi
+  if (chunk > 0 && tid < NP) {
+    int s = tid < N ? tid : 0;
+    for (int t = t_hi; t > t_lo; --t) s = prow[t - t_lo][s];
+    a.G[((size_t)b * a.nchunks + chunk) * NP + tid] = prow[0][s];
+  }
+}
+
+// Banded psi rows (band.h): psi_t[o] = first argmax_i fl(delta_{t-1,i} + L[i][o]).  With
+// g_i = fl(delta_{t-1,i} + r_i), M = max_i g_i and i1 its first index, the maximum is
+// v = max(M, window values) and its first index is min({i1 if M == v} U {window i with
+// value == v}): an index outside the window has value g_i, and no g_j == M precedes i1;
+// i1 itself attains v whenever M == v (inside the window its value is >= g_i1 = M = v).
+template <int NP>
+__device__ __forceinline__ void psi_band_rows(const VitArgs& a, uint8_t (*prow)[NP], float* rowM, int* rowI,
+                                              int b, int t_lo, int t_hi) {
+  using C = VF<NP>;
+  const BandDesc* __restrict__ d = a.band;
+  const int tid = threadIdx.x, w = tid >> 6, l = tid & 63;
+  const int T = a.T, N = a.N, W = d->wcp;
+  const float* dbase = a.delta + (size_t)b * T * N;
+  const int t_first = t_lo > 0 ? t_lo : 1;
+  for (int t = t_first + w; t <= t_hi; t += C::NW) {
+    float bv = -INFINITY;
+    int bi = 0x7fffffff;
+#pragma unroll
+    for (int blk = 0; blk < C::NBLK; ++blk) {
+      const int i = 64 * blk + l;
+      const bool ok = i < N;
+      const float g = dbase[(size_t)(t - 1) * N + (ok ? i : 0)] + d->rfl[i];
+      if (ok) argmax_combine(bv, bi, g, i);
+    }
+    wave_argmax(bv, bi);
+    if (l == 0) { rowM[t - t_lo] = bv; rowI[t - t_lo] = bi; }
+  }
+  __syncthreads();
+  const int rows = t_hi - t_first + 1;
+  for (int idx = tid; idx < rows * NP; idx += C::NT) {
+    const int t = t_first + idx / NP, o = idx % NP;
+    int arg = 0;
+    if (o < N) {
+      const float M = rowM[t - t_lo];
+      const int lo = d->clo[o];
+      const float* drow = dbase + (size_t)(t - 1) * N + lo;
+      float v = M;
+      float val[kBandMax];
+#pragma unroll
+      for (int k = 0; k < kBandMax; ++k) {
+        val[k] = (k < W && lo + k < N) ? drow[k] + d->cL[o][k] : -INFINITY;
+        v = fmaxf(v, val[k]);
+      }
+      arg = M == v ? rowI[t - t_lo] : 0x7fffffff;
+#pragma unroll
+      for (int k = 0; k < kBandMax; ++k)
+        if (k < W && val[k] == v && lo + k < arg) arg = lo + k;
+    }
+    prow[t - t_lo][o] = (uint8_t)arg;
+  }
 }
 
 // ---------------------------------------------------------------------------- psi
@@ -84,6 +163,14 @@ __global__ void __launch_bounds__(VF<NP>::NT) vit_psi_kernel(VitArgs a) {
       M[blk][n] = ok ? v : -INFINITY;
     }
   if (t_lo == 0 && tid < NP) prow[0][tid] = 0;  // psi_0 (hmm.py:156 zeros)
+  if (a.band && a.band->wc <= kBandMax) {
+    __shared__ float rowM[kChunk];
+    __shared__ int rowI[kChunk];
+    psi_band_rows<NP>(a, prow, rowM, rowI, b, t_lo, t_hi);
+    __syncthreads();
+    psi_write_rows<NP>(a, prow, b, chunk, t_lo, t_hi);
+    return;
+  }
 
   const float* dbase = a.delta + (size_t)b * T * N;
   auto load_row = [&](int t, float(&yv)[C::NBLK]) {
@@ -136,19 +223,7 @@ __global__ void __launch_bounds__(VF<NP>::NT) vit_psi_kernel(VitArgs a) {
     for (int blk = 0; blk < C::NBLK; ++blk) ycur[blk] = ynext[blk];
   }
   __syncthreads();
-  // write psi rows (16 B per thread-iteration)
-  const int rows = t_hi - t_lo + 1;
-  uint8_t* pdst = a.psi + ((size_t)b * T + t_lo) * NP;
-  for (int idx = tid; idx < rows * NP / 16; idx += C::NT) {
-    const int row = idx / (NP / 16), c16 = (idx % (NP / 16)) * 16;
-    *reinterpret_cast<uint4*>(pdst + (size_t)row * NP + c16) = *reinterpret_cast<const uint4*>(&prow[row][c16]);
-  }
-  // chunk map: G[j] = state at t_lo - 1 given state j at t_hi
-  if (chunk > 0 && tid < NP) {
-    int s = tid < N ? tid : 0;
-    for (int t = t_hi; t > t_lo; --t) s = prow[t - t_lo][s];
-    a.G[((size_t)b * a.nchunks + chunk) * NP + tid] = prow[0][s];
-  }
+  psi_write_rows<NP>(a, prow, b, chunk, t_lo, t_hi);
 }
 
 // ----------------------------------------------------------------------- backtrace
@@ -212,7 +287,11 @@ template <int NP>
 static hipError_t launch_vit(const VitArgs& va, hipStream_t sm) {
   hipError_t e = allow_lds(vit_fwd_kernel<NP>, kExclusiveLds);  // own the CU (recur.h)
   if (e != hipSuccess) return e;
-  RecArgs ra{va.obs, va.log_P, va.init, va.delta, nullptr, nullptr, va.B, va.T, va.N, va.obs_mode, va.N};
+  if (va.band) {
+    e = launch_band_prep(va.log_P, va.N, const_cast<BandDesc*>(va.band), sm);
+    if (e != hipSuccess) return e;
+  }
+  RecArgs ra{va.obs, va.log_P, va.init, va.delta, nullptr, nullptr, va.B, va.T, va.N, va.obs_mode, va.N, va.band};
   hipLaunchKernelGGL(vit_fwd_kernel<NP>, dim3(va.B), dim3(RC<NP>::NT), kExclusiveLds, sm, ra);
   e = hipGetLastError();
   if (e != hipSuccess) return e;
@@ -231,7 +310,7 @@ HMM355_API size_t hmm355_viterbi_workspace_bytes(int B, int T, int N) {
   if (B < 0 || T < 1 || N < 1 || N > 256) return 0;
   const size_t NP = pad_states(N);
   const size_t nc = (T + kChunk - 1) / kChunk;
-  return align_up((size_t)B * T * NP, 256) + align_up((size_t)B * nc * NP, 256);
+  return align_up((size_t)B * T * NP, 256) + align_up((size_t)B * nc * NP, 256) + align_up(sizeof(BandDesc), 256);
 }
 
 HMM355_API int hmm355_viterbi_f32(const float* obs, int obs_mode, const float* log_P, const float* init, int B,
@@ -249,7 +328,8 @@ HMM355_API int hmm355_viterbi_f32(const float* obs, int obs_mode, const float* l
   const int nc = (T + kChunk - 1) / kChunk;
   uint8_t* psi = static_cast<uint8_t*>(workspace);
   uint8_t* G = psi + align_up((size_t)B * T * NP, 256);
-  VitArgs va{obs, log_P, init, log_delta, final_score, states, psi, G, B, T, N, obs_mode, nc};
+  BandDesc* band = use_band() ? reinterpret_cast<BandDesc*>(G + align_up((size_t)B * nc * NP, 256)) : nullptr;
+  VitArgs va{obs, log_P, init, log_delta, final_score, states, psi, G, B, T, N, obs_mode, nc, band};
   hipStream_t sm = static_cast<hipStream_t>(stream);
   hipError_t e;
   switch (NP) {
