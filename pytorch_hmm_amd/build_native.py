@@ -5,6 +5,7 @@
 The shared library lands in pytorch_hmm_amd/lib/ so it travels with the repository
 snapshot to the GPU box (it is git-ignored, not gpurun-ignored).
 """
+import glob
 import os
 import subprocess
 import sys
@@ -33,8 +34,9 @@ def build(force=False, verbose=False, defines=(), out=None):
     lib = out or LIB
     os.makedirs(os.path.dirname(lib), exist_ok=True)
     srcs = [s for s in SOURCES if os.path.exists(os.path.join(CSRC, s))]
-    deps = [os.path.join(CSRC, s) for s in srcs] + [os.path.join(CSRC, "common.h"),
-                                                    os.path.join(HERE, "..", "include", "hmm355.h")]
+    # every header the sources include (csrc/*.h and the public header) is a dependency
+    deps = ([os.path.join(CSRC, s) for s in srcs] + sorted(glob.glob(os.path.join(CSRC, "*.h"))) +
+            [os.path.join(HERE, "..", "include", "hmm355.h"), os.path.abspath(__file__)])
     if not force and os.path.exists(lib):
         lt = os.path.getmtime(lib)
         if all(os.path.getmtime(d) <= lt for d in deps if os.path.exists(d)):

@@ -26,21 +26,10 @@ template <int NP>
 __global__ void __launch_bounds__(RC<NP>::NT) fb_recur_kernel(RecArgs fa, RecArgs fb) {
   extern __shared__ __attribute__((aligned(16))) float lds[];
   const int b = blockIdx.x >> 1;
-  if (blockIdx.x & 1) {
-    switch (rec_band_width<kFbBeta>(fb)) {
-      case 2: rec_band<NP, kFbBeta, 2>(fb, lds, b, fb.band); break;
-      case 4: rec_band<NP, kFbBeta, 4>(fb, lds, b, fb.band); break;
-      case 8: rec_band<NP, kFbBeta, 8>(fb, lds, b, fb.band); break;
-      default: rec_run<NP, kFbBeta>(fb, lds, b); break;
-    }
-  } else {
-    switch (rec_band_width<kFbAlpha>(fa)) {
-      case 2: rec_band<NP, kFbAlpha, 2>(fa, lds, b, fa.band); break;
-      case 4: rec_band<NP, kFbAlpha, 4>(fa, lds, b, fa.band); break;
-      case 8: rec_band<NP, kFbAlpha, 8>(fa, lds, b, fa.band); break;
-      default: rec_run<NP, kFbAlpha>(fa, lds, b); break;
-    }
-  }
+  if (blockIdx.x & 1)
+    rec_dispatch<NP, kFbBeta>(fb, lds, b);
+  else
+    rec_dispatch<NP, kFbAlpha>(fa, lds, b);
 }
 
 struct PostArgs {

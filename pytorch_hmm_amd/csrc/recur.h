@@ -47,8 +47,9 @@ struct RC {
   static constexpr int OFF_PART = 0;                       // [2][NP][2] half-wave partials
   static constexpr int OFF_EMIS = OFF_PART + 2 * NP * 2;   // [3][16][NP]
   static constexpr int OFF_RING = OFF_EMIS + 3 * 16 * NP;  // [RING][NP]
-  static constexpr int OFF_SC = OFF_RING + RING * NP;      // [RING] normalisers c_rho
-  static constexpr int LDS_FLOATS = OFF_SC + RING;
+  static constexpr int OFF_SC = OFF_RING + RING * NP;      // [RING][64] normalisers c_rho (entry 0;
+                                                           // the banded chain writes all 64 lanes)
+  static constexpr int LDS_FLOATS = OFF_SC + RING * 64;
   static_assert(LDS_FLOATS * 4 <= kExclusiveLds, "LDS layout too large");
 };
 
@@ -56,8 +57,9 @@ struct RC {
 // from lane 63: wave-uniform.
 __device__ __forceinline__ float wave_sum_bcast(float x) {
   x = row16_sum(x);
-  x += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, x), 0x142, 0xA, 0xF, false));
-  x += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, x), 0x143, 0xC, 0xF, false));
+  // row_bcast:15 / :31 folded into the add; rows outside the mask keep x (one instruction each)
+  asm("s_nop 1\n\tv_add_f32_dpp %0, %0, %0 row_bcast:15 row_mask:0xa bank_mask:0xf" : "+v"(x));
+  asm("s_nop 1\n\tv_add_f32_dpp %0, %0, %0 row_bcast:31 row_mask:0xc bank_mask:0xf" : "+v"(x));
   return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, x), 63));
 }
 
@@ -67,10 +69,103 @@ __device__ __forceinline__ float wave_max_bcast(float x) {
   x = fmaxf(x, dpp_f<0x4E>(x));
   x = fmaxf(x, dpp_f<0x124>(x));
   x = fmaxf(x, dpp_f<0x128>(x));
-  const int ninf = __builtin_bit_cast(int, -INFINITY);
-  x = fmaxf(x, __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(ninf, __builtin_bit_cast(int, x), 0x142, 0xA, 0xF, false)));
-  x = fmaxf(x, __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(ninf, __builtin_bit_cast(int, x), 0x143, 0xC, 0xF, false)));
+  asm("s_nop 1\n\tv_max_f32_dpp %0, %0, %0 row_bcast:15 row_mask:0xa bank_mask:0xf" : "+v"(x));
+  asm("s_nop 1\n\tv_max_f32_dpp %0, %0, %0 row_bcast:31 row_mask:0xc bank_mask:0xf" : "+v"(x));
   return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, x), 63));
+}
+
+// ---- one-instruction shifted window terms (DPP on src0; a lane whose DPP source falls off
+// the 64-lane wave is disabled and keeps the destination's previous value)
+#define HMM355_DPP_OP(name, op, ctrl)                                                         \
+  __device__ __forceinline__ void name(float& dst, float src, float w) {                      \
+    asm("s_nop 1\n\t" op " %0, %1, %2 " ctrl " row_mask:0xf bank_mask:0xf" : "+v"(dst) : "v"(src), "v"(w)); \
+  }
+HMM355_DPP_OP(dpp_add_shr1, "v_add_f32_dpp", "wave_shr:1")    // dst = src[l-1] + w  (lane 0 keeps)
+HMM355_DPP_OP(dpp_add_shl1, "v_add_f32_dpp", "wave_shl:1")    // dst = src[l+1] + w  (lane 63 keeps)
+HMM355_DPP_OP(dpp_add_ror1, "v_add_f32_dpp", "wave_ror:1")    // dst = src[l-1 mod 64] + w
+HMM355_DPP_OP(dpp_add_rol1, "v_add_f32_dpp", "wave_rol:1")    // dst = src[l+1 mod 64] + w
+HMM355_DPP_OP(dpp_mul_shr1, "v_mul_f32_dpp", "wave_shr:1")
+HMM355_DPP_OP(dpp_mul_shl1, "v_mul_f32_dpp", "wave_shl:1")
+HMM355_DPP_OP(dpp_mul_ror1, "v_mul_f32_dpp", "wave_ror:1")
+HMM355_DPP_OP(dpp_mul_rol1, "v_mul_f32_dpp", "wave_rol:1")
+HMM355_DPP_OP(dpp_fmac_shr1, "v_fmac_f32_dpp", "wave_shr:1")  // dst += src[l-1] * w (lane 0 keeps)
+HMM355_DPP_OP(dpp_fmac_shl1, "v_fmac_f32_dpp", "wave_shl:1")  // dst += src[l+1] * w (lane 63 keeps)
+#undef HMM355_DPP_OP
+
+// Window term of slot offset DD in {-1, +1} for state vector v (state 64*blk + lane), weights
+// w: Viterbi -> t = v(s + DD) + w (neutral -inf past the ends); FB -> acc += v(s + DD) * w.
+template <int NB, bool FB, int DD>
+__device__ __forceinline__ void win_term1(const float (&v)[NB], const float (&w)[NB], float (&acc)[NB]) {
+#pragma unroll
+  for (int blk = 0; blk < NB; ++blk) {
+    const bool edge = DD < 0 ? blk == 0 : blk == NB - 1;  // no neighbouring block
+    if (FB) {
+      if (edge) {
+        if (DD < 0) dpp_fmac_shr1(acc[blk], v[blk], w[blk]);
+        else dpp_fmac_shl1(acc[blk], v[blk], w[blk]);
+      } else {
+        float t;
+        if (DD < 0) { dpp_mul_ror1(t, v[blk - 1], w[blk]); dpp_mul_shr1(t, v[blk], w[blk]); }
+        else { dpp_mul_rol1(t, v[blk + 1], w[blk]); dpp_mul_shl1(t, v[blk], w[blk]); }
+        acc[blk] += t;
+      }
+    } else {
+      float t = -INFINITY;
+      if (!edge) {
+        if (DD < 0) dpp_add_ror1(t, v[blk - 1], w[blk]);
+        else dpp_add_rol1(t, v[blk + 1], w[blk]);
+      }
+      if (DD < 0) dpp_add_shr1(t, v[blk], w[blk]);
+      else dpp_add_shl1(t, v[blk], w[blk]);
+      acc[blk] = fmaxf(acc[blk], t);
+    }
+  }
+}
+
+// Whole-vector lane shifts of a state vector held as v[blk] = state 64*blk + lane (DPP
+// wave_shr:1 / wave_shl:1; the lane that falls off a 64-block takes the neighbouring block's
+// edge value through wave_ror:1 / wave_rol:1 passed as the DPP "old" operand).
+// out(s) = v(s - 1) (shr) or v(s + 1) (shl); states outside [0, NB*64) read `edge`.
+template <int NB>
+__device__ __forceinline__ void vec_shr1(const float (&v)[NB], float (&out)[NB], float edge) {
+#pragma unroll
+  for (int blk = NB - 1; blk >= 0; --blk) {
+    const int carry = blk > 0 ? __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v[blk - 1]), 0x13C, 0xF, 0xF, false)
+                              : __builtin_bit_cast(int, edge);
+    out[blk] = __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(carry, __builtin_bit_cast(int, v[blk]), 0x138, 0xF, 0xF, false));
+  }
+}
+template <int NB>
+__device__ __forceinline__ void vec_shl1(const float (&v)[NB], float (&out)[NB], float edge) {
+#pragma unroll
+  for (int blk = 0; blk < NB; ++blk) {
+    const int carry = blk < NB - 1 ? __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v[blk + 1]), 0x134, 0xF, 0xF, false)
+                                   : __builtin_bit_cast(int, edge);
+    out[blk] = __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(carry, __builtin_bit_cast(int, v[blk]), 0x130, 0xF, 0xF, false));
+  }
+}
+// window slots k = 0..TW-1 <-> states s + TD0 + k, from registers
+template <int NB, int TD0, int TW>
+__device__ __forceinline__ void vec_window(const float (&v)[NB], float (&win)[NB][TW > 0 ? TW : 1], float edge) {
+  float neg[3][NB], pos[3][NB];
+  // negative offsets: successive right shifts; positive: successive left shifts
+  if constexpr (TD0 < 0) {
+    vec_shr1<NB>(v, neg[0], edge);
+    if constexpr (TD0 < -1) vec_shr1<NB>(neg[0], neg[1], edge);
+    if constexpr (TD0 < -2) vec_shr1<NB>(neg[1], neg[2], edge);
+  }
+  if constexpr (TD0 + TW - 1 > 0) {
+    vec_shl1<NB>(v, pos[0], edge);
+    if constexpr (TD0 + TW - 1 > 1) vec_shl1<NB>(pos[0], pos[1], edge);
+    if constexpr (TD0 + TW - 1 > 2) vec_shl1<NB>(pos[1], pos[2], edge);
+  }
+#pragma unroll
+  for (int k = 0; k < TW; ++k) {
+    const int dd = TD0 + k;
+#pragma unroll
+    for (int blk = 0; blk < NB; ++blk)
+      win[blk][k] = dd == 0 ? v[blk] : (dd < 0 ? neg[-dd - 1][blk] : pos[dd - 1][blk]);
+  }
 }
 
 struct RecArgs {
@@ -83,15 +178,6 @@ struct RecArgs {
   int B, T, N, obs_mode, row_stride;
   const BandDesc* band;  // banded decomposition (band.h) or null: dense chain
 };
-
-// the banded chain serves a chain iff band_prep measured a narrow enough window; returns
-// the padded window width (2 / 4 / 8) or 0 for the dense chain
-template <int KIND>
-__device__ __forceinline__ int rec_band_width(const RecArgs& a) {
-  if (!a.band) return 0;
-  const int W = KIND == kFbBeta ? a.band->wr : a.band->wc;
-  return W <= kBandMax ? (KIND == kFbBeta ? a.band->wrp : a.band->wcp) : 0;
-}
 
 template <int KIND>
 __device__ __forceinline__ int rec_tau(int q, int T) {
@@ -158,7 +244,7 @@ __device__ __forceinline__ void rec_flush(const RecArgs& a, const float* lds, in
     // LS_rho = LS_{rho-1} + log c_{rho-1}: 16-lane inclusive scan, running base in double
     const int j = tid & 15, lane = tid & 63;
     const int rho = q_base + j;
-    float x = (lane < 16 && rho >= 1 && rho < a.T) ? __logf(lds[C::OFF_SC + ((rho - 1) & (C::RING - 1))]) : 0.f;
+    float x = (lane < 16 && rho >= 1 && rho < a.T) ? __logf(lds[C::OFF_SC + 64 * ((rho - 1) & (C::RING - 1))]) : 0.f;
     x += dpp_f<0x111>(x);  // row_shr:1
     x += dpp_f<0x112>(x);  // row_shr:2
     x += dpp_f<0x114>(x);  // row_shr:4
@@ -311,7 +397,7 @@ __device__ __forceinline__ void rec_run(const RecArgs& a, float* lds, int b) {
           __builtin_amdgcn_sched_barrier(0);
         }
         const float scale = __builtin_amdgcn_rcpf(cs);
-        if (tid == 0) lds[C::OFF_SC + ((q - 1) & (C::RING - 1))] = cs;
+        if (tid == 0) lds[C::OFF_SC + 64 * ((q - 1) & (C::RING - 1))] = cs;
         float h0 = (a0 + a1) + (a2 + a3), h1 = h0;
         permlane32_swap(h0, h1);  // rows {0,2} / {1,3} summed: lanes 0..31 hold both halves
         const float acc = h0 + h1;
@@ -362,14 +448,14 @@ __device__ __forceinline__ void rec_run(const RecArgs& a, float* lds, int b) {
 #pragma unroll
     for (int blk = 1; blk < C::NBLK; ++blk) ys += y[blk];
     const float cs = wave_sum_bcast(ys);
-    if (l == 0) lds[C::OFF_SC + ((T - 1) & (C::RING - 1))] = cs;  // c_{T-1} (loglik only)
+    if (l == 0) lds[C::OFF_SC + 64 * ((T - 1) & (C::RING - 1))] = cs;  // c_{T-1} (loglik only)
   }
   lds_barrier();
   if (nblocks >= 2) rec_flush<NP, KIND>(a, lds, b, nblocks - 2, tid, base);
   rec_flush<NP, KIND>(a, lds, b, nblocks - 1, tid, base);
   if (KIND == kFbAlpha && a.loglik && tid == C::NT - 64) {
     // loglik = LS_{T-1} + log c_{T-1}; `base` (wave NW-1) now holds LS_{T-1}
-    a.loglik[b] = (float)(base + (double)__logf(lds[C::OFF_SC + ((T - 1) & (C::RING - 1))]));
+    a.loglik[b] = (float)(base + (double)__logf(lds[C::OFF_SC + 64 * ((T - 1) & (C::RING - 1))]));
   }
 }
 
@@ -383,138 +469,202 @@ __device__ __forceinline__ void rec_run(const RecArgs& a, float* lds, int b) {
 // issue the global loads of block kb+2 and flush the rows and log-scales of block kb-2, so
 // the chain wave issues no global memory operation and no transcendental of the staging.
 // All waves meet at one s_barrier per 16 steps.
-template <int NP, int KIND, int WP>
+template <int NP, int KIND, int WP, int TD0 = 0, int TW = 0>
 __device__ __forceinline__ void rec_band(const RecArgs& a, float* lds, int b, const BandDesc* __restrict__ d) {
   using C = RC<NP>;
   constexpr int NB = C::NBLK;
-  constexpr int NH = C::NW - 1;  // helper waves
+  // Waves 1..3 are the helpers; waves 4.. exit at once, so the chain wave is alone on its
+  // SIMD (a workgroup's waves are spread over the 4 SIMDs) and no helper instruction
+  // competes with it for issue.  Ended waves do not take part in s_barrier.
+  constexpr int NH = 3;
   constexpr int HV = (C::NW + NH - 1) / NH;  // virtual staging waves per helper
   constexpr bool FB = KIND != kVit;
   const int tid = threadIdx.x;
   const int w = tid >> 6, l = tid & 63;
+  if (w > NH) return;
   const int T = a.T, N = a.N;
   const int nblocks = (T + 15) / 16;
   double base = 0.0;
 
-  // prologue: every wave stages its column group of block 0 and loads block 1
-  {
-    float er[4];
-    rec_load<NP, KIND>(a, b, 0, w, l, er);
-    rec_stage<NP, KIND>(a, lds, 0, w, l, er);
-  }
+  // prologue: the helpers stage block 0 and load block 1
   float er0[HV][4], er1[HV][4];
   if (w > 0) {
 #pragma unroll
     for (int h = 0; h < HV; ++h) {
       const int vw = (w - 1) + h * NH;
-      if (vw < C::NW && nblocks > 1) rec_load<NP, KIND>(a, b, 1, vw, l, er1[h]);
+      if (vw < C::NW) {
+        float er[4];
+        rec_load<NP, KIND>(a, b, 0, vw, l, er);
+        rec_stage<NP, KIND>(a, lds, 0, vw, l, er);
+        if (nblocks > 1) rec_load<NP, KIND>(a, b, 1, vw, l, er1[h]);
+      }
     }
   }
   lds_barrier();
 
   if (w == 0) {
     // ------------------------------------------------------------------ chain wave
+    // Lane l holds the consecutive states s = NB*l + j (j < NB): a window offset of +-1 is
+    // then another register of the same lane or ONE DPP lane shift (zero-filled at the wave
+    // edge, where the window weight is the neutral element), folded by the compiler into the
+    // add / fma that consumes it.  A wave issues one instruction per ~4 cycles, so the step is
+    // written for instruction count: 16-step blocks fully unrolled (no scalar address math),
+    // the emission read one step ahead, the block's normalisers collected by v_writelane and
+    // stored once per block.
+    constexpr int WW = TW > 0 ? TW : WP;  // window slots per state
     int lo[NB];
-    float wv[NB][WP], fl[NB];
+    float wv[NB][WW], fl[NB];
 #pragma unroll
-    for (int blk = 0; blk < NB; ++blk) {
-      const int s = 64 * blk + l;
-      lo[blk] = KIND == kFbBeta ? d->rlo[s] : d->clo[s];
+    for (int j = 0; j < NB; ++j) {
+      const int s = NB * l + j;
+      lo[j] = KIND == kFbBeta ? d->rlo[s] : d->clo[s];
 #pragma unroll
-      for (int k = 0; k < WP; ++k)
-        wv[blk][k] = KIND == kVit ? d->cL[s][k] : (KIND == kFbAlpha ? d->cD[s][k] : d->rD[s][k]);
-      fl[blk] = KIND == kVit ? d->rfl[s] : d->afl[s];
+      for (int k = 0; k < WW; ++k) {
+        if (TW > 0)
+          wv[j][k] = KIND == kVit ? d->tL[s][k] : (KIND == kFbAlpha ? d->tD[s][k] : d->tR[s][k]);
+        else
+          wv[j][k] = KIND == kVit ? d->cL[s][k] : (KIND == kFbAlpha ? d->cD[s][k] : d->rD[s][k]);
+      }
+      fl[j] = KIND == kVit ? d->rfl[s] : d->afl[s];
     }
-    auto emis = [&](int rho, int idx) { return lds[C::OFF_EMIS + (((rho >> 4) % 3) * 16 + (rho & 15)) * NP + idx]; };
+    const bool uafl = d->uafl != 0;  // one floor for every row: weighted sum = afl0 * plain sum
+    const float afl0 = d->afl[0];
+    auto erow = [&](int rho) { return lds + C::OFF_EMIS + (((rho >> 4) % 3) * 16 + (rho & 15)) * NP + NB * l; };
+    auto ld = [&](const float* p, float(&v)[NB]) {
+      if constexpr (NB == 1) v[0] = p[0];
+      else if constexpr (NB == 2) { const float2 t = *reinterpret_cast<const float2*>(p); v[0] = t.x; v[1] = t.y; }
+      else { const float4 t = *reinterpret_cast<const float4*>(p); v[0] = t.x; v[1] = t.y; v[2] = t.z; v[3] = t.w; }
+    };
+    auto st = [&](float* p, const float(&v)[NB]) {
+      if constexpr (NB == 1) p[0] = v[0];
+      else if constexpr (NB == 2) *reinterpret_cast<float2*>(p) = make_float2(v[0], v[1]);
+      else *reinterpret_cast<float4*>(p) = make_float4(v[0], v[1], v[2], v[3]);
+    };
     float y[NB];
+    {
+      float e0[NB];
+      ld(erow(0), e0);
 #pragma unroll
-    for (int blk = 0; blk < NB; ++blk) {
-      const int s = 64 * blk + l;
-      const int ss = s < N ? s : 0;
-      if (KIND == kFbAlpha) y[blk] = s < N ? __expf(a.init[ss]) * emis(0, s) : 0.f;
-      else if (KIND == kFbBeta) y[blk] = s < N ? 1.f : 0.f;
-      else y[blk] = s < N ? a.init[ss] + emis(0, s) : -INFINITY;
+      for (int j = 0; j < NB; ++j) {
+        const int s = NB * l + j;
+        const int ss = s < N ? s : 0;
+        if (KIND == kFbAlpha) y[j] = s < N ? __expf(a.init[ss]) * e0[j] : 0.f;
+        else if (KIND == kFbBeta) y[j] = s < N ? 1.f : 0.f;
+        else y[j] = s < N ? a.init[ss] + e0[j] : -INFINITY;
+      }
     }
-    float* ybuf = lds + C::OFF_PART;  // beta's window source [2][NP]
+    float* ybuf = lds + C::OFF_PART;  // beta's LDS window source [2][NP] (LDS-window mode)
+    constexpr int EL = KIND == kFbBeta ? 1 : 0;
+    float en[NB];  // the next step's emission (alpha / Viterbi e_q, beta e_{q-1})
+
+    // the value of state s + dd (s = NB*l + j) from register vector v
+    auto at = [&](const float(&v)[NB], int j, int dd) -> float {
+      const int t = j + dd + 4 * NB;
+      const int qq = t / NB - 4, jj = t % NB;
+      const int x = __builtin_bit_cast(int, v[jj]);
+      if (qq == 0) return v[jj];
+      if (qq == -1) return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, x, 0x138, 0xF, 0xF, true));
+      if (qq == 1) return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, x, 0x130, 0xF, 0xF, true));
+      if (qq == -2) {
+        const int t1 = __builtin_amdgcn_update_dpp(0, x, 0x138, 0xF, 0xF, true);
+        return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, t1, 0x138, 0xF, 0xF, true));
+      }
+      const int t1 = __builtin_amdgcn_update_dpp(0, x, 0x130, 0xF, 0xF, true);
+      return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, t1, 0x130, 0xF, 0xF, true));
+    };
+
+    auto step = [&](int q, int jj, bool last_in_block) {
+      float* row = lds + C::OFF_RING + ((q - 1) & (C::RING - 1)) * NP;
+      st(row + NB * l, y);  // row q-1: flushed by the helpers, window source in LDS mode
+      float eo[NB];
+#pragma unroll
+      for (int j = 0; j < NB; ++j) eo[j] = en[j];
+      if (!last_in_block) ld(erow(q + 1 - EL), en);
+      float acc[NB], src[NB];
+      float cs = 0.f, scale = 1.f;
+      if (KIND == kFbBeta) {  // the product input is y = v * e_{q-1} (hmm.py:113-115)
+        float t = 0.f;
+#pragma unroll
+        for (int j = 0; j < NB; ++j) { src[j] = y[j] * eo[j]; t += src[j]; }
+        if (TW == 0) st(ybuf + ((q - 1) & 1) * NP + NB * l, src);
+        cs = wave_sum_bcast(t);
+#pragma unroll
+        for (int j = 0; j < NB; ++j) acc[j] = fl[j] * cs;
+      } else if (KIND == kFbAlpha) {
+        float t = 0.f;
+#pragma unroll
+        for (int j = 0; j < NB; ++j) { src[j] = y[j]; t += y[j]; }
+        cs = wave_sum_bcast(t);
+        float sw;
+        if (uafl) {
+          sw = afl0 * cs;
+        } else {
+          float tw = 0.f;
+#pragma unroll
+          for (int j = 0; j < NB; ++j) tw = fmaf(y[j], fl[j], tw);
+          sw = wave_sum_bcast(tw);
+        }
+#pragma unroll
+        for (int j = 0; j < NB; ++j) acc[j] = sw;
+      } else {
+        float g = -INFINITY;
+#pragma unroll
+        for (int j = 0; j < NB; ++j) { src[j] = y[j]; g = fmaxf(g, y[j] + fl[j]); }
+        const float M = wave_max_bcast(g);
+#pragma unroll
+        for (int j = 0; j < NB; ++j) acc[j] = M;
+      }
+      if (FB) {
+        scale = __builtin_amdgcn_rcpf(cs);
+        lds[C::OFF_SC + 64 * ((q - 1) & (C::RING - 1)) + l] = cs;  // c_{q-1}: one conflict-free store
+      }
+      if constexpr (TW > 0) {
+#pragma unroll
+        for (int k = 0; k < TW; ++k)
+#pragma unroll
+          for (int j = 0; j < NB; ++j) {
+            const float v = at(src, j, TD0 + k);
+            acc[j] = FB ? fmaf(v, wv[j][k], acc[j]) : fmaxf(acc[j], v + wv[j][k]);
+          }
+      } else {
+        const float* wsrc = KIND == kFbBeta ? ybuf + ((q - 1) & 1) * NP : row;
+#pragma unroll
+        for (int j = 0; j < NB; ++j)
+#pragma unroll
+          for (int k = 0; k < WW; ++k) {
+            const float v = wsrc[lo[j] + k];
+            acc[j] = FB ? fmaf(v, wv[j][k], acc[j]) : fmaxf(acc[j], v + wv[j][k]);
+          }
+      }
+#pragma unroll
+      for (int j = 0; j < NB; ++j) {
+        // padded states: the staged emission is 0 (FB) / -inf (Viterbi) and the floors 0
+        if (KIND == kFbAlpha) y[j] = acc[j] * (scale * eo[j]);
+        else if (KIND == kFbBeta) y[j] = acc[j] * scale;
+        else y[j] = acc[j] + eo[j];
+      }
+    };
+
     for (int kb = 0; kb < nblocks; ++kb) {
       const int q0 = kb * 16 < 1 ? 1 : kb * 16;
       const int q1 = (kb + 1) * 16 < T ? (kb + 1) * 16 : T;
-      for (int q = q0; q < q1; ++q) {
-        float* row = lds + C::OFF_RING + ((q - 1) & (C::RING - 1)) * NP;
+      if (q0 < q1) ld(erow(q0 - EL), en);
+      if (q0 == kb * 16 && q1 == kb * 16 + 16) {
 #pragma unroll
-        for (int blk = 0; blk < NB; ++blk) row[64 * blk + l] = y[blk];
-        float eo[NB];
-#pragma unroll
-        for (int blk = 0; blk < NB; ++blk) eo[blk] = emis(q, 64 * blk + l);
-        const float* src = row;
-        float red, cs = 0.f;
-        float win[NB][WP];
-        if (KIND == kFbBeta) {  // y = v * e_{q-1} is the product input (hmm.py:113-115)
-          float* yb = ybuf + ((q - 1) & 1) * NP;
-          float t = 0.f;
-#pragma unroll
-          for (int blk = 0; blk < NB; ++blk) {
-            const float yy = y[blk] * emis(q - 1, 64 * blk + l);
-            yb[64 * blk + l] = yy;
-            t += yy;
-          }
-          src = yb;
-#pragma unroll
-          for (int blk = 0; blk < NB; ++blk)
-#pragma unroll
-            for (int k = 0; k < WP; ++k) win[blk][k] = src[lo[blk] + k];
-          cs = wave_sum_bcast(t);
-          red = cs;
-        } else if (KIND == kFbAlpha) {
-#pragma unroll
-          for (int blk = 0; blk < NB; ++blk)
-#pragma unroll
-            for (int k = 0; k < WP; ++k) win[blk][k] = src[lo[blk] + k];
-          float t = 0.f, tw = 0.f;
-#pragma unroll
-          for (int blk = 0; blk < NB; ++blk) { t += y[blk]; tw = fmaf(y[blk], fl[blk], tw); }
-          cs = wave_sum_bcast(t);
-          red = wave_sum_bcast(tw);
-        } else {
-#pragma unroll
-          for (int blk = 0; blk < NB; ++blk)
-#pragma unroll
-            for (int k = 0; k < WP; ++k) win[blk][k] = src[lo[blk] + k];
-          float g = -INFINITY;
-#pragma unroll
-          for (int blk = 0; blk < NB; ++blk) g = fmaxf(g, y[blk] + fl[blk]);
-          red = wave_max_bcast(g);
-        }
-        float scale = 1.f;
-        if (FB) {
-          scale = __builtin_amdgcn_rcpf(cs);
-          if (l == 0) lds[C::OFF_SC + ((q - 1) & (C::RING - 1))] = cs;
-        }
-#pragma unroll
-        for (int blk = 0; blk < NB; ++blk) {
-          const int s = 64 * blk + l;
-          float acc = KIND == kFbBeta ? fl[blk] * red : red;
-#pragma unroll
-          for (int k = 0; k < WP; ++k) {
-            if (FB) acc = fmaf(win[blk][k], wv[blk][k], acc);
-            else acc = fmaxf(acc, win[blk][k] + wv[blk][k]);
-          }
-          if (KIND == kFbAlpha) y[blk] = s < N ? acc * (scale * eo[blk]) : 0.f;
-          else if (KIND == kFbBeta) y[blk] = s < N ? acc * scale : 0.f;
-          else y[blk] = acc + eo[blk];  // eo = -inf on padded states
-        }
+        for (int jj = 0; jj < 16; ++jj) step(kb * 16 + jj, jj, jj == 15);
+      } else {
+        for (int q = q0; q < q1; ++q) step(q, q - kb * 16, q + 1 == q1);
       }
       lds_barrier();  // B_{kb+1}: block kb+1 staged by the helpers, rows of block kb-1 written
     }
     float* row = lds + C::OFF_RING + ((T - 1) & (C::RING - 1)) * NP;
-#pragma unroll
-    for (int blk = 0; blk < NB; ++blk) row[64 * blk + l] = y[blk];
+    st(row + NB * l, y);
     if (KIND == kFbAlpha && a.loglik) {
       float t = 0.f;
 #pragma unroll
-      for (int blk = 0; blk < NB; ++blk) t += y[blk];
+      for (int j = 0; j < NB; ++j) t += y[j];
       const float cs = wave_sum_bcast(t);
-      if (l == 0) lds[C::OFF_SC + ((T - 1) & (C::RING - 1))] = cs;
+      if (l == 0) lds[C::OFF_SC + 64 * ((T - 1) & (C::RING - 1))] = cs;
     }
     lds_barrier();
   } else {
@@ -524,9 +674,11 @@ __device__ __forceinline__ void rec_band(const RecArgs& a, float* lds, int b, co
       for (int h = 0; h < HV; ++h) {
         const int vw = (w - 1) + h * NH;
         if (vw < C::NW) {
-          if (kb + 1 < nblocks) rec_stage<NP, KIND>(a, lds, kb + 1, vw, l, ernext[h]);
-          if (kb + 2 < nblocks) rec_load<NP, KIND>(a, b, kb + 2, vw, l, erfree[h]);
-          if (kb >= 2) rec_flush<NP, KIND>(a, lds, b, kb - 2, l + 64 * vw, base);
+          if (!(kAbl & 64)) {
+            if (kb + 1 < nblocks) rec_stage<NP, KIND>(a, lds, kb + 1, vw, l, ernext[h]);
+            if (kb + 2 < nblocks) rec_load<NP, KIND>(a, b, kb + 2, vw, l, erfree[h]);
+          }
+          if (!(kAbl & 32) && kb >= 2) rec_flush<NP, KIND>(a, lds, b, kb - 2, l + 64 * vw, base);
         }
       }
       lds_barrier();
@@ -543,9 +695,47 @@ __device__ __forceinline__ void rec_band(const RecArgs& a, float* lds, int b, co
         if (nblocks >= 2) rec_flush<NP, KIND>(a, lds, b, nblocks - 2, l + 64 * vw, base);
         rec_flush<NP, KIND>(a, lds, b, nblocks - 1, l + 64 * vw, base);
         if (KIND == kFbAlpha && a.loglik && vw == C::NW - 1 && l == 0)
-          a.loglik[b] = (float)(base + (double)__logf(lds[C::OFF_SC + ((T - 1) & (C::RING - 1))]));
+          a.loglik[b] = (float)(base + (double)__logf(lds[C::OFF_SC + 64 * ((T - 1) & (C::RING - 1))]));
       }
     }
+  }
+}
+
+// Which chain serves a recursion (band.h): Toeplitz register windows when the window is a
+// fixed offset range instantiated below (code 16*TW + TD0 + 2), else banded with LDS windows
+// of the padded width (2/4/8), else the dense chain (0).
+template <int KIND, int NP>
+__device__ __forceinline__ int rec_band_code(const RecArgs& a) {
+  if (!a.band) return 0;
+  const BandDesc* d = a.band;
+  const int W = KIND == kFbBeta ? d->wr : d->wc;
+  if (W > kBandMax) return 0;
+  const int tw = KIND == kFbBeta ? d->trw : d->tcw;
+  const int td0 = KIND == kFbBeta ? d->trd0 : d->tcd0;
+  if (NP <= 128 && tw > 0) {
+    const int code = 16 * tw + td0 + 2;
+    switch (code) {
+      case 16 * 1 + 0 + 2: case 16 * 2 - 1 + 2: case 16 * 2 + 0 + 2:
+      case 16 * 3 - 2 + 2: case 16 * 3 - 1 + 2: case 16 * 3 + 0 + 2: return code;
+      default: break;
+    }
+  }
+  return KIND == kFbBeta ? d->wrp : d->wcp;
+}
+
+template <int NP, int KIND>
+__device__ __forceinline__ void rec_dispatch(const RecArgs& a, float* lds, int b) {
+  switch (rec_band_code<KIND, NP>(a)) {
+    case 2: rec_band<NP, KIND, 2>(a, lds, b, a.band); break;
+    case 4: rec_band<NP, KIND, 4>(a, lds, b, a.band); break;
+    case 8: rec_band<NP, KIND, 8>(a, lds, b, a.band); break;
+    case 16 * 1 + 0 + 2: rec_band<NP, KIND, 2, 0, 1>(a, lds, b, a.band); break;
+    case 16 * 2 - 1 + 2: rec_band<NP, KIND, 2, -1, 2>(a, lds, b, a.band); break;
+    case 16 * 2 + 0 + 2: rec_band<NP, KIND, 2, 0, 2>(a, lds, b, a.band); break;
+    case 16 * 3 - 2 + 2: rec_band<NP, KIND, 2, -2, 3>(a, lds, b, a.band); break;
+    case 16 * 3 - 1 + 2: rec_band<NP, KIND, 2, -1, 3>(a, lds, b, a.band); break;
+    case 16 * 3 + 0 + 2: rec_band<NP, KIND, 2, 0, 3>(a, lds, b, a.band); break;
+    default: rec_run<NP, KIND>(a, lds, b); break;
   }
 }
 

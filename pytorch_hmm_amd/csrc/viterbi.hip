@@ -55,15 +55,31 @@ struct VitArgs {
   const BandDesc* band;  // banded decomposition (band.h) or null
 };
 
+// log_obs = log(x + 1e-8) (hmm.py:152), fp32 add then fp64 log rounded once (common.h)
+__global__ void __launch_bounds__(256) log_obs_kernel(const float* __restrict__ x, float* __restrict__ y, size_t n,
+                                                      int vec4) {
+  const size_t n4 = vec4 ? n / 4 : 0;
+  const size_t stride = (size_t)gridDim.x * blockDim.x;
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += stride) {
+    const float4 v = reinterpret_cast<const float4*>(x)[i];
+    reinterpret_cast<float4*>(y)[i] = make_float4(log_obs_cr(v.x), log_obs_cr(v.y), log_obs_cr(v.z), log_obs_cr(v.w));
+  }
+  for (size_t i = n4 * 4 + (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) y[i] = log_obs_cr(x[i]);
+}
+
+static hipError_t launch_log_obs(const float* x, float* y, size_t n, hipStream_t st) {
+  if (n == 0) return hipSuccess;
+  size_t blocks = (n / 4 + 255) / 256;
+  blocks = blocks < 4096 ? (blocks > 0 ? blocks : 1) : 4096;
+  const int vec4 = ((reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(y)) & 15) == 0;
+  hipLaunchKernelGGL(log_obs_kernel, dim3((unsigned)blocks), dim3(256), 0, st, x, y, n, vec4);
+  return hipGetLastError();
+}
+
 template <int NP>
 __global__ void __launch_bounds__(RC<NP>::NT) vit_fwd_kernel(RecArgs ra) {
   extern __shared__ __attribute__((aligned(16))) float lds[];
-  switch (rec_band_width<kVit>(ra)) {
-    case 2: rec_band<NP, kVit, 2>(ra, lds, blockIdx.x, ra.band); break;
-    case 4: rec_band<NP, kVit, 4>(ra, lds, blockIdx.x, ra.band); break;
-    case 8: rec_band<NP, kVit, 8>(ra, lds, blockIdx.x, ra.band); break;
-    default: rec_run<NP, kVit>(ra, lds, blockIdx.x); break;
-  }
+  rec_dispatch<NP, kVit>(ra, lds, blockIdx.x);
 }
 
 // psi rows of one chunk -> HBM, and the chunk map G[j] = state at t_lo - 1 given j at t_hi
@@ -94,52 +110,62 @@ __device__ __forceinline__ void psi_write_rows(const VitArgs& a, uint8_t (*prow)
 // i1 itself attains v whenever M == v (inside the window its value is >= g_i1 = M = v).
 template <int NP>
 __device__ __forceinline__ void psi_band_rows(const VitArgs& a, uint8_t (*prow)[NP], float* rowM, int* rowI,
-                                              int b, int t_lo, int t_hi) {
+                                              float* drows, int b, int t_lo, int t_hi) {
   using C = VF<NP>;
   const BandDesc* __restrict__ d = a.band;
   const int tid = threadIdx.x, w = tid >> 6, l = tid & 63;
   const int T = a.T, N = a.N, W = d->wcp;
-  const float* dbase = a.delta + (size_t)b * T * N;
   const int t_first = t_lo > 0 ? t_lo : 1;
-  for (int t = t_first + w; t <= t_hi; t += C::NW) {
+  const int rows = t_hi - t_first + 1;
+  // the chunk's delta rows t_first-1 .. t_hi-1, coalesced, into LDS (row stride NP)
+  const float* dsrc = a.delta + ((size_t)b * T + (t_first - 1)) * N;
+  for (int idx = tid; idx < rows * N; idx += C::NT) {
+    const int r = idx / N, c = idx - r * N;
+    drows[r * NP + c] = dsrc[idx];
+  }
+  __syncthreads();
+  float rf[C::NBLK];
+#pragma unroll
+  for (int blk = 0; blk < C::NBLK; ++blk) rf[blk] = d->rfl[64 * blk + l];
+  for (int r = w; r < rows; r += C::NW) {
     float bv = -INFINITY;
     int bi = 0x7fffffff;
 #pragma unroll
     for (int blk = 0; blk < C::NBLK; ++blk) {
       const int i = 64 * blk + l;
-      const bool ok = i < N;
-      const float g = dbase[(size_t)(t - 1) * N + (ok ? i : 0)] + d->rfl[i];
-      if (ok) argmax_combine(bv, bi, g, i);
+      if (i < N) argmax_combine(bv, bi, drows[r * NP + i] + rf[blk], i);
     }
     wave_argmax(bv, bi);
-    if (l == 0) { rowM[t - t_lo] = bv; rowI[t - t_lo] = bi; }
+    if (l == 0) { rowM[r] = bv; rowI[r] = bi; }
   }
+  // each thread keeps one output column o for all rows (NT is a multiple of NP)
+  static_assert(C::NT % NP == 0, "psi layout");
+  const int o = tid % NP;
+  const int lo = d->clo[o];
+  float wl[kBandMax];
+#pragma unroll
+  for (int k = 0; k < kBandMax; ++k) wl[k] = (k < W && lo + k < N) ? d->cL[o][k] : -INFINITY;
   __syncthreads();
-  const int rows = t_hi - t_first + 1;
-  for (int idx = tid; idx < rows * NP; idx += C::NT) {
-    const int t = t_first + idx / NP, o = idx % NP;
+  for (int r = tid / NP; r < rows; r += C::NT / NP) {
     int arg = 0;
     if (o < N) {
-      const float M = rowM[t - t_lo];
-      const int lo = d->clo[o];
-      const float* drow = dbase + (size_t)(t - 1) * N + lo;
+      const float M = rowM[r];
       float v = M;
       float val[kBandMax];
 #pragma unroll
       for (int k = 0; k < kBandMax; ++k) {
-        val[k] = (k < W && lo + k < N) ? drow[k] + d->cL[o][k] : -INFINITY;
+        val[k] = (k < W && lo + k < N) ? drows[r * NP + lo + k] + wl[k] : -INFINITY;
         v = fmaxf(v, val[k]);
       }
-      arg = M == v ? rowI[t - t_lo] : 0x7fffffff;
+      arg = M == v ? rowI[r] : 0x7fffffff;
 #pragma unroll
       for (int k = 0; k < kBandMax; ++k)
         if (k < W && val[k] == v && lo + k < arg) arg = lo + k;
     }
-    prow[t - t_lo][o] = (uint8_t)arg;
+    prow[t_first + r - t_lo][o] = (uint8_t)arg;
   }
 }
 
-// ---------------------------------------------------------------------------- psi
 template <int NP>
 __global__ void __launch_bounds__(VF<NP>::NT) vit_psi_kernel(VitArgs a) {
   using C = VF<NP>;
@@ -166,7 +192,8 @@ __global__ void __launch_bounds__(VF<NP>::NT) vit_psi_kernel(VitArgs a) {
   if (a.band && a.band->wc <= kBandMax) {
     __shared__ float rowM[kChunk];
     __shared__ int rowI[kChunk];
-    psi_band_rows<NP>(a, prow, rowM, rowI, b, t_lo, t_hi);
+    extern __shared__ __attribute__((aligned(16))) float drows[];  // [kChunk][NP] (dynamic)
+    psi_band_rows<NP>(a, prow, rowM, rowI, drows, b, t_lo, t_hi);
     __syncthreads();
     psi_write_rows<NP>(a, prow, b, chunk, t_lo, t_hi);
     return;
@@ -295,7 +322,9 @@ static hipError_t launch_vit(const VitArgs& va, hipStream_t sm) {
   hipLaunchKernelGGL(vit_fwd_kernel<NP>, dim3(va.B), dim3(RC<NP>::NT), kExclusiveLds, sm, ra);
   e = hipGetLastError();
   if (e != hipSuccess) return e;
-  hipLaunchKernelGGL(vit_psi_kernel<NP>, dim3(va.nchunks, va.B), dim3(VF<NP>::NT), 0, sm, va);
+  // banded psi stages the chunk's delta rows in LDS (dynamic, kChunk x NP floats)
+  const size_t psi_lds = va.band ? (size_t)kChunk * NP * sizeof(float) : 0;
+  hipLaunchKernelGGL(vit_psi_kernel<NP>, dim3(va.nchunks, va.B), dim3(VF<NP>::NT), psi_lds, sm, va);
   e = hipGetLastError();
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL(vit_backtrace_kernel<NP>, dim3(va.nchunks, va.B), dim3(64), 0, sm, va);
@@ -310,7 +339,8 @@ HMM355_API size_t hmm355_viterbi_workspace_bytes(int B, int T, int N) {
   if (B < 0 || T < 1 || N < 1 || N > 256) return 0;
   const size_t NP = pad_states(N);
   const size_t nc = (T + kChunk - 1) / kChunk;
-  return align_up((size_t)B * T * NP, 256) + align_up((size_t)B * nc * NP, 256) + align_up(sizeof(BandDesc), 256);
+  return align_up((size_t)B * T * NP, 256) + align_up((size_t)B * nc * NP, 256) + align_up(sizeof(BandDesc), 256) +
+         align_up((size_t)B * T * N * sizeof(float), 256);
 }
 
 HMM355_API int hmm355_viterbi_f32(const float* obs, int obs_mode, const float* log_P, const float* init, int B,
@@ -328,7 +358,18 @@ HMM355_API int hmm355_viterbi_f32(const float* obs, int obs_mode, const float* l
   const int nc = (T + kChunk - 1) / kChunk;
   uint8_t* psi = static_cast<uint8_t*>(workspace);
   uint8_t* G = psi + align_up((size_t)B * T * NP, 256);
-  BandDesc* band = use_band() ? reinterpret_cast<BandDesc*>(G + align_up((size_t)B * nc * NP, 256)) : nullptr;
+  uint8_t* bandp = G + align_up((size_t)B * nc * NP, 256);
+  BandDesc* band = use_band() ? reinterpret_cast<BandDesc*>(bandp) : nullptr;
+  hipStream_t sm0 = static_cast<hipStream_t>(stream);
+  if (obs_mode == HMM355_OBS_PROB) {
+    // log(x + 1e-8) once over the whole tensor, full chip (fp64 log, rounded once): the
+    // serial chain then stages plain copies
+    float* lo = reinterpret_cast<float*>(bandp + align_up(sizeof(BandDesc), 256));
+    const hipError_t e0 = launch_log_obs(obs, lo, (size_t)B * T * N, sm0);
+    if (e0 != hipSuccess) return (int)e0;
+    obs = lo;
+    obs_mode = HMM355_OBS_LOG;
+  }
   VitArgs va{obs, log_P, init, log_delta, final_score, states, psi, G, B, T, N, obs_mode, nc, band};
   hipStream_t sm = static_cast<hipStream_t>(stream);
   hipError_t e;

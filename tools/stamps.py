@@ -22,14 +22,19 @@ dev = torch.device("cuda", 0)
 B, T, N = int(os.environ.get("B", 32)), int(os.environ.get("T", 2000)), int(os.environ.get("N", 128))
 NW = {64: 4, 128: 8, 256: 16}[128 if N > 64 and N <= 128 else (64 if N <= 64 else 256)]
 obs = torch.softmax(torch.randn(B, T, N, device=dev), -1)
-P = torch.rand(N, N, device=dev); lP = torch.log(P / P.sum(1, keepdim=True) + 1e-8); lp0 = torch.full((N,), -4.85, device=dev)
+if os.environ.get("HMM355_DENSE") == "1":
+    P = torch.rand(N, N, device=dev)
+else:  # left-to-right 0.7 (the bench matrix): banded chains
+    P = torch.zeros(N, N, device=dev); i = torch.arange(N - 1, device=dev)
+    P[i, i] = 0.7; P[i, i + 1] = 0.3; P[N - 1, N - 1] = 1.0
+lP = torch.log(P / P.sum(1, keepdim=True) + 1e-8); lp0 = torch.full((N,), -4.85, device=dev)
 p = lambda t: ctypes.c_void_p(t.data_ptr())
 st = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
 post = torch.empty(B, T, N, device=dev); ll = torch.empty(B, device=dev); lr = torch.empty(B, device=dev)
 ws = torch.empty(L.hmm355_fb_workspace_bytes(B, T, N), dtype=torch.uint8, device=dev)
 states = torch.empty(B, T, dtype=torch.int64, device=dev); delta = torch.empty(B, T, N, device=dev); fin = torch.empty(B, device=dev)
 wsv = torch.empty(L.hmm355_viterbi_workspace_bytes(B, T, N), dtype=torch.uint8, device=dev)
-names = ["gather", "compute", "write", "barrier"]
+names = ["gather", "compute", "write", "barrier"] if os.environ.get("HMM355_DENSE") == "1" else ["issue+reduce", "window+update", "block-end", "block-barrier"]
 
 
 def report(tag, fn, nblocks):
@@ -42,6 +47,8 @@ def report(tag, fn, nblocks):
     buf = (ctypes.c_ulonglong * n)()
     assert sym(buf, n) == 0
     a = np.frombuffer(buf, dtype=np.uint64).reshape(-1, 8)[: nblocks * NW].astype(np.float64)
+    if os.environ.get("HMM355_DENSE") != "1":  # banded: the chain is wave 0 of each block
+        a = a.reshape(nblocks, NW, 8)[:, :1].repeat(NW, axis=1).reshape(-1, 8)
     steps = np.maximum(a[:, 4], 1)
     seg = a[:, :4] / steps[:, None]
     clk = a[:, 6] / np.maximum(a[:, 7], 1) * 100.0
