@@ -41,6 +41,10 @@ def parse():
     p.add_argument("--gather", action="store_true", help="RCCL gather of posteriors+states to rank 0 each step")
     p.add_argument("--serial", action="store_true", help="run FB and Viterbi on one stream")
     p.add_argument("--cpu-seconds", type=float, default=12.0, help="bounded CPU-baseline budget (0 = skip)")
+    p.add_argument("--no-graph", action="store_true",
+                   help="launch every step eagerly instead of replaying one captured HIP graph")
+    p.add_argument("--transition", default="left_to_right", choices=["left_to_right", "ergodic"],
+                   help="transition matrix of the workload (BASELINE: left_to_right 0.7)")
     return p.parse_args()
 
 
@@ -55,6 +59,27 @@ def setup_dist(args):
     else:
         torch.cuda.set_device(0)
     return rank, world, local
+
+
+def profiled_traffic(op, B, T, N, transition):
+    """HBM bytes per launch of `op` from the committed rocprofv3 PMC summary (FETCH_SIZE x 2 +
+    WRITE_SIZE, MI355X_MICROARCH.md's gfx950 correction; tools/gpu_prof.sh -> profiles/),
+    when it was taken on this exact configuration; else None."""
+    import glob
+    for f in sorted(glob.glob(os.path.join(HERE, "profiles", "*_summary.json")), reverse=True):
+        try:
+            d = json.load(open(f))
+        except (OSError, ValueError):
+            continue
+        cfg = d.get("bench_config") or {}
+        if (cfg.get("batch_per_gpu"), cfg.get("seq_len"), cfg.get("num_states")) != (B, T, N):
+            continue
+        if transition not in str(cfg.get("transition", "")):
+            continue
+        v = d.get("ops", {}).get(op, {}).get("hbm_bytes_per_launch")
+        if v:
+            return float(v), os.path.relpath(f, HERE)
+    return None, None
 
 
 def cpu_baseline(B, T, N, budget):
@@ -90,7 +115,10 @@ def main():
     from pytorch_hmm_amd import ops
 
     B, T, N = args.batch, args.T, args.N
-    hmm = ph.HMMPyTorch(ph.create_left_to_right_matrix(N, 0.7))
+    if args.transition == "ergodic":
+        hmm = ph.HMMPyTorch(ph.create_transition_matrix(N, "ergodic"))
+    else:
+        hmm = ph.HMMPyTorch(ph.create_left_to_right_matrix(N, 0.7))
     g = torch.Generator(device=dev).manual_seed(1234 + rank)
     obs = torch.softmax(torch.randn(B, T, N, device=dev, generator=g), dim=-1)
     hmm._params_for(obs)
@@ -98,7 +126,6 @@ def main():
 
     s_fb = torch.cuda.Stream(dev)
     s_vit = s_fb if args.serial else torch.cuda.Stream(dev)
-    main_s = torch.cuda.current_stream(dev)
     ev = {k: [] for k in ("fb", "vit")}
 
     gather_bufs = None
@@ -107,6 +134,7 @@ def main():
                        [torch.empty(B, T, dtype=torch.int64, device=dev) for _ in range(world)])
 
     def step(record):
+        main_s = torch.cuda.current_stream(dev)  # the capture stream while a graph is captured
         s_fb.wait_stream(main_s)
         s_vit.wait_stream(main_s)
         with torch.cuda.stream(s_fb):
@@ -138,15 +166,34 @@ def main():
                 dist.gather(states, None, dst=0)
         return post, states
 
+    use_graph = not args.no_graph and not (args.gather and world > 1)
+    graph = None
+    if use_graph:
+        # one step (both streams) captured as a HIP graph: the timed loop replays it, so the
+        # host launch path (op dispatch, workspace allocation, ctypes) is out of the step
+        for _ in range(2):
+            step(False)
+        torch.cuda.synchronize(dev)
+        graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(graph):
+            step(False)
+        torch.cuda.synchronize(dev)
+
+    def run_step():
+        if graph is not None:
+            graph.replay()
+        else:
+            step(True)
+
     for _ in range(args.warmup):
-        step(False)
+        run_step()
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        step(True)
+        run_step()
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
@@ -156,6 +203,12 @@ def main():
         tt = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         elapsed = float(tt.item())
+    if graph is not None:
+        # per-op launch durations for the roofline: the same ops, eagerly, HIP events on the
+        # stream each op's kernels run on
+        for _ in range(min(args.steps, 10)):
+            step(True)
+        torch.cuda.synchronize(dev)
 
     fb_ms = sum(a.elapsed_time(b) for a, b in ev["fb"]) / len(ev["fb"])
     vit_ms = sum(a.elapsed_time(b) for a, b in ev["vit"]) / len(ev["vit"])
@@ -166,11 +219,12 @@ def main():
     # roofline of the dominant op, algorithmic bytes per SURVEY.md §8(d)
     if fb_ms >= vit_ms:
         dom, dur_ms, bytes_per_launch = "forward_backward", fb_ms, 16 * N * B * T
-        kernels = "fb_recur_kernel + fb_posterior_kernel"
+        kernels = "band_prep_kernel + fb_recur_kernel + fb_posterior_kernel"
     else:
         dom, dur_ms, bytes_per_launch = "viterbi", vit_ms, (8 * N + 8) * B * T
-        kernels = "vit_fwd_kernel + vit_psi_kernel + vit_backtrace_kernel"
+        kernels = "band_prep_kernel + log_obs_kernel + vit_fwd_kernel + vit_psi_kernel + vit_backtrace_kernel"
     achieved = bytes_per_launch / (dur_ms * 1e-3) / 1e9
+    traffic, traffic_src = profiled_traffic(dom, B, T, N, args.transition)
     out = {
         "metric": "frames/sec forward-backward+Viterbi, B=32 T=2000 N=128, 1/2/4/8 GPU",
         "value": value, "unit": "frames/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
@@ -178,12 +232,15 @@ def main():
         "dtype": "f32", "data": "synthetic: softmax(randn(B,T,N)) emissions, left-to-right(0.7) transitions",
         "config": {"workload": "HMMPyTorch forward_backward + viterbi_decode", "batch_per_gpu": B,
                    "global_batch": B * world, "seq_len": T, "num_states": N,
-                   "transition": "left_to_right(0.7)", "parallelism": f"batch-sharded x{world}",
-                   "streams": 1 if args.serial else 2, "gather": bool(args.gather and world > 1)},
+                   "transition": "left_to_right(0.7)" if args.transition == "left_to_right" else "ergodic",
+                   "parallelism": f"batch-sharded x{world}",
+                   "streams": 1 if args.serial else 2, "gather": bool(args.gather and world > 1),
+                   "hip_graph": graph is not None},
         "op_ms": {"forward_backward": fb_ms, "viterbi": vit_ms},
         "roofline": {"bound": "hbm", "kernel": dom, "kernels": kernels, "achieved": achieved,
                      "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
-                     "traffic": None, "bytes_per_launch": bytes_per_launch, "avg_launch_ms": dur_ms},
+                     "traffic": traffic, "traffic_source": traffic_src,
+                     "bytes_per_launch": bytes_per_launch, "avg_launch_ms": dur_ms},
     }
     if rank == 0 and world == 1 and args.cpu_seconds > 0:
         out["cpu_baseline"] = cpu_baseline(B, T, N, args.cpu_seconds)
