@@ -45,6 +45,9 @@ def parse():
                    help="launch every step eagerly instead of replaying one captured HIP graph")
     p.add_argument("--transition", default="left_to_right", choices=["left_to_right", "ergodic"],
                    help="transition matrix of the workload (BASELINE: left_to_right 0.7)")
+    p.add_argument("--workload", default="ns", choices=["ns", "c1", "c2", "c3", "c5"],
+                   help="ns: the BASELINE metric (default).  c1/c2/c3/c5: BASELINE configs 1, 2, 3, 5 "
+                        "(HMMLayer, GaussianHMMLayer, MixtureGaussianHMMLayer, HSMMLayer) through the layers")
     return p.parse_args()
 
 
@@ -94,7 +97,7 @@ def cpu_baseline(B, T, N, budget):
     lP, lp0 = O.hmm_params(O.left_to_right_matrix(N, 0.7))
     frames, elapsed, reps = 0, 0.0, 0
     with torch.no_grad():
-        while reps == 0 or (elapsed < budget and reps < 8):
+        while reps == 0 or (elapsed < budget and reps < 64):
             t0 = time.perf_counter()
             O.forward_backward(obs, lP, lp0)
             O.viterbi_decode(obs, lP, lp0)
@@ -107,9 +110,173 @@ def cpu_baseline(B, T, N, budget):
                       f"{threads} threads, {elapsed:.1f}s)"}
 
 
+VALU_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md: FP32 vector peak (spec)
+
+
+def layer_workload(args, rank, world, dev):
+    """BASELINE configs 1/2/3/5 through the drop-in layers.
+    One step = the config's reference call sequence on one synthetic batch (random-init layer
+    of the named architecture, seed 0), inputs resident in HBM; each rank runs its own batch
+    (weak scaling).  Prints one JSON line with the dominant kernel's roofline and a bounded
+    CPU baseline (the oracle restatement, rank 0, N=1)."""
+    import pytorch_hmm_amd as ph
+    from oracle import hmm_oracle as O
+    wl = args.workload
+    torch.manual_seed(0)
+    gx = torch.Generator(device=dev).manual_seed(1234 + rank)
+    if wl == "c1":
+        B, T, K = 2, 100, 5
+        layer = ph.HMMLayer(K).to(dev)
+        x = torch.randn(B, T, K, device=dev, generator=gx)
+
+        def step():
+            layer.train()
+            post = layer(x)                 # forward-backward posteriors
+            layer.eval()
+            onehot, align = layer(x, return_alignment=True)   # Viterbi
+            return post, align
+        desc = {"workload": "HMMLayer(5) train forward-backward + eval Viterbi", "batch_per_gpu": B,
+                "seq_len": T, "num_states": K}
+        dom, flops, bytes_ = "hmm_layer_pair", None, (16 * K + 8 * K + 8) * B * T
+    elif wl == "c2":
+        B, T, K, D = 32, 2000, 64, 80
+        layer = ph.GaussianHMMLayer(K, D).to(dev)
+        x = torch.randn(B, T, D, device=dev, generator=gx)
+
+        def step():
+            layer.train()
+            post = layer(x)                 # Gaussian emission + forward-backward
+            layer.eval()
+            onehot = layer(x)               # Gaussian emission + Viterbi
+            return post, onehot
+        desc = {"workload": "GaussianHMMLayer(64,80) train forward-backward + eval Viterbi", "batch_per_gpu": B,
+                "seq_len": T, "num_states": K, "feature_dim": D}
+        dom, flops, bytes_ = "gaussian_pair", None, (2 * 4 * D + 8 * K + 12 * K) * B * T
+    elif wl == "c3":
+        B, T, S, C, D = 32, 2000, 128, 4, 80
+        layer = ph.MixtureGaussianHMMLayer(S, D, num_components=C).to(dev)
+        x = torch.randn(B, T, D, device=dev, generator=gx)
+
+        def step():
+            return layer(x, return_log_probs=True)   # GMM emission + Viterbi
+        desc = {"workload": "MixtureGaussianHMMLayer(128,80,num_components=4) forward (emission + Viterbi)",
+                "batch_per_gpu": B, "seq_len": T, "num_states": S, "num_components": C, "feature_dim": D}
+        dom, flops, bytes_ = "gmm_score_kernel", 4.0 * S * C * D * B * T, (4 * D + 4 * S) * B * T
+    else:  # c5
+        B, T, S, D, Dm = 16, 2000, 64, 80, 40
+        layer = ph.HSMMLayer(S, D, max_duration=Dm).to(dev)
+        x = torch.randn(B, T, D, device=dev, generator=gx)
+
+        def step():
+            return layer(x)                 # Gaussian emission + segment Viterbi
+        desc = {"workload": "HSMMLayer(64,80,max_duration=40) forward (segment Viterbi)", "batch_per_gpu": B,
+                "seq_len": T, "num_states": S, "max_duration": Dm, "feature_dim": D}
+        # reorganised recursion: per start, S*S*Dmax (max over d') + S*S (candidates) adds/max
+        dom, flops, bytes_ = "hsmm_fwd_kernel", 2.0 * (S * S * Dm + S * S) * B * T, (4 * S + 8) * B * T
+
+    with torch.no_grad():
+        for _ in range(max(args.warmup, 1)):
+            step()
+        torch.cuda.synchronize(dev)
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize(dev)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        t0 = time.perf_counter()
+        e0.record()
+        for _ in range(args.steps):
+            step()
+        e1.record()
+        torch.cuda.synchronize(dev)
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize(dev)
+        elapsed = time.perf_counter() - t0
+    if world > 1:
+        tt = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        elapsed = float(tt.item())
+    step_ms = e0.elapsed_time(e1) / args.steps
+    frames = desc["batch_per_gpu"] * desc["seq_len"]
+    value = frames * world * args.steps / elapsed
+    if flops is not None:
+        achieved = flops / (step_ms * 1e-3) / 1e12
+        roof = {"bound": "valu", "kernel": dom, "achieved": achieved, "peak": VALU_PEAK_TFLOPS, "unit": "TFLOP/s",
+                "frac": achieved / VALU_PEAK_TFLOPS, "traffic": None, "flops_per_launch": flops,
+                "avg_launch_ms": step_ms, "note": "whole step time (HIP events) as the launch duration"}
+    else:
+        achieved = bytes_ / (step_ms * 1e-3) / 1e9
+        roof = {"bound": "hbm", "kernel": dom, "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": achieved / HBM_PEAK_GBS, "traffic": None, "bytes_per_launch": bytes_,
+                "avg_launch_ms": step_ms, "note": "whole step time (HIP events) as the launch duration"}
+    out = {"metric": f"frames/sec {desc['workload']}", "value": value, "unit": "frames/s", "n_gpus": world,
+           "steps": args.steps, "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3,
+           "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32",
+           "data": "synthetic: randn features, random-init layer (seed 0)",
+           "config": dict(desc, global_batch=desc["batch_per_gpu"] * world, parallelism=f"batch-sharded x{world}"),
+           "roofline": roof}
+    if rank == 0 and world == 1 and args.cpu_seconds > 0:
+        out["cpu_baseline"] = layer_cpu_baseline(wl, layer, args.cpu_seconds)
+        out["cpu_baseline"]["speedup_gpu_over_cpu"] = value / out["cpu_baseline"]["value"]
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+
+
+def layer_cpu_baseline(wl, layer, budget):
+    """Bounded CPU baseline for a layer workload: the oracle restatement of the reference's op
+    sequence (torch-CPU, or the C restatement for the HSMM recursion, whose literal reference
+    loop takes ~55 h per sequence at this size), on a sample of the batch."""
+    from oracle import hmm_oracle as O
+    import numpy as np
+    threads = max(1, min(int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1)), os.cpu_count() or 1))
+    torch.set_num_threads(threads)
+    g = torch.Generator().manual_seed(7)
+    frames, elapsed, reps = 0, 0.0, 0
+    with torch.no_grad():
+        sd = {k: v.detach().cpu() for k, v in layer.state_dict().items()}
+        while reps == 0 or (elapsed < budget and reps < 64):
+            t0 = time.perf_counter()
+            if wl == "c1":
+                x = torch.randn(2, 100, 5, generator=g)
+                lP, lp0 = O.hmmlayer_params(sd["log_transition_logits"], sd["log_initial_logits"], True)
+                O.forward_backward(torch.sigmoid(x), lP, lp0)
+                O.viterbi_decode(torch.sigmoid(x), lP, lp0)
+                n = 200
+            elif wl == "c2":
+                x = torch.randn(2, 2000, 80, generator=g)
+                lP, lp0 = O.hmmlayer_params(sd["hmm_layer.log_transition_logits"], sd["hmm_layer.log_initial_logits"], True)
+                pr = torch.exp(O.gaussian_log_probs(x, sd["means"], sd["log_scales"]))
+                O.forward_backward(pr, lP, lp0)
+                O.viterbi_decode(pr, lP, lp0)
+                n = 4000
+            elif wl == "c3":
+                x = torch.randn(1, 2000, 80, generator=g)
+                lp = O.mixture_log_probs(x, sd["mixture_weights_logits"], sd["means"], sd["log_vars"], t_chunk=250)
+                O.mixture_viterbi(lp, O.mixture_log_transitions(sd["transition_logits"]))
+                n = 2000
+            else:
+                x = torch.randn(1, 2000, 80, generator=g)
+                lp = O.hsmm_log_probs(x, sd["observation_means"], sd["observation_log_vars"])
+                du = O.hsmm_duration_log_probs(sd["duration_shape"], sd["duration_rate"], 1, 40)
+                O.c_hsmm(lp.numpy(), du.numpy(), O.hsmm_log_transitions(sd["transition_logits"]).numpy())
+                n = 2000
+            elapsed += time.perf_counter() - t0
+            frames += n
+            reps += 1
+    kind_note = {"c1": "B=2 T=100", "c2": "B=2 of 32, T=2000", "c3": "B=1 of 32, T=2000",
+                 "c5": "B=1 of 16, T=2000; HSMM recursion in the C restatement (1 thread)"}[wl]
+    return {"value": frames / elapsed, "unit": "frames/s", "cores": threads if wl != "c5" else 1, "kind": "port",
+            "sample": f"{reps} x ({kind_note}) oracle restatement of the reference op sequence, {elapsed:.1f}s"}
+
+
 def main():
     args = parse()
     rank, world, local = setup_dist(args)
+    if args.workload != "ns":
+        layer_workload(args, rank, world, torch.device("cuda", local))
+        if world > 1:
+            dist.destroy_process_group()
+        return
     dev = torch.device("cuda", local)
     import pytorch_hmm_amd as ph
     from pytorch_hmm_amd import ops

@@ -64,6 +64,21 @@ int hmm355_version(void);
  *   workspace  >= hmm355_fb_workspace_bytes(B,T,N) bytes of device memory
  * ------------------------------------------------------------------------------ */
 size_t hmm355_fb_workspace_bytes(int B, int T, int N);
+/* Same as hmm355_forward_backward_f32 with a custom terminal backward vector:
+ *   log_beta_T (B,N) or NULL: log beta_{T-1} (NULL = 0, the reference's beta_{T-1} = 1,
+ *              hmm.py:105).  With log_beta_T = log(dL/d log alpha_{T-1}) - log alpha_{T-1}
+ *              the backward pass is the adjoint of the forward recursion for a loss L of
+ *              alpha_{T-1}: dL/d log_obs_t = G * posterior_t with G = sum_j dL/d log alpha_{T-1,j}
+ *              (pytorch_hmm_amd/autograd.py; replaces the reference's autograd through
+ *              hmm.py:89-101 for compute_likelihood / HMMLayer.compute_loss, hmm_layer.py:144-173).
+ * Workspace layout (256-B aligned pieces, in order): U (B,T,NP) scaled alpha rows | V
+ * (B,T,NP) scaled beta rows | LA (B,T) | LB (B,T) | ... ; alpha_t = U_t exp(LA_t),
+ * beta_t = V_t exp(LB_t), NP = N padded to 64/128/256. */
+int hmm355_forward_backward_ex_f32(const float* obs, int obs_mode, const float* log_P,
+                                   const float* log_p0, const float* log_beta_T, int B, int T, int N,
+                                   unsigned out_mask, float* posterior, float* forward,
+                                   float* backward, float* loglik, float* lik_ref, void* workspace,
+                                   size_t workspace_bytes, void* stream);
 int hmm355_forward_backward_f32(const float* obs, int obs_mode, const float* log_P,
                                 const float* log_p0, int B, int T, int N, unsigned out_mask,
                                 float* posterior, float* forward, float* backward,

@@ -20,7 +20,7 @@ FB_BACKWARD = 4
 # every symbol include/hmm355.h declares (checked by tests/test_native_abi.py)
 EXPORTS = (
     "hmm355_strerror", "hmm355_version",
-    "hmm355_fb_workspace_bytes", "hmm355_forward_backward_f32",
+    "hmm355_fb_workspace_bytes", "hmm355_forward_backward_f32", "hmm355_forward_backward_ex_f32",
     "hmm355_viterbi_workspace_bytes", "hmm355_viterbi_f32",
     "hmm355_gmm_workspace_bytes", "hmm355_gmm_diag_logprob_f32",
     "hmm355_hsmm_workspace_bytes", "hmm355_hsmm_viterbi_f32",
@@ -49,6 +49,8 @@ def lib():
     L.hmm355_fb_workspace_bytes.argtypes, L.hmm355_fb_workspace_bytes.restype = [I, I, I], S
     L.hmm355_forward_backward_f32.argtypes = [P, I, P, P, I, I, I, U, P, P, P, P, P, P, S, P]
     L.hmm355_forward_backward_f32.restype = I
+    L.hmm355_forward_backward_ex_f32.argtypes = [P, I, P, P, P, I, I, I, U, P, P, P, P, P, P, S, P]
+    L.hmm355_forward_backward_ex_f32.restype = I
     L.hmm355_viterbi_workspace_bytes.argtypes, L.hmm355_viterbi_workspace_bytes.restype = [I, I, I], S
     L.hmm355_viterbi_f32.argtypes = [P, I, P, P, I, I, I, P, P, P, P, S, P]
     L.hmm355_viterbi_f32.restype = I

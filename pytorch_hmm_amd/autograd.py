@@ -1,17 +1,222 @@
-"""Autograd for the forward-backward op (training-mode HMMLayer / compute_loss).
+"""Autograd for the forward-backward path (HMMLayer.compute_loss / training).
 
-The reference differentiates through its Python loop with plain autograd
-(hmm_layer.py:144-173, test_hmm.py:189-208).  Here the gradient is the analytic adjoint
-of the two recursions, computed by HIP kernels (csrc/fb_grad.hip).
+The reference differentiates through its Python loops with plain autograd
+(hmm.py:89-101 via hmm_layer.py:144-173; test_hmm.py:189-208 trains HMMLayer through
+compute_loss).  Here the gradient is the analytic adjoint of the forward recursion, run by
+the same HIP kernels:
+
+For a loss L(log alpha_{T-1}) with g = dL/d log alpha_{T-1} and G = sum_j g_j, the adjoint
+lambda_t = dL/d log alpha_t satisfies lambda_t = alpha_t * mu_t where mu is the BACKWARD
+recursion started from mu_{T-1} = g / alpha_{T-1} (hmm355_forward_backward_ex_f32 with
+log_beta_T = log mu_{T-1}); sum_j lambda_t(j) = G at every t, so
+    dL/d log_obs_t = G * posterior'_t          (posterior' = u v / sum(u v) of that pass)
+    dL/d log_p0    = sum_b G_b posterior'_{b,0}
+    dL/d log_P     = exp(log_P) * sum_{b,t} G_b X_t (x) Y_t,
+        X_t = u_{t-1} / (c_{t-1} * sum_k u_t v_t),  Y_t = e_t * v_t,  c_{t-1} = sum u_{t-1}
+(u, v: the scaled rows the chains store; every factor is O(1), no exp of log-scales).  The
+last contraction is a plain batched GEMM (torch.einsum -> hipBLASLt).
+
+Losses: 'ref'   = the reference's compute_likelihood value LSE_j log(exp(log alpha_{T-1,j}) + 1e-8)
+                  (its gradient underflows to 0 exactly where the reference's does);
+        'exact' = log sum_j alpha_{T-1,j}  (HMMPyTorch.log_likelihood).
+Posteriors from forward_backward are returned as values; back-propagating THROUGH them
+(e.g. the supervised cross-entropy of compute_loss) is not implemented and raises.
 """
+import math
+
 import torch
+
+from . import _native as nat
 
 
 def needs_grad(*tensors) -> bool:
     return torch.is_grad_enabled() and any(t is not None and t.requires_grad for t in tensors)
 
 
-def forward_backward_with_grad(obs, log_P, log_p0):
-    raise NotImplementedError(
-        "differentiable forward-backward (analytic adjoint kernels) is not built yet; "
-        "call under torch.no_grad() for inference")
+def _pad(N):
+    return 64 if N <= 64 else (128 if N <= 128 else 256)
+
+
+def _run_fb(obs, log_P, log_p0, obs_mode, log_beta_T=None, posterior=False):
+    """One hmm355_forward_backward_ex_f32 call; returns (posterior|None, loglik, lik_ref, U, V, LA, LB)."""
+    B, T, N = obs.shape
+    NP = _pad(N)
+    dev = obs.device
+    L = nat.lib()
+    ws = torch.empty(L.hmm355_fb_workspace_bytes(B, T, N), dtype=torch.uint8, device=dev)
+    post = torch.empty(B, T, N, device=dev) if posterior else None
+    loglik = torch.empty(B, device=dev)
+    lik_ref = torch.empty(B, device=dev)
+    with torch.cuda.device(dev):
+        nat.check(L.hmm355_forward_backward_ex_f32(
+            nat.ptr(obs), obs_mode, nat.ptr(log_P), nat.ptr(log_p0), nat.ptr(log_beta_T), B, T, N,
+            nat.FB_POSTERIOR if posterior else 0, nat.ptr(post), None, None, nat.ptr(loglik), nat.ptr(lik_ref),
+            nat.ptr(ws), ws.numel(), nat.stream_of(dev)))
+    rows = B * T
+    # workspace layout: U | V (B,T,NP) then LA | LB (B,T), pieces 256-B aligned (hmm355.h)
+    fl = ws.view(torch.float32)
+    U = fl[: rows * NP].view(B, T, NP)[..., :N]
+    V = fl[rows * NP: 2 * rows * NP].view(B, T, NP)[..., :N]
+    off = ((2 * rows * NP * 4 + 255) // 256) * 256 // 4
+    LA = fl[off: off + rows].view(B, T)
+    LB = fl[off + rows: off + 2 * rows].view(B, T)
+    return post, loglik, lik_ref, U, V, LA, LB
+
+
+class SequenceLogLik(torch.autograd.Function):
+    """(B,) log-likelihood of each sequence ('ref' or 'exact'), differentiable in obs,
+    log_P and log_p0."""
+
+    @staticmethod
+    def forward(ctx, obs, log_P, log_p0, obs_mode, kind):
+        nat.require_gpu(obs, log_P, log_p0)
+        obs_c, lP, l0 = (t.detach().to(torch.float32).contiguous() for t in (obs, log_P, log_p0))
+        _, loglik, lik_ref, _, _, _, _ = _run_fb(obs_c, lP, l0, obs_mode)
+        ctx.save_for_backward(obs_c, lP, l0)
+        ctx.obs_mode, ctx.kind = obs_mode, kind
+        return lik_ref if kind == "ref" else loglik
+
+    @staticmethod
+    def backward(ctx, gout):
+        obs, lP, l0 = ctx.saved_tensors
+        B, T, N = obs.shape
+        _, _, _, U, _, LA, _ = _run_fb(obs, lP, l0, ctx.obs_mode)
+        a_last = torch.log(U[:, -1]) + LA[:, -1:]                 # log alpha_{T-1}  (B,N)
+        if ctx.kind == "ref":
+            f = torch.exp(a_last)                                 # the reference's forward[:, -1]
+            z = torch.log(f + 1e-8)
+            w = torch.softmax(z, dim=-1)
+            g = w * f / (f + 1e-8)                                # dL/d log alpha_{T-1}
+            log_mu = torch.log(w) - z                             # log(g / alpha_{T-1})
+        else:
+            g = torch.softmax(a_last, dim=-1)
+            log_mu = torch.zeros_like(a_last)
+        G = g.sum(-1) * gout                                      # (B,)
+        post, _, _, U, V, _, _ = _run_fb(obs, lP, l0, ctx.obs_mode, log_beta_T=log_mu.contiguous(),
+                                         posterior=True)
+        grad_lo = G[:, None, None] * post
+        if ctx.obs_mode == nat.OBS_PROB:
+            grad_obs = grad_lo / (obs + 1e-8)
+            e = obs + 1e-8
+        else:
+            grad_obs = grad_lo
+            e = torch.exp(obs)
+        grad_l0 = (G[:, None] * post[:, 0]).sum(0)
+        grad_lP = None
+        if T > 1 and ctx.needs_input_grad[1]:
+            c = U.sum(-1)                                         # c_t = sum_j u_t(j)   (B,T)
+            S = (U * V).sum(-1)                                   # (B,T)
+            X = U[:, :-1] / (c[:, :-1] * S[:, 1:]).unsqueeze(-1) * G[:, None, None]
+            Y = e[:, 1:] * V[:, 1:]
+            M = torch.einsum("bti,btj->ij", X, Y)
+            grad_lP = torch.exp(lP) * M
+        return grad_obs, grad_lP, grad_l0, None, None
+
+
+class _NoPosteriorGrad(torch.autograd.Function):
+    """Carries forward-backward outputs (computed by the kernels) into a graph whose inputs
+    require grad: the values are exact, back-propagating through them raises."""
+
+    @staticmethod
+    def forward(ctx, obs, log_P, log_p0, *outs):
+        return tuple(o.clone() for o in outs)
+
+    @staticmethod
+    def backward(ctx, *grads):
+        raise NotImplementedError(
+            "gradients through forward-backward posteriors are not implemented on the MI355X path; "
+            "differentiate compute_likelihood / compute_loss (unsupervised) instead")
+
+
+def forward_backward_with_grad(obs, log_P, log_p0, outs):
+    return _NoPosteriorGrad.apply(obs, log_P, log_p0, *outs)
+
+
+class GmmLogProb(torch.autograd.Function):
+    """Diagonal-Gaussian (mixture) emission log-probabilities: forward by the gfx950 scorer
+    (ops.gmm_diag_logprob), backward analytic.  With comp[b,t,s,c] the component log-density
+    plus log_w and r = d lp / d comp (softmax over c of the reference's clamped LSE,
+    mixture_gaussian.py:141-155; r = 1 when mix_lse == 0):
+        d/d means   = r g (x - mu) / var          d/d log_vars = r g ((x - mu)^2 / var - 1) / 2
+        d/d x       = -sum_{s,c} r g (x - mu) / var                d/d log_w = r g
+    expanded into GEMMs over the frames (hipBLASLt through torch.matmul), T-chunked."""
+
+    @staticmethod
+    def forward(ctx, x, means, log_vars, log_w, mix_lse):
+        from . import ops
+        lp = ops.gmm_diag_logprob(x.detach(), means.detach(), log_vars.detach(), log_w.detach(), mix_lse)
+        ctx.save_for_backward(x, means, log_vars, log_w, lp)
+        ctx.mix_lse = mix_lse
+        return lp
+
+    @staticmethod
+    def backward(ctx, g):
+        x, means, log_vars, log_w, lp = ctx.saved_tensors
+        B, T, D = x.shape
+        S, C, _ = means.shape
+        mu = means.detach().float().reshape(S * C, D)
+        lv = log_vars.detach().float().reshape(S * C, D)
+        iv = torch.exp(-lv)                                   # 1 / var
+        cst = lv.sum(-1) + D * math.log(2 * math.pi)          # (SC)
+        lw = log_w.detach().float().reshape(S * C)
+        q2 = (mu * mu * iv).sum(-1)                           # sum mu^2 / var
+        gm = torch.zeros_like(mu)      # sum gc (x - mu) / var  pieces
+        gx2 = torch.zeros_like(mu)     # sum gc x^2
+        gx1 = torch.zeros_like(mu)     # sum gc x
+        gsum = torch.zeros(S * C, device=x.device)
+        grad_x = torch.empty_like(x, dtype=torch.float32) if ctx.needs_input_grad[0] else None
+        step = max(1, (1 << 22) // max(1, B * S * C))       # frames-of-T per chunk (bounded temp)
+        xf = x.detach().float()
+        for t0 in range(0, T, step):
+            xc = xf[:, t0:t0 + step].reshape(-1, D)           # (F, D)
+            gl = g[:, t0:t0 + step].reshape(-1, S).float()    # (F, S)
+            maha = (xc * xc) @ iv.t() - 2.0 * (xc @ (mu * iv).t()) + q2   # (F, SC)
+            comp = -0.5 * (maha + cst) + lw
+            if ctx.mix_lse:
+                comp3 = comp.view(-1, S, C)
+                m = comp3.max(-1, keepdim=True)[0]
+                m = torch.where(torch.isinf(m), torch.zeros_like(m), m)
+                ex = torch.exp(comp3 - m)
+                se = ex.sum(-1, keepdim=True)
+                r = torch.where(se > 1e-8, ex / se, torch.zeros_like(ex))   # clamp(min=1e-8) has 0 slope below
+                gc = (r * gl.unsqueeze(-1)).reshape(-1, S * C)
+            else:
+                gc = gl.reshape(-1, S * C)
+            gsum += gc.sum(0)
+            gx1 += gc.t() @ xc
+            gx2 += gc.t() @ (xc * xc)
+            if grad_x is not None:
+                gxx = -(xc * (gc @ iv) - gc @ (mu * iv))
+                grad_x[:, t0:t0 + step] = gxx.view(B, -1, D)
+        grad_means = (gx1 - mu * gsum[:, None]) * iv
+        grad_lv = 0.5 * ((gx2 - 2 * mu * gx1 + mu * mu * gsum[:, None]) * iv - gsum[:, None])
+        return (grad_x, grad_means.view(S, C, D).to(means.dtype), grad_lv.view(S, C, D).to(log_vars.dtype),
+                gsum.view(S, C).to(log_w.dtype), None)
+
+
+class ViterbiScore(torch.autograd.Function):
+    """(states, max_j delta_{T-1}[j]) of the Viterbi recursion (ops.viterbi, OBS_LOG), with the
+    gradient of the score: the reference's max-plus recursion (mixture_gaussian.py:290-338)
+    routes it along the decoded path only — d/d lp[b,t,s_t] = g_b, d/d log_T[s_{t-1},s_t] += g_b."""
+
+    @staticmethod
+    def forward(ctx, lp, log_T, init):
+        from . import ops
+        states, _, final = ops.viterbi(lp.detach(), log_T.detach(), init.detach(), ops.OBS_LOG)
+        ctx.save_for_backward(states)
+        ctx.shapes = (lp.shape, log_T.shape)
+        ctx.mark_non_differentiable(states)
+        return states, final
+
+    @staticmethod
+    def backward(ctx, g_states, g):
+        (states,) = ctx.saved_tensors
+        (B, T, S), _ = ctx.shapes
+        grad_lp = torch.zeros(B, T, S, device=g.device)
+        grad_lp.scatter_(2, states.unsqueeze(-1), g.view(B, 1, 1).expand(B, T, 1).contiguous())
+        grad_T = torch.zeros(S * S, device=g.device)
+        if T > 1:
+            idx = (states[:, :-1] * S + states[:, 1:]).reshape(-1)
+            grad_T.index_add_(0, idx, g.view(B, 1).expand(B, T - 1).reshape(-1))
+        grad_init = torch.zeros(S, device=g.device).index_add_(0, states[:, 0], g)
+        return grad_lp, grad_T.view(S, S), grad_init

@@ -75,11 +75,12 @@ static __global__ void __launch_bounds__(kPrepThreads) band_prep_kernel(const fl
   __shared__ float rfl[kBandN];
   __shared__ int clo_s[kBandN], chi_s[kBandN], rlo_s[kBandN], rhi_s[kBandN];
   __shared__ int red[6];  // wc, wr, cd0, cd1, rd0, rd1
+  __shared__ int dense_s;
   const int tid = threadIdx.x, w = tid >> 6, l = tid & 63;
   constexpr int NWV = kPrepThreads / 64;
   if (kAbl & 16) return;  // diagnostic builds only (tools/ablate.py)
   for (int j = tid; j < kBandN; j += kPrepThreads) { clo_s[j] = rlo_s[j] = 1 << 20; chi_s[j] = rhi_s[j] = -1; }
-  if (tid == 0) { red[0] = red[1] = 0; red[2] = red[4] = 1 << 20; red[3] = red[5] = -(1 << 20); }
+  if (tid == 0) { red[0] = red[1] = 0; red[2] = red[4] = 1 << 20; red[3] = red[5] = -(1 << 20); dense_s = 0; }
   __syncthreads();
   // all of this wave's row loads first (rows w, w + 16, ...), then one DPP min per row
   constexpr int RPW = kBandN / NWV;  // rows per wave (<= 16)
@@ -103,6 +104,18 @@ static __global__ void __launch_bounds__(kPrepThreads) band_prep_kernel(const fl
     for (int k = 1; k < KB; ++k) m = fminf(m, v[rr][k]);
     m = -wave_max_dpp(-m);
     if (l == 0) rfl[i] = m;
+    // a row with more than kBandMax non-floor entries makes the table dense: record that
+    // and skip its hull updates (a dense table would otherwise issue N^2 LDS atomics)
+    int cnt = 0;
+#pragma unroll
+    for (int k = 0; k < KB; ++k) {
+      const int o = l + 64 * k;
+      cnt += __popcll(__ballot(o < N && v[rr][k] != m));
+    }
+    if (cnt > kBandMax) {
+      if (l == 0) dense_s = 1;
+      continue;
+    }
 #pragma unroll
     for (int k = 0; k < KB; ++k) {
       const int o = l + 64 * k;
@@ -137,7 +150,7 @@ static __global__ void __launch_bounds__(kPrepThreads) band_prep_kernel(const fl
     }
   }
   __syncthreads();
-  const int wc = red[0], wr = red[1];
+  const int wc = dense_s ? kBandN : red[0], wr = dense_s ? kBandN : red[1];
   const int wcp = band_pad(wc), wrp = band_pad(wr);
   int cd0 = red[2], cd1 = red[3], rd0 = red[4], rd1 = red[5];
   if (cd1 < cd0) { cd0 = 0; cd1 = 0; }  // all-floor table: any range fits

@@ -121,23 +121,68 @@ static hipError_t launch_fb(const RecArgs& fa, const RecArgs& fb, const PostArgs
   return hipGetLastError();
 }
 
+// Workspace layout (documented in include/hmm355.h for adjoint callers):
+//   U (B,T,NP) | V (B,T,NP) | LA (B,T) | LB (B,T) | BandDesc | beta init (B,NP) | its scale (B)
+struct FbWs {
+  float *U, *V, *LA, *LB, *binit, *bscale;
+  BandDesc* band;
+};
+static size_t fb_ws_layout(int B, int T, int N, char* base, FbWs* w) {
+  const size_t NP = pad_states(N);
+  const size_t rows = (size_t)B * T;
+  size_t off = 0;
+  auto take = [&](size_t bytes) { const size_t o = off; off += align_up(bytes, 256); return o; };
+  const size_t oU = take(2 * rows * NP * sizeof(float));
+  const size_t oL = take(2 * rows * sizeof(float));
+  const size_t oD = take(sizeof(BandDesc));
+  const size_t oI = take((size_t)B * NP * sizeof(float));
+  const size_t oS = take((size_t)B * sizeof(float));
+  if (w && base) {
+    w->U = reinterpret_cast<float*>(base + oU);
+    w->V = w->U + rows * NP;
+    w->LA = reinterpret_cast<float*>(base + oL);
+    w->LB = w->LA + rows;
+    w->band = reinterpret_cast<BandDesc*>(base + oD);
+    w->binit = reinterpret_cast<float*>(base + oI);
+    w->bscale = reinterpret_cast<float*>(base + oS);
+  }
+  return off;
+}
+
+// terminal backward vector from its logarithm: binit = exp(l - max l) (padded states 0),
+// bscale = max l.  One wave per sequence.
+template <int NP>
+__global__ void __launch_bounds__(64) beta_init_kernel(const float* __restrict__ lbt, int N, float* binit, float* bscale) {
+  const int b = blockIdx.x, l = threadIdx.x;
+  constexpr int K = NP / 64;
+  float v[K], m = -INFINITY;
+#pragma unroll
+  for (int k = 0; k < K; ++k) {
+    const int j = l + 64 * k;
+    v[k] = j < N ? lbt[(size_t)b * N + j] : -INFINITY;
+    m = fmaxf(m, v[k]);
+  }
+  m = wave_max(m);
+  if (m == -INFINITY) m = 0.f;  // an all-zero terminal vector: every adjoint is 0
+#pragma unroll
+  for (int k = 0; k < K; ++k) binit[(size_t)b * NP + l + 64 * k] = (l + 64 * k < N) ? __expf(v[k] - m) : 0.f;
+  if (l == 0) bscale[b] = m;
+}
+
 }  // namespace hmm355
 
 using namespace hmm355;
 
 HMM355_API size_t hmm355_fb_workspace_bytes(int B, int T, int N) {
   if (B < 0 || T < 1 || N < 1 || N > 256) return 0;
-  const size_t NP = pad_states(N);
-  const size_t rows = (size_t)B * T;
-  return align_up(2 * rows * NP * sizeof(float), 256) + align_up(2 * rows * sizeof(float), 256) +
-         align_up(sizeof(BandDesc), 256);
+  return fb_ws_layout(B, T, N, nullptr, nullptr);
 }
 
-HMM355_API int hmm355_forward_backward_f32(const float* obs, int obs_mode, const float* log_P,
-                                           const float* log_p0, int B, int T, int N, unsigned out_mask,
-                                           float* posterior, float* forward, float* backward, float* loglik,
-                                           float* lik_ref, void* workspace, size_t workspace_bytes,
-                                           void* stream) {
+HMM355_API int hmm355_forward_backward_ex_f32(const float* obs, int obs_mode, const float* log_P,
+                                              const float* log_p0, const float* log_beta_T, int B, int T, int N,
+                                              unsigned out_mask, float* posterior, float* forward, float* backward,
+                                              float* loglik, float* lik_ref, void* workspace,
+                                              size_t workspace_bytes, void* stream) {
   if (B < 0 || N < 0) return HMM355_E_ARG;
   if (N < 1 || N > 256) return HMM355_E_STATES;
   if (T < 1) return HMM355_E_SHAPE;
@@ -150,19 +195,26 @@ HMM355_API int hmm355_forward_backward_f32(const float* obs, int obs_mode, const
   if ((size_t)B * T > (size_t)1 << 40) return HMM355_E_SHAPE;
   if (workspace_bytes < hmm355_fb_workspace_bytes(B, T, N)) return HMM355_E_WORKSPACE;
   const int NP = pad_states(N);
-  const size_t rows = (size_t)B * T;
-  char* ws = static_cast<char*>(workspace);
-  float* U = reinterpret_cast<float*>(ws);
-  float* V = U + rows * NP;
-  float* LA = reinterpret_cast<float*>(ws + align_up(2 * rows * NP * sizeof(float), 256));
-  float* LB = LA + rows;
-  BandDesc* band = use_band() ? reinterpret_cast<BandDesc*>(ws + align_up(2 * rows * NP * sizeof(float), 256) +
-                                                           align_up(2 * rows * sizeof(float), 256))
-                              : nullptr;
-  RecArgs fa{obs, log_P, log_p0, U, LA, loglik, B, T, N, obs_mode, NP, band};
-  RecArgs fb{obs, log_P, log_p0, V, LB, nullptr, B, T, N, obs_mode, NP, band};
-  PostArgs pa{U, V, LA, LB, posterior, forward, backward, lik_ref, B, T, N, out_mask};
+  FbWs w;
+  fb_ws_layout(B, T, N, static_cast<char*>(workspace), &w);
+  BandDesc* band = use_band() ? w.band : nullptr;
   hipStream_t st = static_cast<hipStream_t>(stream);
+  const float* binit = nullptr;
+  const float* bscale = nullptr;
+  if (log_beta_T) {
+    switch (NP) {
+      case 64: hipLaunchKernelGGL(beta_init_kernel<64>, dim3(B), dim3(64), 0, st, log_beta_T, N, w.binit, w.bscale); break;
+      case 128: hipLaunchKernelGGL(beta_init_kernel<128>, dim3(B), dim3(64), 0, st, log_beta_T, N, w.binit, w.bscale); break;
+      default: hipLaunchKernelGGL(beta_init_kernel<256>, dim3(B), dim3(64), 0, st, log_beta_T, N, w.binit, w.bscale); break;
+    }
+    const hipError_t e0 = hipGetLastError();
+    if (e0 != hipSuccess) return (int)e0;
+    binit = w.binit;
+    bscale = w.bscale;
+  }
+  RecArgs fa{obs, log_P, log_p0, w.U, w.LA, loglik, B, T, N, obs_mode, NP, band, nullptr, nullptr};
+  RecArgs fb{obs, log_P, log_p0, w.V, w.LB, nullptr, B, T, N, obs_mode, NP, band, binit, bscale};
+  PostArgs pa{w.U, w.V, w.LA, w.LB, posterior, forward, backward, lik_ref, B, T, N, out_mask};
   hipError_t e;
   switch (NP) {
     case 64: e = launch_fb<64>(fa, fb, pa, st); break;
@@ -170,6 +222,15 @@ HMM355_API int hmm355_forward_backward_f32(const float* obs, int obs_mode, const
     default: e = launch_fb<256>(fa, fb, pa, st); break;
   }
   return e == hipSuccess ? HMM355_OK : (int)e;
+}
+
+HMM355_API int hmm355_forward_backward_f32(const float* obs, int obs_mode, const float* log_P,
+                                           const float* log_p0, int B, int T, int N, unsigned out_mask,
+                                           float* posterior, float* forward, float* backward, float* loglik,
+                                           float* lik_ref, void* workspace, size_t workspace_bytes,
+                                           void* stream) {
+  return hmm355_forward_backward_ex_f32(obs, obs_mode, log_P, log_p0, nullptr, B, T, N, out_mask, posterior, forward,
+                                        backward, loglik, lik_ref, workspace, workspace_bytes, stream);
 }
 
 #if HMM355_STAMP

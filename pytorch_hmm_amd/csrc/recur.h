@@ -177,6 +177,8 @@ struct RecArgs {
   float* loglik;      // (B) sequence log-likelihood (FB alpha) or null
   int B, T, N, obs_mode, row_stride;
   const BandDesc* band;  // banded decomposition (band.h) or null: dense chain
+  const float* binit;    // backward only: (B,NP) terminal vector (max-normalised) or null = ones
+  const float* bscale;   // backward only: (B) log-scale of binit
 };
 
 template <int KIND>
@@ -289,14 +291,14 @@ __device__ __forceinline__ void rec_run(const RecArgs& a, float* lds, int b) {
     float v0;
     const int oo = o < N ? o : 0;
     if (KIND == kFbAlpha) v0 = o < N ? __expf(a.init[oo]) * emis(0, o) : 0.f;  // alpha_0 = p0 * e_0
-    else if (KIND == kFbBeta) v0 = o < N ? 1.f : 0.f;                             // beta_{T-1} = 1
+    else if (KIND == kFbBeta) v0 = o < N ? (a.binit ? a.binit[(size_t)b * NP + o] : 1.f) : 0.f;  // beta_{T-1}
     else v0 = o < N ? a.init[oo] + emis(0, o) : -INFINITY;                      // delta_0 = init + lo_0
     const float ident = FB ? 0.f : -INFINITY;
     if (r < 2) lds[C::OFF_PART + o * 2 + r] = r == 0 ? v0 : ident;
   }
   lds_barrier();
 
-  double base = 0.0;
+  double base = (KIND == kFbBeta && a.bscale) ? (double)a.bscale[b] : 0.0;
   unsigned long long st_acc[4] = {0, 0, 0, 0}, st_prev = 0, st_t0 = 0, st_steps = 0;
   long long rt0 = 0;
   if (kStamp) { st_t0 = stamp(); st_prev = st_t0; rt0 = __builtin_amdgcn_s_memrealtime(); }
@@ -484,7 +486,7 @@ __device__ __forceinline__ void rec_band(const RecArgs& a, float* lds, int b, co
   if (w > NH) return;
   const int T = a.T, N = a.N;
   const int nblocks = (T + 15) / 16;
-  double base = 0.0;
+  double base = (KIND == kFbBeta && a.bscale) ? (double)a.bscale[b] : 0.0;
 
   // prologue: the helpers stage block 0 and load block 1
   float er0[HV][4], er1[HV][4];
@@ -549,7 +551,7 @@ __device__ __forceinline__ void rec_band(const RecArgs& a, float* lds, int b, co
         const int s = NB * l + j;
         const int ss = s < N ? s : 0;
         if (KIND == kFbAlpha) y[j] = s < N ? __expf(a.init[ss]) * e0[j] : 0.f;
-        else if (KIND == kFbBeta) y[j] = s < N ? 1.f : 0.f;
+        else if (KIND == kFbBeta) y[j] = s < N ? (a.binit ? a.binit[(size_t)b * NP + s] : 1.f) : 0.f;
         else y[j] = s < N ? a.init[ss] + e0[j] : -INFINITY;
       }
     }

@@ -318,7 +318,8 @@ static hipError_t launch_vit(const VitArgs& va, hipStream_t sm) {
     e = launch_band_prep(va.log_P, va.N, const_cast<BandDesc*>(va.band), sm);
     if (e != hipSuccess) return e;
   }
-  RecArgs ra{va.obs, va.log_P, va.init, va.delta, nullptr, nullptr, va.B, va.T, va.N, va.obs_mode, va.N, va.band};
+  RecArgs ra{va.obs, va.log_P, va.init, va.delta, nullptr, nullptr, va.B, va.T, va.N, va.obs_mode, va.N, va.band,
+             nullptr, nullptr};
   hipLaunchKernelGGL(vit_fwd_kernel<NP>, dim3(va.B), dim3(RC<NP>::NT), kExclusiveLds, sm, ra);
   e = hipGetLastError();
   if (e != hipSuccess) return e;

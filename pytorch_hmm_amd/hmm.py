@@ -12,7 +12,7 @@ import numpy as np
 import torch
 
 from . import ops
-from .autograd import forward_backward_with_grad, needs_grad
+from .autograd import SequenceLogLik, forward_backward_with_grad, needs_grad
 
 
 class HMM:
@@ -73,10 +73,11 @@ class HMMPyTorch(HMM):
         B, T, K = obs.shape
         assert K == self.K, f"Observation dim {K} must match model states {self.K}"
         log_P, log_p0 = self._params_for(obs)
-        if needs_grad(obs, log_P, log_p0):
-            return forward_backward_with_grad(obs, log_P, log_p0)
         post, fwd, bwd, _, _ = ops.forward_backward(
-            obs, log_P, log_p0, ops.OBS_PROB, ops.FB_POSTERIOR | ops.FB_FORWARD | ops.FB_BACKWARD)
+            obs.detach(), log_P.detach(), log_p0.detach(), ops.OBS_PROB,
+            ops.FB_POSTERIOR | ops.FB_FORWARD | ops.FB_BACKWARD)
+        if needs_grad(obs, log_P, log_p0):
+            post, fwd, bwd = forward_backward_with_grad(obs, log_P, log_p0, (post, fwd, bwd))
         return post, fwd, bwd
 
     def posteriors(self, observations: torch.Tensor) -> torch.Tensor:
@@ -84,9 +85,11 @@ class HMMPyTorch(HMM):
         obs, _ = self._as_batch(observations)
         assert obs.shape[-1] == self.K, f"Observation dim {obs.shape[-1]} must match model states {self.K}"
         log_P, log_p0 = self._params_for(obs)
+        post = ops.forward_backward(obs.detach(), log_P.detach(), log_p0.detach(), ops.OBS_PROB,
+                                    ops.FB_POSTERIOR)[0]
         if needs_grad(obs, log_P, log_p0):
-            return forward_backward_with_grad(obs, log_P, log_p0)[0]
-        return ops.forward_backward(obs, log_P, log_p0, ops.OBS_PROB, ops.FB_POSTERIOR)[0]
+            (post,) = forward_backward_with_grad(obs, log_P, log_p0, (post,))
+        return post
 
     def viterbi_decode(self, observations: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor]:
         """(states (B,T) int64, log_delta (B,T,K)); 2-D input squeezed (hmm.py:132-184)."""
@@ -107,8 +110,7 @@ class HMMPyTorch(HMM):
         assert K == self.K, f"Observation dim {K} must match model states {self.K}"
         log_P, log_p0 = self._params_for(obs)
         if needs_grad(obs, log_P, log_p0):
-            _, fwd, _ = forward_backward_with_grad(obs, log_P, log_p0)
-            ll = torch.logsumexp(torch.log(fwd[:, -1] + 1e-8), dim=-1)
+            ll = SequenceLogLik.apply(obs, log_P, log_p0, ops.OBS_PROB, "ref")
         else:
             ll = ops.forward_backward(obs, log_P, log_p0, ops.OBS_PROB, 0)[4]
         return ll.squeeze(0) if squeeze else ll
@@ -119,7 +121,10 @@ class HMMPyTorch(HMM):
         obs, squeeze = self._as_batch(observations)
         assert obs.shape[-1] == self.K, f"Observation dim {obs.shape[-1]} must match model states {self.K}"
         log_P, log_p0 = self._params_for(obs)
-        ll = ops.forward_backward(obs, log_P, log_p0, ops.OBS_PROB, 0)[3]
+        if needs_grad(obs, log_P, log_p0):
+            ll = SequenceLogLik.apply(obs, log_P, log_p0, ops.OBS_PROB, "exact")
+        else:
+            ll = ops.forward_backward(obs, log_P, log_p0, ops.OBS_PROB, 0)[3]
         return ll.squeeze(0) if squeeze else ll
 
     def sample(self, seq_length: int, batch_size: int = 1) -> Tuple[torch.Tensor, torch.Tensor]:

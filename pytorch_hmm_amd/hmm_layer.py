@@ -15,6 +15,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from . import ops
+from .autograd import GmmLogProb, needs_grad
 from .hmm import HMMPyTorch
 from .utils import create_left_to_right_matrix, create_transition_matrix
 
@@ -158,10 +159,12 @@ class GaussianHMMLayer(nn.Module):
         """(B,T,D) -> (B,T,K) Gaussian log-densities on the gfx950 scorer
         (hmm_layer.py:270-323)."""
         B, T, D = observations.shape
+        log_w = torch.zeros(self.num_states, 1, device=self.means.device)
+        if needs_grad(observations, self.means, self.log_scales):
+            lv = _gaussian_component_params(self.log_scales, self.covariance_type, D)
+            return GmmLogProb.apply(observations, self.means.unsqueeze(1), lv, log_w, 0)
         lv = _gaussian_component_params(self.log_scales.detach(), self.covariance_type, D)
-        means = self.means.detach().unsqueeze(1)                     # (K,1,D)
-        log_w = torch.zeros(self.num_states, 1, device=means.device)
-        return ops.gmm_diag_logprob(observations.detach(), means, lv, log_w, 0)
+        return ops.gmm_diag_logprob(observations.detach(), self.means.detach().unsqueeze(1), lv, log_w, 0)
 
     def forward(self, observations: torch.Tensor) -> torch.Tensor:
         observation_probs = torch.exp(self._compute_gaussian_log_probs(observations))

@@ -17,6 +17,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from . import ops
+from .autograd import GmmLogProb, needs_grad
 
 
 class HSMMLayer(nn.Module):
@@ -82,10 +83,13 @@ class HSMMLayer(nn.Module):
     def get_observation_log_probs(self, observations: torch.Tensor) -> torch.Tensor:
         """(B,T,D) -> (B,T,S) diagonal-Gaussian log-densities (hsmm.py:181-206)."""
         S = self.num_states
+        zeros = torch.zeros(S, 1, device=observations.device)
+        if needs_grad(observations, self.observation_means, self.observation_log_vars):
+            return GmmLogProb.apply(observations, self.observation_means.unsqueeze(1),
+                                    self.observation_log_vars.unsqueeze(1), zeros, 0)
         with torch.no_grad():
             return ops.gmm_diag_logprob(observations, self.observation_means.unsqueeze(1),
-                                        self.observation_log_vars.unsqueeze(1),
-                                        torch.zeros(S, 1, device=observations.device), 0)
+                                        self.observation_log_vars.unsqueeze(1), zeros, 0)
 
     # -- decoding (hsmm.py:208-354) -------------------------------------------------------
     def viterbi_decode_hsmm(self, observations: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor]:
@@ -93,8 +97,8 @@ class HSMMLayer(nn.Module):
         B, T, _ = observations.shape
         if T > 1000:
             warnings.warn(f"Long sequence ({T} frames) may cause memory issues in HSMM decoding.")
-        obs_log_probs = self.get_observation_log_probs(observations)
-        with torch.no_grad():
+        with torch.no_grad():  # the segment Viterbi is not differentiated (as in the reference)
+            obs_log_probs = self.get_observation_log_probs(observations)
             dur_lp = torch.log(self.get_duration_probabilities() + self.eps)
             log_T = torch.log(self.get_transition_matrix() + self.eps)
         if dur_lp.shape[1] < self.max_duration:

@@ -19,6 +19,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from . import ops
+from .autograd import GmmLogProb, ViterbiScore, needs_grad
 
 
 class MixtureGaussianHMMLayer(nn.Module):
@@ -97,6 +98,9 @@ class MixtureGaussianHMMLayer(nn.Module):
         if T > self.max_sequence_length:
             warnings.warn(f"Sequence length {T} exceeds recommended maximum "
                           f"{self.max_sequence_length}. Consider chunked processing.")
+        if needs_grad(observations, *self.parameters()):
+            log_w = self._safe_log(F.softmax(self.mixture_weights_logits, dim=-1))
+            return GmmLogProb.apply(observations, self.means, self._component_log_vars(), log_w, 1)
         with torch.no_grad():
             log_w = self._safe_log(F.softmax(self.mixture_weights_logits, dim=-1))
             return ops.gmm_diag_logprob(observations, self.means, self._component_log_vars(), log_w, 1)
@@ -107,14 +111,16 @@ class MixtureGaussianHMMLayer(nn.Module):
         (mixture_gaussian.py:290-338)."""
         S = obs_log_probs.shape[-1]
         init = -(torch.zeros(S, device=obs_log_probs.device) + math.log(S))
+        if needs_grad(obs_log_probs, log_transitions):
+            # the score's gradient follows the decoded path (the reference's max-plus autograd)
+            return ViterbiScore.apply(obs_log_probs, log_transitions, init)
         states, _, final = ops.viterbi(obs_log_probs, log_transitions, init, ops.OBS_LOG)
         return states, final
 
     def forward(self, observations: torch.Tensor,
                 return_log_probs: bool = False) -> Tuple[torch.Tensor, Optional[torch.Tensor]]:
         obs_log_probs = self.get_observation_log_probs(observations)
-        with torch.no_grad():
-            log_transitions = self._safe_log(self.get_transition_matrix())
+        log_transitions = self._safe_log(self.get_transition_matrix())
         states, scores = self._viterbi_decode(obs_log_probs, log_transitions)
         return (states, scores) if return_log_probs else (states, None)
 

@@ -49,7 +49,7 @@ def test_gaussian_layer(name, K, D, seed):
     torch.manual_seed(seed)
     layer = ph.GaussianHMMLayer(K, D).to(DEV)
     x = t(g["x"])
-    lp = layer._compute_gaussian_log_probs(x).cpu().numpy()
+    lp = layer._compute_gaussian_log_probs(x).detach().cpu().numpy()
     np.testing.assert_allclose(lp, g["log_probs"], rtol=2e-6, atol=2e-5)
     layer.train()
     post = layer(x)
@@ -67,9 +67,11 @@ def test_mixture_layer(name, S, D, C, seed):
     torch.manual_seed(seed)
     m = ph.MixtureGaussianHMMLayer(S, D, num_components=C).to(DEV)
     x = t(g["x"])
-    lp = m.get_observation_log_probs(x)
+    with torch.no_grad():
+        lp = m.get_observation_log_probs(x)
     np.testing.assert_allclose(lp.cpu().numpy(), g["log_probs"], rtol=2e-6, atol=2e-5)
-    states, scores = m(x, return_log_probs=True)
+    states, scores = m(x, return_log_probs=True)   # grad-enabled path (ViterbiScore)
+    scores = scores.detach()
     assert np.array_equal(states.cpu().numpy(), g["states"])
     np.testing.assert_allclose(scores.cpu().numpy(), g["scores"], rtol=2e-6)
     s2, none = m(x)
@@ -83,7 +85,8 @@ def test_hsmm_layer(name, S, D, Dm, seed):
     torch.manual_seed(seed)
     h = ph.HSMMLayer(S, D, max_duration=Dm).to(DEV)
     x = t(g["x"])
-    np.testing.assert_allclose(h.get_observation_log_probs(x).cpu().numpy(), g["log_probs"], rtol=2e-6, atol=2e-5)
+    np.testing.assert_allclose(h.get_observation_log_probs(x).detach().cpu().numpy(), g["log_probs"],
+                               rtol=2e-6, atol=2e-5)
     states, scores = h(x)
     assert np.array_equal(states.cpu().numpy(), g["states"])
     np.testing.assert_allclose(scores.cpu().numpy(), g["scores"], rtol=2e-6)
