@@ -17,10 +17,11 @@
 //   obs_sum is torch-CPU's order for a strided slice of length d: four accumulators over
 //   whole groups of 4, the tail folded into the first, then ((a0+a1)+a2)+a3.
 //
-// hsmm_fwd_kernel: one 256-thread workgroup per sequence, 3 barriers per start time:
+// hsmm_fwd_kernel: one 1024-thread workgroup per sequence (16 lanes = one DPP row per
+// state), 3 barriers per start time:
 //   A  group-complete updates of the per-(start,state) accumulators F0..F3 (LDS ring);
 //   B  the S x Dmax candidate values delta[st-1][s'][d'] and their max over d';
-//   C  M[st][s], p1 and xb (4 lanes per s, quad DPP combines).
+//   C  M[st][s], p1 and xb (row-wide DPP combines).
 //   lp rows arrive 64 at a time into a 128-row LDS ring, prefetched a chunk ahead.
 // hsmm_backtrace_kernel: one wave per sequence walks the segments (hsmm.py:331-352).
 #include "common.h"
@@ -30,7 +31,8 @@ namespace hmm355 {
 constexpr int kHsS = 64;    // max states
 constexpr int kHsR = 64;    // start-time ring (>= Dmax + 1)
 constexpr int kHsL = 128;   // lp row ring
-constexpr int kHsThreads = 256;
+constexpr int kHsSub = 16;                 // lanes per state in phases B/C (one DPP row)
+constexpr int kHsThreads = kHsS * kHsSub;  // 1024
 
 struct HsArgs {
   const float* lp;      // (B,T,S)
@@ -76,28 +78,48 @@ __device__ __forceinline__ float hs_obs_sum(const HsLds& L, int st0, int d, int 
   return r;
 }
 
+// all-reduce over the 16 lanes of a DPP row (the SUB lanes of one state)
+__device__ __forceinline__ float row_max16(float v) {
+  v = fmaxf(v, dpp_f<0xB1>(v));
+  v = fmaxf(v, dpp_f<0x4E>(v));
+  v = fmaxf(v, dpp_f<0x124>(v));
+  return fmaxf(v, dpp_f<0x128>(v));
+}
+__device__ __forceinline__ int row_min16_i(int v) {
+  v = min(v, dpp_i<0xB1>(v));
+  v = min(v, dpp_i<0x4E>(v));
+  v = min(v, dpp_i<0x124>(v));
+  return min(v, dpp_i<0x128>(v));
+}
+
 __global__ void __launch_bounds__(kHsThreads) hsmm_fwd_kernel(HsArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   HsLds& L = *reinterpret_cast<HsLds*>(smem);
   const int b = blockIdx.x, tid = threadIdx.x;
   const int T = a.T, S = a.S, Dm = a.Dm;
   const float* lp = a.lp + (size_t)b * T * S;
-  const int q = tid >> 2, sub = tid & 3;  // (state, quarter) for phases B/C
+  // phases B/C: 16 lanes (one DPP row) per state q; lane `sub` owns d' = sub + 1 + 16j and
+  // s' = sub + 16j
+  const int q = tid >> 4, sub = tid & 15;
+  constexpr int NJ = kHsR / kHsSub;  // 4
 
   for (int i = tid; i < S * S; i += kHsThreads) L.logT[i / S][i % S] = a.logT[i];
-  // duration log-probs this lane needs in phase B: d' = sub + 1 + 4j
-  float du[16];
+  float du[NJ];
 #pragma unroll
-  for (int j = 0; j < 16; ++j) {
-    const int d = sub + 1 + 4 * j;
+  for (int j = 0; j < NJ; ++j) {
+    const int d = sub + 1 + kHsSub * j;
     const bool ok = q < S && d <= Dm;
     const float v = a.dur[ok ? (size_t)q * Dm + d - 1 : 0];
     du[j] = ok ? v : 0.f;
   }
-  // lp chunk 0 (and chunk 1 into registers)
-  auto chunk_load = [&](int c, float (&r)[kHsS * 64 / kHsThreads]) {
+  // phase-A item walk without integer division in the loop
+  const int a_k0 = tid / S, a_s0 = tid % S;
+  const int a_dk = kHsThreads / S, a_ds = kHsThreads % S;
+
+  constexpr int PER = kHsS * 64 / kHsThreads;  // lp values per thread per 64-row chunk
+  auto chunk_load = [&](int c, float (&r)[PER]) {
 #pragma unroll
-    for (int k = 0; k < kHsS * 64 / kHsThreads; ++k) {
+    for (int k = 0; k < PER; ++k) {
       const int idx = tid + k * kHsThreads;
       const int row = c * 64 + idx / kHsS, col = idx % kHsS;
       const bool ok = row < T && col < S;
@@ -105,35 +127,29 @@ __global__ void __launch_bounds__(kHsThreads) hsmm_fwd_kernel(HsArgs a) {
       r[k] = ok ? v : 0.f;
     }
   };
-  auto chunk_store = [&](int c, const float (&r)[kHsS * 64 / kHsThreads]) {
+  auto chunk_store = [&](int c, const float (&r)[PER]) {
 #pragma unroll
-    for (int k = 0; k < kHsS * 64 / kHsThreads; ++k) {
+    for (int k = 0; k < PER; ++k) {
       const int idx = tid + k * kHsThreads;
       const int row = c * 64 + idx / kHsS, col = idx % kHsS;
       L.lpr[row % kHsL][col] = r[k];
     }
   };
-  float rc[kHsS * 64 / kHsThreads];
+  float rc[PER];
   chunk_load(0, rc);
   chunk_store(0, rc);
   if (T > 64) chunk_load(1, rc);
   __syncthreads();
 
-  // st = 0 has no M (the init formula); mark it so the candidate code takes that branch
-  for (int st = 1; st <= T; ++st) {
-    // ---- lp chunk pipeline: at the first step of chunk c (rows 64c..), stage chunk c+1
-    if ((st & 63) == 0) {
-      const int c = st >> 6;
-      chunk_store(c, rc);  // chunk c was loaded one chunk ago
-      if ((c + 1) * 64 < T) chunk_load(c + 1, rc);
-    }
-    // ---- A: new element row st-1 joins every active start; complete groups fold into F
-    {
-      const int e = st - 1;
-      for (int idx = tid; idx < (Dm + 0) * S; idx += kHsThreads) {
-        const int k = idx / S, sp = idx % S;
-        const int st0 = e - k;  // start whose element index k is row e
-        if (st0 < 0) continue;
+  // ---- A(st): element row st-1 joins every active start; complete groups fold into F.
+  // Runs for st = 1 before the loop and for st + 1 in the same phase as C(st) (they touch
+  // disjoint LDS), so a start costs two barriers: A+C | B.
+  auto phaseA = [&](int st) {
+    const int e = st - 1;
+    int k = a_k0, sp = a_s0;
+    while (k < Dm) {
+      const int st0 = e - k;  // start whose element index k is row e
+      if (st0 >= 0) {
         float* Fv = L.F[st0 % kHsR][sp];
         if (k == 0) { Fv[0] = 0.f; Fv[1] = 0.f; Fv[2] = 0.f; Fv[3] = 0.f; }
         if ((k & 3) == 3) {  // group [k-3, k] complete
@@ -143,31 +159,39 @@ __global__ void __launch_bounds__(kHsThreads) hsmm_fwd_kernel(HsArgs a) {
           Fv[3] += L.lpr[(st0 + k) % kHsL][sp];
         }
       }
+      k += a_dk;
+      sp += a_ds;
+      if (sp >= S) { sp -= S; ++k; }
     }
-    __syncthreads();
-    // ---- B: candidates delta[st-1][s'][d'-1], d' = sub+1+4j, and max over d'
+  };
+  phaseA(1);
+  __syncthreads();
+
+  for (int st = 1; st <= T; ++st) {
+    // ---- B: candidates delta[st-1][s'][d'-1] and their max over d'
     const int dlim = Dm < st ? Dm : st;
     if (q < S) {
       float mx = -INFINITY;
 #pragma unroll
-      for (int j = 0; j < 16; ++j) {
-        const int d = sub + 1 + 4 * j;
-        if (d > Dm) break;
-        float v = -INFINITY;
-        if (d <= dlim) {
-          const int st0 = st - d;
-          const float o = hs_obs_sum(L, st0, d, q);
-          if (st0 == 0) {
-            v = o + du[j];
-          } else {
-            const float m = L.Mr[st0 % kHsR][q];
-            v = (m == -INFINITY) ? -INFINITY : (m + o) + du[j];
+      for (int j = 0; j < NJ; ++j) {
+        const int d = sub + 1 + kHsSub * j;
+        if (d <= Dm) {
+          float v = -INFINITY;
+          if (d <= dlim) {
+            const int st0 = st - d;
+            const float o = hs_obs_sum(L, st0, d, q);
+            if (st0 == 0) {
+              v = o + du[j];
+            } else {
+              const float m = L.Mr[st0 % kHsR][q];
+              v = (m == -INFINITY) ? -INFINITY : (m + o) + du[j];
+            }
           }
+          L.cand[q][d - 1] = v;
+          mx = fmaxf(mx, v);
         }
-        L.cand[q][d - 1] = v;
-        mx = fmaxf(mx, v);
       }
-      mx = quad_max(mx);
+      mx = row_max16(mx);
       if (sub == 0) L.dmx[q] = mx;
     }
     __syncthreads();
@@ -177,47 +201,50 @@ __global__ void __launch_bounds__(kHsThreads) hsmm_fwd_kernel(HsArgs a) {
       const int s = q;
       float lm = -INFINITY;
       int ls = 0x7fff;
-      for (int j = 0; j < 16; ++j) {
-        const int sp = sub + 4 * j;
-        if (sp >= S) break;
-        const float dm = L.dmx[sp];
-        const float v = (sp == s || dm == -INFINITY) ? -INFINITY : dm + L.logT[sp][s];
-        if (v > lm) { lm = v; ls = sp; }
-      }
-      const float M = quad_max(lm);
-      int s1 = quad_min_i(lm == M && M != -INFINITY ? ls : 0x7fff);
-      float xb1 = -INFINITY;
-      int d1 = 0x7fff;
-      float xb2 = -INFINITY;
-      if (M != -INFINITY) {
-        for (int j = 0; j < 16; ++j) {
-          const int sp = sub + 4 * j;
-          if (sp >= s1) break;
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) {
+        const int sp = sub + kHsSub * j;
+        if (sp < S) {
           const float dm = L.dmx[sp];
           const float v = (sp == s || dm == -INFINITY) ? -INFINITY : dm + L.logT[sp][s];
-          xb1 = fmaxf(xb1, v);
+          if (v > lm) { lm = v; ls = sp; }
+        }
+      }
+      const float M = row_max16(lm);
+      int s1 = row_min16_i(lm == M && M != -INFINITY ? ls : 0x7fff);
+      float xb1 = -INFINITY, xb2 = -INFINITY;
+      int d1 = 0x7fff;
+      if (M != -INFINITY) {
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) {
+          const int sp = sub + kHsSub * j;
+          if (sp < s1) {
+            const float dm = L.dmx[sp];
+            const float v = (sp == s || dm == -INFINITY) ? -INFINITY : dm + L.logT[sp][s];
+            xb1 = fmaxf(xb1, v);
+          }
         }
         const float lt = L.logT[s1][s];
         int ld = 0x7fff;
-        for (int j = 0; j < 16; ++j) {
-          const int d = sub + 1 + 4 * j;
-          if (d > Dm) break;
-          const float c = L.cand[s1][d - 1];
-          const float v = c == -INFINITY ? -INFINITY : c + lt;
-          if (v == M && ld == 0x7fff) ld = d;
+        float cv[NJ];
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) {
+          const int d = sub + 1 + kHsSub * j;
+          const float c = d <= Dm ? L.cand[s1][d - 1] : -INFINITY;
+          cv[j] = c == -INFINITY ? -INFINITY : c + lt;
+          if (d <= Dm && cv[j] == M && ld == 0x7fff) ld = d;
         }
-        d1 = quad_min_i(ld);
-        for (int j = 0; j < 16; ++j) {
-          const int d = sub + 1 + 4 * j;
-          if (d >= d1 || d > Dm) break;
-          const float c = L.cand[s1][d - 1];
-          xb2 = fmaxf(xb2, c == -INFINITY ? -INFINITY : c + lt);
+        d1 = row_min16_i(ld);
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) {
+          const int d = sub + 1 + kHsSub * j;
+          if (d < d1 && d <= Dm) xb2 = fmaxf(xb2, cv[j]);
         }
       } else {
         s1 = 0;
         d1 = 0;  // literal: psi never written (hsmm.py:313)
       }
-      const float xb = quad_max(fmaxf(xb1, xb2));
+      const float xb = row_max16(fmaxf(xb1, xb2));
       if (sub == 0) {
         L.Mr[st % kHsR][s] = M;
         const size_t gi = ((size_t)b * T + st) * S + s;
@@ -226,20 +253,36 @@ __global__ void __launch_bounds__(kHsThreads) hsmm_fwd_kernel(HsArgs a) {
         a.XB[gi] = xb;
       }
     }
+    if ((st + 1) % 64 == 0) {  // chunk c = (st+1)/64 holds row st, which A(st+1) needs
+      const int c = (st + 1) >> 6;
+      chunk_store(c, rc);
+      if ((c + 1) * 64 < T) chunk_load(c + 1, rc);
+    }
+    phaseA(st + 1);
     __syncthreads();
   }
-  // final: best over (s asc, d asc) of delta[T-1][s][d-1], strict > (hsmm.py:319-329)
-  if (tid == 0) {
-    float best = -INFINITY;
-    int fs = 0, fd = 1;
-    for (int s = 0; s < S; ++s)
-      for (int d = 1; d <= Dm; ++d) {
-        const float v = L.cand[s][d - 1];
-        if (v > best) { best = v; fs = s; fd = d; }
-      }
-    a.scores[b] = best;
-    a.fin[2 * b] = fs;
-    a.fin[2 * b + 1] = fd;
+  // final: best over (s asc, d asc) of delta[T-1][s][d-1], strict > (hsmm.py:319-329):
+  // the maximum with the smallest linear index s*Dm + d-1
+  {
+    float bv = -INFINITY;
+    int bi = 0x7fffffff;
+    for (int i = tid; i < S * Dm; i += kHsThreads) {
+      const float v = L.cand[i / Dm][i % Dm];
+      argmax_combine(bv, bi, v, i);
+    }
+    wave_argmax(bv, bi);
+    __shared__ float fv[kHsThreads / 64];
+    __shared__ int fi[kHsThreads / 64];
+    if ((tid & 63) == 0) { fv[tid >> 6] = bv; fi[tid >> 6] = bi; }
+    __syncthreads();
+    if (tid == 0) {
+      float best = fv[0];
+      int besti = fi[0];
+      for (int w = 1; w < kHsThreads / 64; ++w) argmax_combine(best, besti, fv[w], fi[w]);
+      a.scores[b] = best;
+      a.fin[2 * b] = besti / Dm;
+      a.fin[2 * b + 1] = besti % Dm + 1;
+    }
   }
 }
 
