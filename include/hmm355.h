@@ -135,6 +135,48 @@ int hmm355_hsmm_viterbi_f32(const float* lp, const float* dur_lp, const float* l
                             int T, int S, int Dmax, int64_t* states, float* scores,
                             void* workspace, size_t workspace_bytes, void* stream);
 
+/* ---------------------------------------------------------------------------------
+ * Recursions with one transition matrix per time step (NeuralHMM).  Replace
+ * NeuralHMM._forward_algorithm / _backward_algorithm and the posterior epilogue of
+ * NeuralHMM.forward (neural.py:391-461) and NeuralHMM.viterbi_decode (neural.py:463-511).
+ *   log_obs (B,T,N): log-emissions (the observation network's output, any finite values);
+ *   log_A: log transition matrices, element (b,k,i,j) at
+ *          log_A[b*a_bstride + k*a_tstride + i*N + j] (strides in elements; pass 0, 0 for one
+ *          (N,N) matrix shared by every step: neural.py:383-385).  Forward and Viterbi step t
+ *          use matrix k = t-1 (neural.py:419-427, :489-496), backward step t matrix k = t
+ *          (neural.py:449-458); matrix T-1 is never read.  Entries must be <= ~88 (exp range);
+ *          -inf is allowed.
+ *   log_p0 / init (N): log initial probabilities (neural.py:388-389, :478-479).
+ * FB outputs as hmm355_forward_backward_f32 (posterior = exp(log_post), forward =
+ * exp(log_forward), backward = exp(log_backward), loglik = LSE(log_forward[T-1]), lik_ref =
+ * the reference's compute_likelihood LSE(log(forward[T-1] + 1e-8)), neural.py:513-519).
+ * Viterbi: states (B,T) int64, log_delta (B,T,N) fp32 (bit-identical to the reference's
+ * fp32 sums; first index on ties).  1 <= N <= 256.
+ * Workspaces >= hmm355_tv_fb_workspace_bytes / hmm355_tv_viterbi_workspace_bytes(B,T,N).
+ * ------------------------------------------------------------------------------ */
+size_t hmm355_tv_fb_workspace_bytes(int B, int T, int N);
+int hmm355_tv_forward_backward_f32(const float* log_obs, const float* log_A, long long a_bstride,
+                                   long long a_tstride, const float* log_p0, int B, int T, int N,
+                                   unsigned out_mask, float* posterior, float* forward,
+                                   float* backward, float* loglik, float* lik_ref,
+                                   void* workspace, size_t workspace_bytes, void* stream);
+/* As hmm355_tv_forward_backward_f32 with an optional terminal backward vector log_beta_T
+ * (B,N) (NULL = 0, the reference's beta_{T-1}); used by the adjoint (see
+ * hmm355_forward_backward_ex_f32).  Workspace layout: U | V (B,T,NP) | LA | LB (B,T) |
+ * E (B,T,NP) = exp(log_obs - M) | M (B,T) | CA | CB (B,T) | ..., pieces 256-B aligned,
+ * NP = 64/128/256; log alpha = log U + LA, log beta = log V + LB. */
+int hmm355_tv_forward_backward_ex_f32(const float* log_obs, const float* log_A, long long a_bstride,
+                                      long long a_tstride, const float* log_p0,
+                                      const float* log_beta_T, int B, int T, int N,
+                                      unsigned out_mask, float* posterior, float* forward,
+                                      float* backward, float* loglik, float* lik_ref,
+                                      void* workspace, size_t workspace_bytes, void* stream);
+size_t hmm355_tv_viterbi_workspace_bytes(int B, int T, int N);
+int hmm355_tv_viterbi_f32(const float* log_obs, const float* log_A, long long a_bstride,
+                          long long a_tstride, const float* init, int B, int T, int N,
+                          int64_t* states, float* log_delta, void* workspace,
+                          size_t workspace_bytes, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

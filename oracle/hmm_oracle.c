@@ -14,6 +14,10 @@
  *                       for sum(obs_log_probs[t:t+d, s]) (strided slice: 4 accumulators over
  *                       whole groups of 4, tail folded into acc0, then ((a0+a1)+a2)+a3 —
  *                       measured 31200/31200 matches against torch 2.10 CPU).
+ *   tv_viterbi_f32      neural.py:463-511 — Viterbi with one transition matrix per step
+ *                       (log_A (B,T,N,N); step t uses matrix t-1), exact as viterbi_f32.
+ *   tv_fb_f64           neural.py:391-461 in float64 (forward step t uses matrix t-1,
+ *                       backward step t matrix t; tolerance reference).
  *   hsmm_viterbi_fast   the same recursion reorganised (max over d' hoisted out of the
  *                       candidate loop, exact tie re-resolution per d) — bit-identical to
  *                       the literal form; cross-checked in tests/test_oracle.py.
@@ -86,6 +90,75 @@ void fb_f64(const float* log_obs, const float* log_P, const float* log_p0, int B
                     tmp[j] = (double)log_P[(size_t)i * N + j] + lo[(size_t)(t + 1) * N + j] + lb[(size_t)(t + 1) * N + j];
                 lb[(size_t)t * N + i] = lse(tmp, N);
             }
+        for (int t = 0; t < T; ++t) {
+            double* pr = posterior + ((size_t)b * T + t) * N;
+            for (int j = 0; j < N; ++j) tmp[j] = la[(size_t)t * N + j] + lb[(size_t)t * N + j];
+            double z = lse(tmp, N);
+            for (int j = 0; j < N; ++j) pr[j] = exp(tmp[j] - z);
+        }
+        loglik[b] = lse(la + (size_t)(T - 1) * N, N);
+    }
+    free(tmp);
+}
+
+/* ------------------------------------------- time-varying transitions (NeuralHMM) */
+/* log_A element (b,k,i,j) at log_A[b*sb + k*st + i*N + j] (sb = st = 0: one matrix). */
+void tv_viterbi_f32(const float* log_obs, const float* log_A, long long sb, long long st,
+                    const float* init, int B, int T, int N, int64_t* states, float* delta) {
+    uint8_t* ps = (uint8_t*)malloc((size_t)T * N);
+    for (int b = 0; b < B; ++b) {
+        const float* lo = log_obs + (size_t)b * T * N;
+        float* dl = delta + (size_t)b * T * N;
+        for (int j = 0; j < N; ++j) { dl[j] = init[j] + lo[j]; ps[j] = 0; }
+        for (int t = 1; t < T; ++t) {
+            const float* A = log_A + (size_t)b * sb + (size_t)(t - 1) * st;
+            const float* dp = dl + (size_t)(t - 1) * N;
+            for (int j = 0; j < N; ++j) {
+                float best = dp[0] + A[j];
+                int bi = 0;
+                for (int i = 1; i < N; ++i) {
+                    float s = dp[i] + A[(size_t)i * N + j];
+                    if (s > best) { best = s; bi = i; }
+                }
+                dl[(size_t)t * N + j] = best + lo[(size_t)t * N + j];
+                ps[(size_t)t * N + j] = (uint8_t)bi;
+            }
+        }
+        const float* dlast = dl + (size_t)(T - 1) * N;
+        int s = 0;
+        for (int j = 1; j < N; ++j) if (dlast[j] > dlast[s]) s = j;
+        int64_t* so = states + (size_t)b * T;
+        so[T - 1] = s;
+        for (int t = T - 2; t >= 0; --t) { s = ps[(size_t)(t + 1) * N + s]; so[t] = s; }
+    }
+    free(ps);
+}
+
+void tv_fb_f64(const float* log_obs, const float* log_A, long long sb, long long st,
+               const float* log_p0, int B, int T, int N, double* log_alpha, double* log_beta,
+               double* posterior, double* loglik) {
+    double* tmp = (double*)malloc(sizeof(double) * N);
+    for (int b = 0; b < B; ++b) {
+        const float* lo = log_obs + (size_t)b * T * N;
+        double* la = log_alpha + (size_t)b * T * N;
+        double* lb = log_beta + (size_t)b * T * N;
+        for (int j = 0; j < N; ++j) la[j] = (double)log_p0[j] + lo[j];
+        for (int t = 1; t < T; ++t) {
+            const float* A = log_A + (size_t)b * sb + (size_t)(t - 1) * st;
+            for (int j = 0; j < N; ++j) {
+                for (int i = 0; i < N; ++i) tmp[i] = la[(size_t)(t - 1) * N + i] + A[(size_t)i * N + j];
+                la[(size_t)t * N + j] = lse(tmp, N) + lo[(size_t)t * N + j];
+            }
+        }
+        for (int j = 0; j < N; ++j) lb[(size_t)(T - 1) * N + j] = 0.0;
+        for (int t = T - 2; t >= 0; --t) {
+            const float* A = log_A + (size_t)b * sb + (size_t)t * st;
+            for (int i = 0; i < N; ++i) {
+                for (int j = 0; j < N; ++j)
+                    tmp[j] = (double)A[(size_t)i * N + j] + lo[(size_t)(t + 1) * N + j] + lb[(size_t)(t + 1) * N + j];
+                lb[(size_t)t * N + i] = lse(tmp, N);
+            }
+        }
         for (int t = 0; t < T; ++t) {
             double* pr = posterior + ((size_t)b * T + t) * N;
             for (int j = 0; j < N; ++j) tmp[j] = la[(size_t)t * N + j] + lb[(size_t)t * N + j];

@@ -135,6 +135,46 @@ def viterbi_from_log(log_obs, log_P, init, squeeze=False):
     return states, delta
 
 
+# ------------------------------------------------------ NeuralHMM (time-varying transitions)
+def neural_forward_backward(log_obs, log_trans, log_init):
+    """neural.py:391-461: forward step t uses log_trans[:, t-1] (:419-427), backward step t
+    log_trans[:, t] (:449-458); log_trans (B,T,K,K).  Returns posterior, forward, backward and
+    the internal log_forward / log_backward."""
+    B, T, K = log_obs.shape
+    if log_trans.dim() == 2:  # the static matrix expanded over (B,T), neural.py:385
+        log_trans = log_trans.unsqueeze(0).unsqueeze(0).expand(B, T, -1, -1)
+    lf = torch.full((B, T, K), float("-inf"))
+    lf[:, 0] = log_init + log_obs[:, 0]
+    for t in range(1, T):
+        lf[:, t] = torch.logsumexp(lf[:, t - 1].unsqueeze(-1) + log_trans[:, t - 1], dim=1) + log_obs[:, t]
+    lb = torch.full((B, T, K), float("-inf"))
+    lb[:, -1] = 0.0
+    for t in range(T - 2, -1, -1):
+        comb = log_trans[:, t] + log_obs[:, t + 1].unsqueeze(1) + lb[:, t + 1].unsqueeze(1)
+        lb[:, t] = torch.logsumexp(comb, dim=-1)
+    lp = lf + lb
+    lp = lp - torch.logsumexp(lp, dim=-1, keepdim=True)
+    return torch.exp(lp), torch.exp(lf), torch.exp(lb), lf, lb
+
+
+def neural_viterbi(log_obs, log_trans, log_init):
+    """neural.py:463-511 (states (B,T), log_delta (B,T,K))."""
+    B, T, K = log_obs.shape
+    if log_trans.dim() == 2:
+        log_trans = log_trans.unsqueeze(0).unsqueeze(0).expand(B, T, -1, -1)
+    delta = torch.full((B, T, K), float("-inf"))
+    psi = torch.zeros((B, T, K), dtype=torch.long)
+    delta[:, 0] = log_init + log_obs[:, 0]
+    for t in range(1, T):
+        delta[:, t], psi[:, t] = torch.max(delta[:, t - 1].unsqueeze(-1) + log_trans[:, t - 1], dim=1)
+        delta[:, t] += log_obs[:, t]
+    states = torch.zeros((B, T), dtype=torch.long)
+    states[:, -1] = torch.argmax(delta[:, -1], dim=1)
+    for t in range(T - 2, -1, -1):
+        states[:, t] = psi[torch.arange(B), t + 1, states[:, t + 1]]
+    return states, delta
+
+
 # --------------------------------------------------------------------- Gaussian layer
 def gaussian_log_probs(x, means, log_scales, covariance_type="diag"):
     """hmm_layer.py:270-323."""
@@ -254,6 +294,9 @@ def c_oracle():
     lib.viterbi_f32.argtypes = [P, P, P, I, I, I, P, P, P]
     lib.fb_f64.argtypes = [P, P, P, I, I, I, P, P, P, P]
     lib.gmm_diag_f64.argtypes = [P, P, P, P, I, I, I, I, I, P]
+    L = ctypes.c_longlong
+    lib.tv_viterbi_f32.argtypes = [P, P, L, L, P, I, I, I, P, P]
+    lib.tv_fb_f64.argtypes = [P, P, L, L, P, I, I, I, P, P, P, P]
     lib.hsmm_viterbi_literal.argtypes = [P, P, P, I, I, I, P, P]
     lib.hsmm_viterbi_fast.argtypes = [P, P, P, I, I, I, P, P]
     _lib = lib
@@ -285,6 +328,35 @@ def c_fb64(log_obs, log_P, log_p0):
     la = np.zeros((B, T, N)); lb = np.zeros((B, T, N)); post = np.zeros((B, T, N))
     ll = np.zeros(B)
     c_oracle().fb_f64(_p(lo), _p(_f32(log_P)), _p(_f32(log_p0)), B, T, N, _p(la), _p(lb), _p(post), _p(ll))
+    return la, lb, post, ll
+
+
+def _tv_strides(log_A, B, T, N):
+    """(contiguous array, batch stride, step stride) for log_A of shape (N,N) or (B,T,N,N)."""
+    A = _f32(log_A)
+    if A.ndim == 2:
+        return A, 0, 0
+    assert A.shape == (B, T, N, N), A.shape
+    return A, T * N * N, N * N
+
+
+def c_tv_viterbi(log_obs, log_A, init):
+    lo = _f32(log_obs)
+    B, T, N = lo.shape
+    A, sb, st = _tv_strides(log_A, B, T, N)
+    states = np.zeros((B, T), np.int64)
+    delta = np.zeros((B, T, N), np.float32)
+    c_oracle().tv_viterbi_f32(_p(lo), _p(A), sb, st, _p(_f32(init)), B, T, N, _p(states), _p(delta))
+    return states, delta
+
+
+def c_tv_fb64(log_obs, log_A, log_p0):
+    lo = _f32(log_obs)
+    B, T, N = lo.shape
+    A, sb, st = _tv_strides(log_A, B, T, N)
+    la = np.zeros((B, T, N)); lb = np.zeros((B, T, N)); post = np.zeros((B, T, N))
+    ll = np.zeros(B)
+    c_oracle().tv_fb_f64(_p(lo), _p(A), sb, st, _p(_f32(log_p0)), B, T, N, _p(la), _p(lb), _p(post), _p(ll))
     return la, lb, post, ll
 
 

@@ -24,6 +24,8 @@ EXPORTS = (
     "hmm355_viterbi_workspace_bytes", "hmm355_viterbi_f32",
     "hmm355_gmm_workspace_bytes", "hmm355_gmm_diag_logprob_f32",
     "hmm355_hsmm_workspace_bytes", "hmm355_hsmm_viterbi_f32",
+    "hmm355_tv_fb_workspace_bytes", "hmm355_tv_forward_backward_f32", "hmm355_tv_forward_backward_ex_f32",
+    "hmm355_tv_viterbi_workspace_bytes", "hmm355_tv_viterbi_f32",
 )
 
 _lib = None
@@ -60,6 +62,15 @@ def lib():
     L.hmm355_hsmm_workspace_bytes.argtypes, L.hmm355_hsmm_workspace_bytes.restype = [I, I, I, I], S
     L.hmm355_hsmm_viterbi_f32.argtypes = [P, P, P, I, I, I, I, P, P, P, S, P]
     L.hmm355_hsmm_viterbi_f32.restype = I
+    LL = ctypes.c_longlong
+    L.hmm355_tv_fb_workspace_bytes.argtypes, L.hmm355_tv_fb_workspace_bytes.restype = [I, I, I], S
+    L.hmm355_tv_forward_backward_f32.argtypes = [P, P, LL, LL, P, I, I, I, U, P, P, P, P, P, P, S, P]
+    L.hmm355_tv_forward_backward_f32.restype = I
+    L.hmm355_tv_forward_backward_ex_f32.argtypes = [P, P, LL, LL, P, P, I, I, I, U, P, P, P, P, P, P, S, P]
+    L.hmm355_tv_forward_backward_ex_f32.restype = I
+    L.hmm355_tv_viterbi_workspace_bytes.argtypes, L.hmm355_tv_viterbi_workspace_bytes.restype = [I, I, I], S
+    L.hmm355_tv_viterbi_f32.argtypes = [P, P, LL, LL, P, I, I, I, P, P, P, S, P]
+    L.hmm355_tv_viterbi_f32.restype = I
     _lib = L
     return L
 

@@ -113,6 +113,88 @@ class SequenceLogLik(torch.autograd.Function):
         return grad_obs, grad_lP, grad_l0, None, None
 
 
+def _run_tv_fb(log_obs, A, sb, st, log_p0, log_beta_T=None, posterior=False):
+    """One hmm355_tv_forward_backward_ex_f32 call; returns (posterior|None, loglik, lik_ref, U, V, E)."""
+    B, T, N = log_obs.shape
+    NP = _pad(N)
+    dev = log_obs.device
+    L = nat.lib()
+    ws = torch.empty(L.hmm355_tv_fb_workspace_bytes(B, T, N), dtype=torch.uint8, device=dev)
+    post = torch.empty(B, T, N, device=dev) if posterior else None
+    loglik = torch.empty(B, device=dev)
+    lik_ref = torch.empty(B, device=dev)
+    with torch.cuda.device(dev):
+        nat.check(L.hmm355_tv_forward_backward_ex_f32(
+            nat.ptr(log_obs), nat.ptr(A), sb, st, nat.ptr(log_p0), nat.ptr(log_beta_T), B, T, N,
+            nat.FB_POSTERIOR if posterior else 0, nat.ptr(post), None, None, nat.ptr(loglik), nat.ptr(lik_ref),
+            nat.ptr(ws), ws.numel(), nat.stream_of(dev)))
+    rows = B * T
+    al = lambda n: ((n + 255) // 256) * 256
+    fl = ws.view(torch.float32)
+    U = fl[: rows * NP].view(B, T, NP)[..., :N]
+    V = fl[rows * NP: 2 * rows * NP].view(B, T, NP)[..., :N]
+    off = al(2 * rows * NP * 4) + al(2 * rows * 4)          # after U|V and LA|LB (hmm355.h)
+    E = fl[off // 4: off // 4 + rows * NP].view(B, T, NP)[..., :N]
+    offL = al(2 * rows * NP * 4) // 4
+    LA = fl[offL: offL + rows].view(B, T)
+    return post, loglik, lik_ref, U, V, E, LA
+
+
+class TvSequenceLogLik(torch.autograd.Function):
+    """(B,) log-likelihood of each sequence under per-step transition matrices
+    (NeuralHMM.compute_likelihood, neural.py:513-519), differentiable in log_obs, log_A
+    ((N,N) or (B,T,N,N)) and log_p0.  The adjoint of module docstring with the shifted
+    emissions E_t = exp(log_obs_t - M_t) the tv kernels use: dL/d log_A_k = G exp(log_A_k)
+    (X_{k+1} (x) Y_{k+1}) for the matrix k between steps k and k+1."""
+
+    @staticmethod
+    def forward(ctx, log_obs, log_A, log_p0, kind):
+        from .ops import _tv_matrix
+        nat.require_gpu(log_obs, log_A, log_p0)
+        lo = log_obs.detach().to(torch.float32).contiguous()
+        l0 = log_p0.detach().to(torch.float32).contiguous()
+        B, T, N = lo.shape
+        A, sb, st = _tv_matrix(log_A.detach(), B, T, N)
+        _, loglik, lik_ref, _, _, _, _ = _run_tv_fb(lo, A, sb, st, l0)
+        ctx.save_for_backward(lo, A, l0)
+        ctx.sb, ctx.st, ctx.kind, ctx.static = sb, st, kind, log_A.dim() == 2
+        return lik_ref if kind == "ref" else loglik
+
+    @staticmethod
+    def backward(ctx, gout):
+        lo, A, l0 = ctx.saved_tensors
+        B, T, N = lo.shape
+        _, _, _, U, _, _, LA = _run_tv_fb(lo, A, ctx.sb, ctx.st, l0)
+        a_last = torch.log(U[:, -1]) + LA[:, -1:]
+        if ctx.kind == "ref":
+            f = torch.exp(a_last)
+            z = torch.log(f + 1e-8)
+            w = torch.softmax(z, dim=-1)
+            g = w * f / (f + 1e-8)
+            log_mu = torch.log(w) - z
+        else:
+            g = torch.softmax(a_last, dim=-1)
+            log_mu = torch.zeros_like(a_last)
+        G = g.sum(-1) * gout
+        post, _, _, U, V, E, _ = _run_tv_fb(lo, A, ctx.sb, ctx.st, l0, log_beta_T=log_mu.contiguous(), posterior=True)
+        grad_lo = G[:, None, None] * post
+        grad_l0 = (G[:, None] * post[:, 0]).sum(0)
+        grad_A = None
+        if ctx.needs_input_grad[1]:
+            c = U.sum(-1)
+            S = (U * V).sum(-1)
+            X = U[:, :-1] / (c[:, :-1] * S[:, 1:]).unsqueeze(-1) * G[:, None, None]   # (B,T-1,N)
+            Y = E[:, 1:] * V[:, 1:]                                                   # (B,T-1,N)
+            if ctx.static:
+                grad_A = torch.exp(A) * torch.einsum("bti,btj->ij", X, Y)
+            else:
+                Af = A if A.stride(1) != 0 else A.expand(B, T, N, N)
+                grad_A = torch.zeros(B, T, N, N, device=lo.device)
+                if T > 1:
+                    grad_A[:, :-1] = torch.exp(Af[:, :-1]) * X.unsqueeze(-1) * Y.unsqueeze(-2)
+        return grad_lo, grad_A, grad_l0, None
+
+
 class _NoPosteriorGrad(torch.autograd.Function):
     """Carries forward-backward outputs (computed by the kernels) into a graph whose inputs
     require grad: the values are exact, back-propagating through them raises."""

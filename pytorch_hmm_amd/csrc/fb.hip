@@ -19,6 +19,7 @@
 //   backward = exp(log v + LB), and the reference's compute_likelihood value
 //   logsumexp_j(log(forward_{T-1}[j] + 1e-8)) (hmm.py:206) for t = T-1.
 #include "recur.h"
+#include "post.h"
 
 namespace hmm355 {
 
@@ -30,77 +31,6 @@ __global__ void __launch_bounds__(RC<NP>::NT) fb_recur_kernel(RecArgs fa, RecArg
     rec_dispatch<NP, kFbBeta>(fb, lds, b);
   else
     rec_dispatch<NP, kFbAlpha>(fa, lds, b);
-}
-
-struct PostArgs {
-  const float* U;
-  const float* V;
-  const float* LA;
-  const float* LB;
-  float* posterior;
-  float* forward;
-  float* backward;
-  float* lik_ref;
-  int B, T, N;
-  unsigned mask;
-};
-
-template <int NP>
-__global__ void __launch_bounds__(256) fb_posterior_kernel(PostArgs a) {
-  constexpr int K = NP / 64;
-  const int l = threadIdx.x & 63;
-  const int wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
-  const int nwaves = (gridDim.x * blockDim.x) >> 6;
-  const size_t rows = (size_t)a.B * a.T;
-  for (size_t row = wave; row < rows; row += nwaves) {
-    float u[K], v[K];
-#pragma unroll
-    for (int k = 0; k < K; ++k) {
-      u[k] = a.U[row * NP + l + 64 * k];
-      v[k] = a.V[row * NP + l + 64 * k];
-    }
-    const float la = a.LA[row], lb = a.LB[row];
-    float mu = 0.f, mv = 0.f;
-#pragma unroll
-    for (int k = 0; k < K; ++k) { mu = fmaxf(mu, u[k]); mv = fmaxf(mv, v[k]); }
-    mu = wave_max(mu);
-    mv = wave_max(mv);
-    const float iu = mu > 0.f ? 1.f / mu : 0.f, iv = mv > 0.f ? 1.f / mv : 0.f;
-    float p[K], s = 0.f;
-#pragma unroll
-    for (int k = 0; k < K; ++k) { p[k] = (u[k] * iu) * (v[k] * iv); s += p[k]; }
-    s = wave_sum(s);
-    const float is = s > 0.f ? 1.f / s : 0.f;
-    const bool last = (row % a.T) == (size_t)(a.T - 1);
-    float fw[K];
-#pragma unroll
-    for (int k = 0; k < K; ++k) fw[k] = __expf(__logf(u[k]) + la);
-#pragma unroll
-    for (int k = 0; k < K; ++k) {
-      const int j = l + 64 * k;
-      if (j < a.N) {
-        const size_t off = row * a.N + j;
-        if (a.mask & HMM355_FB_POSTERIOR) a.posterior[off] = p[k] * is;
-        if (a.mask & HMM355_FB_FORWARD) a.forward[off] = fw[k];
-        if (a.mask & HMM355_FB_BACKWARD) a.backward[off] = __expf(__logf(v[k]) + lb);
-      }
-    }
-    if (last && a.lik_ref) {
-      // hmm.py:206: logsumexp(log(forward[:, -1] + 1e-8))
-      float lv[K], m = -INFINITY;
-#pragma unroll
-      for (int k = 0; k < K; ++k) {
-        lv[k] = (l + 64 * k < a.N) ? __logf(fw[k] + 1e-8f) : -INFINITY;
-        m = fmaxf(m, lv[k]);
-      }
-      m = wave_max(m);
-      float e = 0.f;
-#pragma unroll
-      for (int k = 0; k < K; ++k) e += (l + 64 * k < a.N) ? __expf(lv[k] - m) : 0.f;
-      e = wave_sum(e);
-      if (l == 0) a.lik_ref[row / a.T] = m + __logf(e);
-    }
-  }
 }
 
 template <int NP>
@@ -147,26 +77,6 @@ static size_t fb_ws_layout(int B, int T, int N, char* base, FbWs* w) {
     w->bscale = reinterpret_cast<float*>(base + oS);
   }
   return off;
-}
-
-// terminal backward vector from its logarithm: binit = exp(l - max l) (padded states 0),
-// bscale = max l.  One wave per sequence.
-template <int NP>
-__global__ void __launch_bounds__(64) beta_init_kernel(const float* __restrict__ lbt, int N, float* binit, float* bscale) {
-  const int b = blockIdx.x, l = threadIdx.x;
-  constexpr int K = NP / 64;
-  float v[K], m = -INFINITY;
-#pragma unroll
-  for (int k = 0; k < K; ++k) {
-    const int j = l + 64 * k;
-    v[k] = j < N ? lbt[(size_t)b * N + j] : -INFINITY;
-    m = fmaxf(m, v[k]);
-  }
-  m = wave_max(m);
-  if (m == -INFINITY) m = 0.f;  // an all-zero terminal vector: every adjoint is 0
-#pragma unroll
-  for (int k = 0; k < K; ++k) binit[(size_t)b * NP + l + 64 * k] = (l + 64 * k < N) ? __expf(v[k] - m) : 0.f;
-  if (l == 0) bscale[b] = m;
 }
 
 }  // namespace hmm355

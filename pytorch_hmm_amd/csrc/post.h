@@ -1,0 +1,196 @@
+// hmm355 — epilogues shared by the time-invariant (fb.hip, viterbi.hip) and time-varying
+// (tv.hip) recursions: the forward-backward posterior pass and the Viterbi chunk maps +
+// backtrace.  Both consume the row layouts the recursions leave in the workspace.
+#pragma once
+#include "common.h"
+#include "band.h"
+
+namespace hmm355 {
+
+struct PostArgs {
+  const float* U;
+  const float* V;
+  const float* LA;
+  const float* LB;
+  float* posterior;
+  float* forward;
+  float* backward;
+  float* lik_ref;
+  int B, T, N;
+  unsigned mask;
+};
+
+template <int NP>
+__global__ void __launch_bounds__(256) fb_posterior_kernel(PostArgs a) {
+  constexpr int K = NP / 64;
+  const int l = threadIdx.x & 63;
+  const int wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const int nwaves = (gridDim.x * blockDim.x) >> 6;
+  const size_t rows = (size_t)a.B * a.T;
+  for (size_t row = wave; row < rows; row += nwaves) {
+    float u[K], v[K];
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+      u[k] = a.U[row * NP + l + 64 * k];
+      v[k] = a.V[row * NP + l + 64 * k];
+    }
+    const float la = a.LA[row], lb = a.LB[row];
+    float mu = 0.f, mv = 0.f;
+#pragma unroll
+    for (int k = 0; k < K; ++k) { mu = fmaxf(mu, u[k]); mv = fmaxf(mv, v[k]); }
+    mu = wave_max(mu);
+    mv = wave_max(mv);
+    const float iu = mu > 0.f ? 1.f / mu : 0.f, iv = mv > 0.f ? 1.f / mv : 0.f;
+    float p[K], s = 0.f;
+#pragma unroll
+    for (int k = 0; k < K; ++k) { p[k] = (u[k] * iu) * (v[k] * iv); s += p[k]; }
+    s = wave_sum(s);
+    const float is = s > 0.f ? 1.f / s : 0.f;
+    const bool last = (row % a.T) == (size_t)(a.T - 1);
+    float fw[K];
+#pragma unroll
+    for (int k = 0; k < K; ++k) fw[k] = __expf(__logf(u[k]) + la);
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+      const int j = l + 64 * k;
+      if (j < a.N) {
+        const size_t off = row * a.N + j;
+        if (a.mask & HMM355_FB_POSTERIOR) a.posterior[off] = p[k] * is;
+        if (a.mask & HMM355_FB_FORWARD) a.forward[off] = fw[k];
+        if (a.mask & HMM355_FB_BACKWARD) a.backward[off] = __expf(__logf(v[k]) + lb);
+      }
+    }
+    if (last && a.lik_ref) {
+      // hmm.py:206: logsumexp(log(forward[:, -1] + 1e-8))
+      float lv[K], m = -INFINITY;
+#pragma unroll
+      for (int k = 0; k < K; ++k) {
+        lv[k] = (l + 64 * k < a.N) ? __logf(fw[k] + 1e-8f) : -INFINITY;
+        m = fmaxf(m, lv[k]);
+      }
+      m = wave_max(m);
+      float e = 0.f;
+#pragma unroll
+      for (int k = 0; k < K; ++k) e += (l + 64 * k < a.N) ? __expf(lv[k] - m) : 0.f;
+      e = wave_sum(e);
+      if (l == 0) a.lik_ref[row / a.T] = m + __logf(e);
+    }
+  }
+}
+
+constexpr int kChunk = 64;  // psi / backtrace chunk length (time steps)
+
+template <int NP>
+struct VF {
+  static constexpr int NW = NP / 16;
+  static constexpr int NT = NW * kWave;
+  static constexpr int NBLK = NP / 64;
+  static constexpr int RING = 32;
+  static constexpr int OFF_EMIS = 0;                       // [2][16][NP]
+  static constexpr int OFF_RING = OFF_EMIS + 2 * 16 * NP;  // [RING][NP]
+  static constexpr int LDS_FLOATS = OFF_RING + RING * NP;
+};
+
+struct VitArgs {
+  const float* obs;
+  const float* log_P;
+  const float* init;
+  float* delta;          // (B,T,N) output trellis
+  float* final_score;    // (B) or null
+  int64_t* states;       // (B,T)
+  uint8_t* psi;          // (B,T,NP) workspace
+  uint8_t* G;            // (B,nchunks,NP) workspace
+  int B, T, N, obs_mode, nchunks;
+  const BandDesc* band;  // banded decomposition (band.h) or null
+};
+
+// chunk map: G[j] = state at t_lo - 1 given state j at t_hi (psi rows of the chunk in LDS)
+template <int NP>
+__device__ __forceinline__ void compose_chunk_map(const VitArgs& a, const uint8_t (*prow)[NP], int b, int chunk,
+                                                  int t_lo, int t_hi) {
+  const int tid = threadIdx.x;
+  if (chunk > 0 && tid < NP) {
+    int s = tid < a.N ? tid : 0;
+    for (int t = t_hi; t > t_lo; --t) s = prow[t - t_lo][s];
+    a.G[((size_t)b * a.nchunks + chunk) * NP + tid] = prow[0][s];
+  }
+}
+
+// ----------------------------------------------------------------------- backtrace
+template <int NP>
+__global__ void __launch_bounds__(64) vit_backtrace_kernel(VitArgs a) {
+  constexpr int K = NP / 64;
+  constexpr int GB = 64;  // chunk maps staged per LDS batch
+  __shared__ __attribute__((aligned(16))) uint8_t gs[GB][NP];
+  __shared__ __attribute__((aligned(16))) uint8_t ps[kChunk][NP];
+  __shared__ int st[kChunk];
+  const int chunk = blockIdx.x, b = blockIdx.y;
+  const int l = threadIdx.x;
+  const int T = a.T, N = a.N, nc = a.nchunks;
+
+  // s_{T-1} = argmax delta_{T-1} (first index; hmm.py:174)
+  const float* dl = a.delta + ((size_t)b * T + T - 1) * N;
+  float bv = -INFINITY;
+  int bi = 0x7fffffff;
+#pragma unroll
+  for (int k = 0; k < K; ++k) {
+    const int j = l + 64 * k;
+    const bool ok = j < N;
+    const float v = dl[ok ? j : 0];
+    if (ok) argmax_combine(bv, bi, v, j);
+  }
+  wave_argmax(bv, bi);
+  if (chunk == 0 && l == 0 && a.final_score) a.final_score[b] = bv;
+  int s = bi;
+
+  // walk the chunk maps from the last chunk down to chunk+1
+  for (int hi = nc - 1; hi > chunk; hi -= GB) {
+    const int lo = hi - GB + 1 > chunk + 1 ? hi - GB + 1 : chunk + 1;
+    const int cnt = hi - lo + 1;
+    const uint8_t* gsrc = a.G + ((size_t)b * nc + lo) * NP;
+    for (int idx = l; idx < cnt * NP / 16; idx += 64)
+      *reinterpret_cast<uint4*>(&gs[0][0] + idx * 16) = *reinterpret_cast<const uint4*>(gsrc + idx * 16);
+    __syncthreads();
+    for (int cc = hi; cc >= lo; --cc) s = gs[cc - lo][s];
+    __syncthreads();
+  }
+  // this chunk's psi rows, then the walk
+  const int t_lo = chunk * kChunk;
+  const int t_hi = (t_lo + kChunk < T ? t_lo + kChunk : T) - 1;
+  const int rows = t_hi - t_lo + 1;
+  const uint8_t* psrc = a.psi + ((size_t)b * T + t_lo) * NP;
+  for (int idx = l; idx < rows * NP / 16; idx += 64)
+    *reinterpret_cast<uint4*>(&ps[0][0] + idx * 16) = *reinterpret_cast<const uint4*>(psrc + idx * 16);
+  __syncthreads();
+  if (l == 0) {
+    st[t_hi - t_lo] = s;
+    for (int t = t_hi; t > t_lo; --t) {
+      s = ps[t - t_lo][s];
+      st[t - 1 - t_lo] = s;
+    }
+  }
+  __syncthreads();
+  for (int i = l; i < rows; i += 64) a.states[(size_t)b * T + t_lo + i] = st[i];
+}
+
+// terminal backward vector from its logarithm: binit = exp(l - max l) (padded states 0),
+// bscale = max l.  One wave per sequence.
+template <int NP>
+__global__ void __launch_bounds__(64) beta_init_kernel(const float* __restrict__ lbt, int N, float* binit, float* bscale) {
+  const int b = blockIdx.x, l = threadIdx.x;
+  constexpr int K = NP / 64;
+  float v[K], m = -INFINITY;
+#pragma unroll
+  for (int k = 0; k < K; ++k) {
+    const int j = l + 64 * k;
+    v[k] = j < N ? lbt[(size_t)b * N + j] : -INFINITY;
+    m = fmaxf(m, v[k]);
+  }
+  m = wave_max(m);
+  if (m == -INFINITY) m = 0.f;  // an all-zero terminal vector: every adjoint is 0
+#pragma unroll
+  for (int k = 0; k < K; ++k) binit[(size_t)b * NP + l + 64 * k] = (l + 64 * k < N) ? __expf(v[k] - m) : 0.f;
+  if (l == 0) bscale[b] = m;
+}
+
+}  // namespace hmm355

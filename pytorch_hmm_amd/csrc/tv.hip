@@ -1,0 +1,668 @@
+// hmm355 — recursions with one transition matrix per time step (NeuralHMM) on gfx950.
+//
+// Replaces NeuralHMM._forward_algorithm / _backward_algorithm / the posterior epilogue
+// (reference neural.py:391-461) and NeuralHMM.viterbi_decode (neural.py:463-511).  The
+// reference feeds log_transition_probs of shape (B,T,N,N) from its transition network
+// (neural.py:377-381); forward step t uses matrix t-1 (neural.py:419-427), backward step t
+// matrix t (:449-458), Viterbi step t matrix t-1 (:489-496).  Without a transition network
+// one matrix is expanded over (B,T) (:383-385): strides sb = st = 0 here.
+//
+// Per (sequence, step) the recursion consumes N^2 fresh matrix entries (64 KiB at N = 128)
+// read once from HBM, so this path is bound by the bytes a chain's CU can pull and by the
+// N^2 exponentials, not by the serial latency that bounds the time-invariant path.
+//
+// HBM layout: the caller's matrices, element (b,k,i,j) at lA[b*sb + k*st + i*N + j].
+// FB workspace: U | V (B,T,NP) | LA | LB (B,T) | E (B,T,NP) | M | CA | CB (B,T).
+//
+// tv_fb<NP>: one 512-thread workgroup (8 waves, two per SIMD) per (sequence, direction),
+//   owning its CU.  Each wave streams a fixed slice of every step's matrix with PD steps of
+//   float4 loads in flight (PD x 64 KiB per CU at N = 128), 128-B row segments per load
+//   instruction on the backward slice and 64-B segments on the forward slice:
+//   - alpha: wave w holds columns [NP/8 w, +NP/8) of every row; lane (q = l % QW,
+//     r = l / QW) the column quad q of rows r + RL k.  u_t[j] = sum_i u_{t-1}[i] exp(lA[i][j])
+//     is a lane-local FMA chain and a reduction over the RL row lanes (transposed through
+//     v_permlane32/16_swap, then DPP row_ror), so a column never leaves its wave.
+//   - beta: wave w holds rows [NP/8 w, +NP/8) of every column; lane (qq = l & 7, r = l >> 3)
+//     the quads qq + 8m of rows r + 8k.  v_t[i] = sum_j exp(lA[i][j]) w_{t+1}[j] reduces over
+//     the 8 quad lanes of a row (DPP quad_perm / row_half_mirror).
+//   The Rabiner normaliser of the previous vector is formed in every wave (each wave reads
+//   all of it), so a step has ONE s_barrier: publish the new vector to LDS, barrier, read it.
+//   Scales: u_t = (u_{t-1} A_t) * E_t / c_{t-1} with E_t = exp(lo_t - M_t), M_t the row max
+//   of the log-emission, so log alpha_t = log u_t + LA_t, LA_t = LA_{t-1} + log c_{t-1} + M_t;
+//   beta likewise.  The normalisers go to CA / CB and one wave per sequence scans them
+//   (tv_scan) in fp64; the posterior epilogue is post.h's.
+// tv_vit<NP>: the alpha layout in max-plus with the first-index argmax kept in the chain
+//   (the matrix is read once, so the argmax cannot be recomputed off-chain for free as
+//   viterbi.hip does), psi rows to the workspace, then post.h's chunk maps and backtrace.
+//   delta_t[j] = fl(max_i fl(delta_{t-1}[i] + lA[i][j]) + lo_t[j]): the reference's sums
+//   (neural.py:494-497), so delta and the states are bit-identical to it.
+#include "post.h"
+
+namespace hmm355 {
+
+template <int NP>
+struct TvGeo {
+  static constexpr int NT = 512;           // 8 waves
+  static constexpr int SLICE = NP / 8;     // columns (alpha/Viterbi) or rows (beta) per wave
+  static constexpr int QW = NP / 32;       // alpha: column quads per wave
+  static constexpr int RL = 64 / QW;       // alpha: row lanes
+  static constexpr int KA = NP / RL;       // alpha: rows per lane
+  static constexpr int KB = NP / 64;       // beta: rows per lane
+  static constexpr int MB = NP / 32;       // beta: column quads per lane
+  static constexpr int NV = KA;            // float4 per lane per step (= KB * MB)
+  static constexpr int PD = NP == 64 ? 8 : (NP == 128 ? 4 : 1);  // steps in flight
+  static_assert(KB * MB == KA, "slice shapes");
+};
+
+struct TvArgs {
+  const float* lo;    // (B,T,N) log emissions
+  const float* lA;    // log transition matrices, element (b,k,i,j) at b*sb + k*st + i*N + j
+  long long sb, st;   // batch / step strides of lA (elements)
+  const float* init;  // (N) log initial probabilities
+  const float* E;     // (B,T,NP) exp(lo - M) (FB)
+  float* rows;        // U or V (B,T,NP) (FB); delta (B,T,N) (Viterbi)
+  float* cs;          // (B,T) normalisers (FB)
+  uint8_t* psi;       // (B,T,NP) (Viterbi)
+  const float* binit; // beta: terminal vector exp(l - max l) (B,NP) or null (= 1)
+  int B, T, N;
+};
+
+enum TvKind : int { kTvAlpha = 0, kTvBeta = 1, kTvVit = 2 };
+
+// one step's slice of the matrix (float4 per entry of dst; -inf outside N x N)
+template <int NP, int KIND, bool VEC>
+__device__ __forceinline__ void tv_load(const TvArgs& a, int b, int kmat, float4 (&dst)[TvGeo<NP>::NV]) {
+  using G = TvGeo<NP>;
+  const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
+  const float* base = a.lA + (size_t)b * a.sb + (size_t)kmat * a.st;
+  const int N = a.N;
+#pragma unroll
+  for (int v = 0; v < G::NV; ++v) {
+    int i, c0;
+    if (KIND == kTvBeta) {
+      const int k = v / G::MB, m = v % G::MB;
+      i = G::SLICE * w + (l >> 3) + 8 * k;
+      c0 = 4 * ((l & 7) + 8 * m);
+    } else {
+      i = (l / G::QW) + G::RL * v;
+      c0 = G::SLICE * w + 4 * (l % G::QW);
+    }
+    const float* p = base + (size_t)i * N + c0;
+    if (VEC) {
+      if (i < N && c0 < N) dst[v] = *reinterpret_cast<const float4*>(p);
+      else dst[v] = make_float4(-INFINITY, -INFINITY, -INFINITY, -INFINITY);
+    } else {
+      const bool ri = i < N;
+      dst[v].x = (ri && c0 < N) ? p[0] : -INFINITY;
+      dst[v].y = (ri && c0 + 1 < N) ? p[1] : -INFINITY;
+      dst[v].z = (ri && c0 + 2 < N) ? p[2] : -INFINITY;
+      dst[v].w = (ri && c0 + 3 < N) ? p[3] : -INFINITY;
+    }
+  }
+}
+
+__device__ __forceinline__ float f4(const float4& v, int c) { return c == 0 ? v.x : (c == 1 ? v.y : (c == 2 ? v.z : v.w)); }
+
+// alpha / Viterbi: full sum over the row lanes (bits log2(QW)..5 of the lane id)
+template <int QW>
+__device__ __forceinline__ float rowlanes_sum(float x) {
+  if (QW <= 2) x += dpp_f<0x4E>(x);   // xor 2
+  if (QW <= 4) x += dpp_f<0x124>(x);  // row_ror:4
+  if (QW <= 8) x += dpp_f<0x128>(x);  // row_ror:8
+  return rows_sum(x);                 // xor 16, xor 32
+}
+
+// alpha: the four column partials reduced over the row lanes, transposed: lane keeps column
+// cc = 2*bit5 + bit4 of its quad
+template <int QW>
+__device__ __forceinline__ float rowlanes_transpose_sum(float (&acc)[4]) {
+  float a0 = acc[0], a2 = acc[2], a1 = acc[1], a3 = acc[3];
+  permlane32_swap(a0, a2);  // lower: (c0 own, c0 partner)  upper: (c2 partner, c2 own)
+  permlane32_swap(a1, a3);
+  float p0 = a0 + a2, p1 = a1 + a3;
+  permlane16_swap(p0, p1);  // even rows: (p0, p0 partner)  odd rows: (p1 partner, p1)
+  float z = p0 + p1;
+  if (QW <= 2) z += dpp_f<0x4E>(z);
+  if (QW <= 4) z += dpp_f<0x124>(z);
+  if (QW <= 8) z += dpp_f<0x128>(z);
+  return z;
+}
+
+template <int QW>
+__device__ __forceinline__ void rowlanes_transpose_argmax(float (&bv)[4], int (&bi)[4], float& v, int& i) {
+  float a0 = bv[0], a2 = bv[2], a1 = bv[1], a3 = bv[3];
+  int i0 = bi[0], i2 = bi[2], i1 = bi[1], i3 = bi[3];
+  permlane32_swap(a0, a2);
+  permlane32_swap_i(i0, i2);
+  permlane32_swap(a1, a3);
+  permlane32_swap_i(i1, i3);
+  argmax_combine(a0, i0, a2, i2);
+  argmax_combine(a1, i1, a3, i3);
+  permlane16_swap(a0, a1);
+  permlane16_swap_i(i0, i1);
+  argmax_combine(a0, i0, a1, i1);
+  if (QW <= 2) argmax_combine(a0, i0, dpp_f<0x4E>(a0), dpp_i<0x4E>(i0));
+  if (QW <= 4) argmax_combine(a0, i0, dpp_f<0x124>(a0), dpp_i<0x124>(i0));
+  if (QW <= 8) argmax_combine(a0, i0, dpp_f<0x128>(a0), dpp_i<0x128>(i0));
+  v = a0;
+  i = i0;
+}
+
+// beta: full sum over the 8 quad lanes of a row (bits 0..2)
+__device__ __forceinline__ float quadlanes_sum(float x) {
+  x += dpp_f<0xB1>(x);   // xor 1
+  x += dpp_f<0x4E>(x);   // xor 2
+  x += dpp_f<0x141>(x);  // row_half_mirror: lane k <-> 7-k (pairs the bit-2 halves)
+  return x;
+}
+
+// beta: the KB row partials reduced over the quad lanes, transposed where KB > 1
+template <int KB>
+__device__ __forceinline__ float quadlanes_transpose_sum(float (&z)[KB], int l) {
+  if constexpr (KB == 1) {
+    return quadlanes_sum(z[0]);
+  } else if constexpr (KB == 2) {
+    const bool hi = l & 4;
+    const float keep = hi ? z[1] : z[0], send = hi ? z[0] : z[1];
+    float x = keep + dpp_f<0x141>(send);
+    x += dpp_f<0xB1>(x);
+    x += dpp_f<0x4E>(x);
+    return x;
+  } else {
+    const bool h2 = l & 4, h1 = l & 2;
+    float y0, y1;
+    {
+      const float k0 = h2 ? z[2] : z[0], s0 = h2 ? z[0] : z[2];
+      const float k1 = h2 ? z[3] : z[1], s1 = h2 ? z[1] : z[3];
+      y0 = k0 + dpp_f<0x141>(s0);
+      y1 = k1 + dpp_f<0x141>(s1);
+    }
+    const float keep = h1 ? y1 : y0, send = h1 ? y0 : y1;
+    float x = keep + dpp_f<0x4E>(send);
+    x += dpp_f<0xB1>(x);
+    return x;
+  }
+}
+
+template <int NP, int KIND, bool VEC>
+__device__ void tv_chain(const TvArgs& a, float* lds, int b) {
+  using G = TvGeo<NP>;
+  constexpr int PD = G::PD;
+  const int tid = threadIdx.x, w = tid >> 6, l = tid & 63;
+  const int T = a.T, N = a.N;
+  float* vbuf = lds;  // [2][NP]
+
+  // this lane's output index after the reduction, and whether it is the lane that stores it
+  int jo;
+  bool writer;
+  if (KIND == kTvBeta) {
+    const int r = l >> 3;
+    int kk = 0;
+    if (G::KB == 2) kk = (l >> 2) & 1;
+    if (G::KB == 4) kk = 2 * ((l >> 2) & 1) + ((l >> 1) & 1);
+    jo = G::SLICE * w + r + 8 * kk;
+    writer = G::KB == 1 ? (l & 7) == 0 : (G::KB == 2 ? (l & 3) == 0 : (l & 1) == 0);
+  } else {
+    const int cc = 2 * (l >> 5) + ((l >> 4) & 1);
+    jo = G::SLICE * w + 4 * (l % G::QW) + cc;
+    writer = ((l / G::QW) & (16 / G::QW - 1)) == 0;
+  }
+  // alpha / Viterbi read the previous vector in row-lane order: pos(i) = (i % RL) * KA + i / RL
+  auto pos = [&](int i) { return KIND == kTvBeta ? i : (i % G::RL) * G::KA + i / G::RL; };
+  const int rl = l / G::QW;  // alpha / Viterbi row lane
+
+  auto kmat_of = [&](int q) { return KIND == kTvBeta ? T - 1 - q : q - 1; };
+  auto tout_of = [&](int q) { return KIND == kTvBeta ? T - 1 - q : q; };
+  // per-step scalar input of this lane: E at the output time (alpha: scales u_t; beta: forms
+  // the next product input w_t = v_t E_t), or the raw log-emission (Viterbi)
+  auto emis_of = [&](int q) -> float {
+    const int t = tout_of(q);
+    if (KIND == kTvVit) return jo < N ? a.lo[((size_t)b * T + t) * N + jo] : -INFINITY;
+    return a.E[((size_t)b * T + t) * NP + jo];
+  };
+
+  float4 raw[PD][G::NV];
+  float eR[PD];
+#pragma unroll
+  for (int s = 0; s < PD; ++s) {
+    if (1 + s < T) {
+      tv_load<NP, KIND, VEC>(a, b, kmat_of(1 + s), raw[s]);
+      eR[s] = emis_of(1 + s);
+    }
+  }
+
+  // row 0 of the recursion
+  {
+    float v0;
+    const int jj = jo < N ? jo : 0;
+    if (KIND == kTvAlpha) v0 = jo < N ? __expf(a.init[jj]) * a.E[(size_t)b * T * NP + jo] : 0.f;
+    else if (KIND == kTvBeta) v0 = jo < N ? a.E[((size_t)b * T + T - 1) * NP + jo] * (a.binit ? a.binit[(size_t)b * NP + jo] : 1.f) : 0.f;  // w_{T-1} = E_{T-1} v_{T-1}
+    else v0 = jo < N ? a.init[jj] + a.lo[(size_t)b * T * N + jo] : -INFINITY;
+    if (writer) {
+      vbuf[pos(jo)] = v0;
+      if (KIND == kTvAlpha) a.rows[(size_t)b * T * NP + jo] = v0;
+      else if (KIND == kTvBeta) a.rows[((size_t)b * T + T - 1) * NP + jo] = jo < N ? (a.binit ? a.binit[(size_t)b * NP + jo] : 1.f) : 0.f;
+      else if (jo < N) a.rows[(size_t)b * T * N + jo] = v0;
+    }
+  }
+  lds_barrier();
+
+  auto step = [&](int q, float4 (&rw)[G::NV], float& er) {
+    const float* prev = vbuf + ((q - 1) & 1) * NP;
+    float* cur = vbuf + (q & 1) * NP;
+    const int t = tout_of(q);
+    if (KIND == kTvBeta) {
+      float wv[G::MB][4];
+#pragma unroll
+      for (int m = 0; m < G::MB; ++m) {
+        const float4 x = *reinterpret_cast<const float4*>(prev + 4 * ((l & 7) + 8 * m));
+        wv[m][0] = x.x; wv[m][1] = x.y; wv[m][2] = x.z; wv[m][3] = x.w;
+      }
+      float cs = 0.f;
+#pragma unroll
+      for (int m = 0; m < G::MB; ++m) cs += (wv[m][0] + wv[m][1]) + (wv[m][2] + wv[m][3]);
+      cs = quadlanes_sum(cs);
+      float z[G::KB];
+#pragma unroll
+      for (int k = 0; k < G::KB; ++k) {
+        float s0 = 0.f, s1 = 0.f;
+#pragma unroll
+        for (int m = 0; m < G::MB; ++m) {
+          const float4 A = rw[k * G::MB + m];
+          s0 = fmaf(__expf(A.x), wv[m][0], s0);
+          s1 = fmaf(__expf(A.y), wv[m][1], s1);
+          s0 = fmaf(__expf(A.z), wv[m][2], s0);
+          s1 = fmaf(__expf(A.w), wv[m][3], s1);
+        }
+        z[k] = s0 + s1;
+      }
+      const float e_t = er;
+      if (q + PD < T) {
+        tv_load<NP, KIND, VEC>(a, b, kmat_of(q + PD), rw);
+        er = emis_of(q + PD);
+      }
+      const float zz = quadlanes_transpose_sum<G::KB>(z, l);
+      const float v = zz * __builtin_amdgcn_rcpf(cs);
+      if (writer) {
+        cur[jo] = v * e_t;
+        a.rows[((size_t)b * T + t) * NP + jo] = v;
+      }
+      if (tid == 0) a.cs[(size_t)b * T + t] = cs;
+    } else {
+      float y[G::KA];
+      const float* src = prev + rl * G::KA;
+      if constexpr (G::KA % 4 == 0) {
+#pragma unroll
+        for (int k4 = 0; k4 < G::KA / 4; ++k4) {
+          const float4 x = *reinterpret_cast<const float4*>(src + 4 * k4);
+          y[4 * k4] = x.x; y[4 * k4 + 1] = x.y; y[4 * k4 + 2] = x.z; y[4 * k4 + 3] = x.w;
+        }
+      } else {
+#pragma unroll
+        for (int k2 = 0; k2 < G::KA / 2; ++k2) {
+          const float2 x = *reinterpret_cast<const float2*>(src + 2 * k2);
+          y[2 * k2] = x.x; y[2 * k2 + 1] = x.y;
+        }
+      }
+      if (KIND == kTvAlpha) {
+        float cs = 0.f;
+#pragma unroll
+        for (int k = 0; k < G::KA; ++k) cs += y[k];
+        cs = rowlanes_sum<G::QW>(cs);
+        float acc[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int k = 0; k < G::KA; ++k) {
+          const float4 A = rw[k];
+          acc[0] = fmaf(y[k], __expf(A.x), acc[0]);
+          acc[1] = fmaf(y[k], __expf(A.y), acc[1]);
+          acc[2] = fmaf(y[k], __expf(A.z), acc[2]);
+          acc[3] = fmaf(y[k], __expf(A.w), acc[3]);
+        }
+        const float e_t = er;
+        if (q + PD < T) {
+          tv_load<NP, KIND, VEC>(a, b, kmat_of(q + PD), rw);
+          er = emis_of(q + PD);
+        }
+        const float z = rowlanes_transpose_sum<G::QW>(acc);
+        const float u = z * (e_t * __builtin_amdgcn_rcpf(cs));
+        if (writer) {
+          cur[pos(jo)] = u;
+          a.rows[((size_t)b * T + t) * NP + jo] = u;
+        }
+        if (tid == 0) a.cs[(size_t)b * T + t] = cs;
+      } else {
+        // max-plus with the first index: rows r + RL k increase with k, strict > keeps the first
+        float bv[4];
+        int bi[4];
+        {
+          const float4 A = rw[0];
+          bv[0] = y[0] + A.x; bv[1] = y[0] + A.y; bv[2] = y[0] + A.z; bv[3] = y[0] + A.w;
+          bi[0] = bi[1] = bi[2] = bi[3] = rl;
+        }
+#pragma unroll
+        for (int k = 1; k < G::KA; ++k) {
+          const float4 A = rw[k];
+          const int ii = rl + G::RL * k;
+#pragma unroll
+          for (int c = 0; c < 4; ++c) {
+            const float s = y[k] + f4(A, c);
+            const bool gt = s > bv[c];
+            bv[c] = gt ? s : bv[c];
+            bi[c] = gt ? ii : bi[c];
+          }
+        }
+        const float lo_t = er;
+        if (q + PD < T) {
+          tv_load<NP, KIND, VEC>(a, b, kmat_of(q + PD), rw);
+          er = emis_of(q + PD);
+        }
+        float v;
+        int vi;
+        rowlanes_transpose_argmax<G::QW>(bv, bi, v, vi);
+        const float d = v + lo_t;
+        if (writer) {
+          cur[pos(jo)] = d;
+          if (jo < N) a.rows[((size_t)b * T + t) * N + jo] = d;
+          a.psi[((size_t)b * T + t) * NP + jo] = (uint8_t)vi;
+        }
+      }
+    }
+    lds_barrier();
+  };
+
+  for (int q0 = 1; q0 < T; q0 += PD) {
+#pragma unroll
+    for (int s = 0; s < PD; ++s) {
+      const int q = q0 + s;
+      if (q >= T) break;
+      step(q, raw[s], eR[s]);
+    }
+  }
+  if (KIND == kTvAlpha) {
+    // c_{T-1} = sum u_{T-1} (the sequence log-likelihood), kept in slot t = 0 of CA
+    const float* last = vbuf + ((T - 1) & 1) * NP + rl * G::KA;
+    float cs = 0.f;
+#pragma unroll
+    for (int k = 0; k < G::KA; ++k) cs += last[k];
+    cs = rowlanes_sum<G::QW>(cs);
+    if (tid == 0) a.cs[(size_t)b * T] = cs;
+  }
+}
+
+template <int NP, bool VEC>
+__global__ void __launch_bounds__(512) tv_fb_kernel(TvArgs fa, TvArgs fb) {
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  const int b = blockIdx.x >> 1;
+  if (blockIdx.x & 1)
+    tv_chain<NP, kTvBeta, VEC>(fb, lds, b);
+  else
+    tv_chain<NP, kTvAlpha, VEC>(fa, lds, b);
+}
+
+template <int NP, bool VEC>
+__global__ void __launch_bounds__(512) tv_vit_kernel(TvArgs va) {
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  tv_chain<NP, kTvVit, VEC>(va, lds, blockIdx.x);
+}
+
+// E = exp(lo - M) per (b,t) row (zero-padded to NP), M = the row max (0 for an all -inf row).
+// One wave per row, grid-stride.
+template <int NP>
+__global__ void __launch_bounds__(256) tv_emis_kernel(const float* __restrict__ lo, float* __restrict__ E,
+                                                      float* __restrict__ M, size_t rows, int N) {
+  constexpr int K = NP / 64;
+  const int l = threadIdx.x & 63;
+  const size_t wave = ((size_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const size_t nw = ((size_t)gridDim.x * blockDim.x) >> 6;
+  for (size_t row = wave; row < rows; row += nw) {
+    float v[K], m = -INFINITY;
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+      const int j = l + 64 * k;
+      v[k] = j < N ? lo[row * N + j] : -INFINITY;
+      m = fmaxf(m, v[k]);
+    }
+    m = wave_max(m);
+    if (m == -INFINITY) m = 0.f;
+#pragma unroll
+    for (int k = 0; k < K; ++k) E[row * NP + l + 64 * k] = __expf(v[k] - m);
+    if (l == 0) M[row] = m;
+  }
+}
+
+// LA_t = M_0 + sum_{s=1..t} (log CA_s + M_s);  LB_t = bscale + sum_{s=t..T-2} (log CB_s + M_{s+1});
+// loglik = LA_{T-1} + log CA_0 (CA_0 holds sum u_{T-1}).  One wave per sequence, fp64.
+__global__ void __launch_bounds__(64) tv_scan_kernel(const float* __restrict__ CA, const float* __restrict__ CB,
+                                                     const float* __restrict__ M, float* __restrict__ LA,
+                                                     float* __restrict__ LB, float* __restrict__ loglik,
+                                                     const float* __restrict__ bscale, int T) {
+  const int b = blockIdx.x, l = threadIdx.x;
+  const size_t o = (size_t)b * T;
+  double base = 0.0;
+  for (int t0 = 0; t0 < T; t0 += 64) {
+    const int t = t0 + l;
+    double x = 0.0;
+    if (t < T) x = t == 0 ? (double)M[o] : (double)__logf(CA[o + t]) + (double)M[o + t];
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+      const double y = __shfl_up(x, off);
+      if (l >= off) x += y;
+    }
+    if (t < T) LA[o + t] = (float)(base + x);
+    base += __shfl(x, 63);
+  }
+  if (l == 0 && loglik) loglik[b] = (float)(base + (double)__logf(CA[o]));
+  base = bscale ? (double)bscale[b] : 0.0;  // LB_{T-1} = log of the terminal vector's scale
+  for (int t1 = T; t1 > 0; t1 -= 64) {
+    const int t = t1 - 1 - l;  // descending
+    double x = 0.0;
+    if (t >= 0 && t <= T - 2) x = (double)__logf(CB[o + t]) + (double)M[o + t + 1];
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+      const double y = __shfl_up(x, off);
+      if (l >= off) x += y;
+    }
+    if (t >= 0) LB[o + t] = (float)(base + x);
+    base += __shfl(x, 63);
+  }
+}
+
+// psi rows of one chunk (written by the chain) -> the chunk map (post.h)
+template <int NP>
+__global__ void __launch_bounds__(NP) tv_chunkmap_kernel(VitArgs a) {
+  __shared__ __attribute__((aligned(16))) uint8_t prow[kChunk][NP];
+  const int chunk = blockIdx.x, b = blockIdx.y;
+  if (chunk == 0) return;
+  const int t_lo = chunk * kChunk;
+  const int t_hi = (t_lo + kChunk < a.T ? t_lo + kChunk : a.T) - 1;
+  const int rows = t_hi - t_lo + 1;
+  const uint8_t* src = a.psi + ((size_t)b * a.T + t_lo) * NP;
+  for (int idx = threadIdx.x; idx < rows * NP / 16; idx += NP)
+    *reinterpret_cast<uint4*>(&prow[0][0] + idx * 16) = *reinterpret_cast<const uint4*>(src + idx * 16);
+  __syncthreads();
+  compose_chunk_map<NP>(a, prow, b, chunk, t_lo, t_hi);
+}
+
+struct TvFbWs {
+  float *U, *V, *LA, *LB, *E, *M, *CA, *CB, *binit, *bscale;
+};
+static size_t tv_fb_ws_layout(int B, int T, int N, char* base, TvFbWs* w) {
+  const size_t NP = pad_states(N), rows = (size_t)B * T;
+  size_t off = 0;
+  auto take = [&](size_t bytes) { const size_t o = off; off += align_up(bytes, 256); return o; };
+  const size_t oU = take(2 * rows * NP * sizeof(float));   // U | V (post.h expects V = U + rows*NP)
+  const size_t oL = take(2 * rows * sizeof(float));        // LA | LB
+  const size_t oE = take(rows * NP * sizeof(float));
+  const size_t oM = take(rows * sizeof(float));
+  const size_t oC = take(2 * rows * sizeof(float));        // CA | CB
+  const size_t oI = take((size_t)B * NP * sizeof(float));   // terminal vector (adjoint)
+  const size_t oS = take((size_t)B * sizeof(float));
+  if (w && base) {
+    w->U = reinterpret_cast<float*>(base + oU);
+    w->V = w->U + rows * NP;
+    w->LA = reinterpret_cast<float*>(base + oL);
+    w->LB = w->LA + rows;
+    w->E = reinterpret_cast<float*>(base + oE);
+    w->M = reinterpret_cast<float*>(base + oM);
+    w->CA = reinterpret_cast<float*>(base + oC);
+    w->CB = w->CA + rows;
+    w->binit = reinterpret_cast<float*>(base + oI);
+    w->bscale = reinterpret_cast<float*>(base + oS);
+  }
+  return off;
+}
+
+static bool tv_vec_ok(const float* lA, long long sb, long long st, int N) {
+  return (N % 4) == 0 && (sb % 4) == 0 && (st % 4) == 0 && (reinterpret_cast<uintptr_t>(lA) & 15) == 0;
+}
+
+template <int NP>
+static hipError_t launch_tv_fb(const TvArgs& fa, const TvArgs& fb, const PostArgs& pa, const TvFbWs& w,
+                               float* loglik, const float* bscale, bool vec, hipStream_t st) {
+  const size_t rows = (size_t)fa.B * fa.T;
+  {
+    const size_t waves = rows < 16384 ? rows : 16384;
+    hipLaunchKernelGGL(tv_emis_kernel<NP>, dim3((unsigned)((waves + 3) / 4)), dim3(256), 0, st, fa.lo, w.E, w.M,
+                       rows, fa.N);
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+  }
+  hipError_t e;
+  if (vec) {
+    e = allow_lds(tv_fb_kernel<NP, true>, kExclusiveLds);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL((tv_fb_kernel<NP, true>), dim3(2 * fa.B), dim3(512), kExclusiveLds, st, fa, fb);
+  } else {
+    e = allow_lds(tv_fb_kernel<NP, false>, kExclusiveLds);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL((tv_fb_kernel<NP, false>), dim3(2 * fa.B), dim3(512), kExclusiveLds, st, fa, fb);
+  }
+  e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(tv_scan_kernel, dim3(fa.B), dim3(64), 0, st, w.CA, w.CB, w.M, w.LA, w.LB, loglik, bscale,
+                     fa.T);
+  e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  const size_t waves = rows < 8192 ? rows : 8192;
+  hipLaunchKernelGGL(fb_posterior_kernel<NP>, dim3((unsigned)((waves + 3) / 4)), dim3(256), 0, st, pa);
+  return hipGetLastError();
+}
+
+template <int NP>
+static hipError_t launch_tv_vit(const TvArgs& ta, const VitArgs& va, bool vec, hipStream_t st) {
+  hipError_t e;
+  if (vec) {
+    e = allow_lds(tv_vit_kernel<NP, true>, kExclusiveLds);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL((tv_vit_kernel<NP, true>), dim3(ta.B), dim3(512), kExclusiveLds, st, ta);
+  } else {
+    e = allow_lds(tv_vit_kernel<NP, false>, kExclusiveLds);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL((tv_vit_kernel<NP, false>), dim3(ta.B), dim3(512), kExclusiveLds, st, ta);
+  }
+  e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(tv_chunkmap_kernel<NP>, dim3(va.nchunks, va.B), dim3(NP), 0, st, va);
+  e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(vit_backtrace_kernel<NP>, dim3(va.nchunks, va.B), dim3(64), 0, st, va);
+  return hipGetLastError();
+}
+
+}  // namespace hmm355
+
+using namespace hmm355;
+
+HMM355_API size_t hmm355_tv_fb_workspace_bytes(int B, int T, int N) {
+  if (B < 0 || T < 1 || N < 1 || N > 256) return 0;
+  return tv_fb_ws_layout(B, T, N, nullptr, nullptr);
+}
+
+HMM355_API int hmm355_tv_forward_backward_ex_f32(const float* log_obs, const float* log_A, long long a_bstride,
+                                                 long long a_tstride, const float* log_p0, const float* log_beta_T,
+                                                 int B, int T, int N, unsigned out_mask, float* posterior,
+                                                 float* forward, float* backward, float* loglik, float* lik_ref,
+                                                 void* workspace, size_t workspace_bytes, void* stream) {
+  if (B < 0 || N < 0 || a_bstride < 0 || a_tstride < 0) return HMM355_E_ARG;
+  if (N < 1 || N > 256) return HMM355_E_STATES;
+  if (T < 1) return HMM355_E_SHAPE;
+  if (B == 0) return HMM355_OK;
+  if (!log_obs || !log_A || !log_p0 || !workspace) return HMM355_E_ARG;
+  if ((out_mask & HMM355_FB_POSTERIOR) && !posterior) return HMM355_E_ARG;
+  if ((out_mask & HMM355_FB_FORWARD) && !forward) return HMM355_E_ARG;
+  if ((out_mask & HMM355_FB_BACKWARD) && !backward) return HMM355_E_ARG;
+  if ((size_t)B * T > (size_t)1 << 40) return HMM355_E_SHAPE;
+  if (workspace_bytes < hmm355_tv_fb_workspace_bytes(B, T, N)) return HMM355_E_WORKSPACE;
+  const int NP = pad_states(N);
+  TvFbWs w;
+  tv_fb_ws_layout(B, T, N, static_cast<char*>(workspace), &w);
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  const float* binit = nullptr;
+  const float* bscale = nullptr;
+  if (log_beta_T) {  // the same terminal-vector preparation as fb.hip
+    switch (NP) {
+      case 64: hipLaunchKernelGGL(beta_init_kernel<64>, dim3(B), dim3(64), 0, st, log_beta_T, N, w.binit, w.bscale); break;
+      case 128: hipLaunchKernelGGL(beta_init_kernel<128>, dim3(B), dim3(64), 0, st, log_beta_T, N, w.binit, w.bscale); break;
+      default: hipLaunchKernelGGL(beta_init_kernel<256>, dim3(B), dim3(64), 0, st, log_beta_T, N, w.binit, w.bscale); break;
+    }
+    const hipError_t e0 = hipGetLastError();
+    if (e0 != hipSuccess) return (int)e0;
+    binit = w.binit;
+    bscale = w.bscale;
+  }
+  TvArgs fa{log_obs, log_A, a_bstride, a_tstride, log_p0, w.E, w.U, w.CA, nullptr, nullptr, B, T, N};
+  TvArgs fb{log_obs, log_A, a_bstride, a_tstride, log_p0, w.E, w.V, w.CB, nullptr, binit, B, T, N};
+  PostArgs pa{w.U, w.V, w.LA, w.LB, posterior, forward, backward, lik_ref, B, T, N, out_mask};
+  const bool vec = tv_vec_ok(log_A, a_bstride, a_tstride, N);
+  hipError_t e;
+  switch (NP) {
+    case 64: e = launch_tv_fb<64>(fa, fb, pa, w, loglik, bscale, vec, st); break;
+    case 128: e = launch_tv_fb<128>(fa, fb, pa, w, loglik, bscale, vec, st); break;
+    default: e = launch_tv_fb<256>(fa, fb, pa, w, loglik, bscale, vec, st); break;
+  }
+  return e == hipSuccess ? HMM355_OK : (int)e;
+}
+
+HMM355_API int hmm355_tv_forward_backward_f32(const float* log_obs, const float* log_A, long long a_bstride,
+                                              long long a_tstride, const float* log_p0, int B, int T, int N,
+                                              unsigned out_mask, float* posterior, float* forward,
+                                              float* backward, float* loglik, float* lik_ref, void* workspace,
+                                              size_t workspace_bytes, void* stream) {
+  return hmm355_tv_forward_backward_ex_f32(log_obs, log_A, a_bstride, a_tstride, log_p0, nullptr, B, T, N, out_mask,
+                                           posterior, forward, backward, loglik, lik_ref, workspace, workspace_bytes,
+                                           stream);
+}
+
+HMM355_API size_t hmm355_tv_viterbi_workspace_bytes(int B, int T, int N) {
+  if (B < 0 || T < 1 || N < 1 || N > 256) return 0;
+  const size_t NP = pad_states(N);
+  const size_t nc = (T + kChunk - 1) / kChunk;
+  return align_up((size_t)B * T * NP, 256) + align_up((size_t)B * nc * NP, 256);
+}
+
+HMM355_API int hmm355_tv_viterbi_f32(const float* log_obs, const float* log_A, long long a_bstride,
+                                     long long a_tstride, const float* init, int B, int T, int N, int64_t* states,
+                                     float* log_delta, void* workspace, size_t workspace_bytes, void* stream) {
+  if (B < 0 || N < 0 || a_bstride < 0 || a_tstride < 0) return HMM355_E_ARG;
+  if (N < 1 || N > 256) return HMM355_E_STATES;
+  if (T < 1) return HMM355_E_SHAPE;
+  if (B == 0) return HMM355_OK;
+  if (!log_obs || !log_A || !init || !states || !log_delta || !workspace) return HMM355_E_ARG;
+  if ((size_t)B * T > (size_t)1 << 40 || B > 65535) return HMM355_E_SHAPE;
+  if (workspace_bytes < hmm355_tv_viterbi_workspace_bytes(B, T, N)) return HMM355_E_WORKSPACE;
+  const int NP = pad_states(N);
+  const int nc = (T + kChunk - 1) / kChunk;
+  uint8_t* psi = static_cast<uint8_t*>(workspace);
+  uint8_t* G = psi + align_up((size_t)B * T * NP, 256);
+  TvArgs ta{log_obs, log_A, a_bstride, a_tstride, init, nullptr, log_delta, nullptr, psi, nullptr, B, T, N};
+  VitArgs va{log_obs, log_A, init, log_delta, nullptr, states, psi, G, B, T, N, HMM355_OBS_LOG, nc, nullptr};
+  const bool vec = tv_vec_ok(log_A, a_bstride, a_tstride, N);
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  hipError_t e;
+  switch (NP) {
+    case 64: e = launch_tv_vit<64>(ta, va, vec, st); break;
+    case 128: e = launch_tv_vit<128>(ta, va, vec, st); break;
+    default: e = launch_tv_vit<256>(ta, va, vec, st); break;
+  }
+  return e == hipSuccess ? HMM355_OK : (int)e;
+}

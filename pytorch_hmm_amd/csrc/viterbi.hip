@@ -26,34 +26,9 @@
 //   (LDS lookups), then this chunk's 64-step walk (hmm.py:177-178).  The serial depth is
 //   T/64 + 64 lookups instead of T dependent gathers.
 #include "recur.h"
+#include "post.h"
 
 namespace hmm355 {
-
-constexpr int kChunk = 64;  // psi / backtrace chunk length (time steps)
-
-template <int NP>
-struct VF {
-  static constexpr int NW = NP / 16;
-  static constexpr int NT = NW * kWave;
-  static constexpr int NBLK = NP / 64;
-  static constexpr int RING = 32;
-  static constexpr int OFF_EMIS = 0;                       // [2][16][NP]
-  static constexpr int OFF_RING = OFF_EMIS + 2 * 16 * NP;  // [RING][NP]
-  static constexpr int LDS_FLOATS = OFF_RING + RING * NP;
-};
-
-struct VitArgs {
-  const float* obs;
-  const float* log_P;
-  const float* init;
-  float* delta;          // (B,T,N) output trellis
-  float* final_score;    // (B) or null
-  int64_t* states;       // (B,T)
-  uint8_t* psi;          // (B,T,NP) workspace
-  uint8_t* G;            // (B,nchunks,NP) workspace
-  int B, T, N, obs_mode, nchunks;
-  const BandDesc* band;  // banded decomposition (band.h) or null
-};
 
 // log_obs = log(x + 1e-8) (hmm.py:152), fp32 add then fp64 log rounded once (common.h)
 __global__ void __launch_bounds__(256) log_obs_kernel(const float* __restrict__ x, float* __restrict__ y, size_t n,
@@ -95,12 +70,7 @@ __device__ __forceinline__ void psi_write_rows(const VitArgs& a, uint8_t (*prow)
     const int row = idx / (NP / 16), c16 = (idx % (NP / 16)) * 16;
     *reinterpret_cast<uint4*>(pdst + (size_t)row * NP + c16) = *reinterpret_cast<const uint4*>(&prow[row][c16]);
   }
-  // chunk map: G[j] = state at t_lo - 1 given state j at t_hi
-  if (chunk > 0 && tid < NP) {
-    int s = tid < N ? tid : 0;
-    for (int t = t_hi; t > t_lo; --t) s = prow[t - t_lo][s];
-    a.G[((size_t)b * a.nchunks + chunk) * NP + tid] = prow[0][s];
-  }
+  compose_chunk_map<NP>(a, prow, b, chunk, t_lo, t_hi);
 }
 
 // Banded psi rows (band.h): psi_t[o] = first argmax_i fl(delta_{t-1,i} + L[i][o]).  With
@@ -251,63 +221,6 @@ __global__ void __launch_bounds__(VF<NP>::NT) vit_psi_kernel(VitArgs a) {
   }
   __syncthreads();
   psi_write_rows<NP>(a, prow, b, chunk, t_lo, t_hi);
-}
-
-// ----------------------------------------------------------------------- backtrace
-template <int NP>
-__global__ void __launch_bounds__(64) vit_backtrace_kernel(VitArgs a) {
-  constexpr int K = NP / 64;
-  constexpr int GB = 64;  // chunk maps staged per LDS batch
-  __shared__ __attribute__((aligned(16))) uint8_t gs[GB][NP];
-  __shared__ __attribute__((aligned(16))) uint8_t ps[kChunk][NP];
-  __shared__ int st[kChunk];
-  const int chunk = blockIdx.x, b = blockIdx.y;
-  const int l = threadIdx.x;
-  const int T = a.T, N = a.N, nc = a.nchunks;
-
-  // s_{T-1} = argmax delta_{T-1} (first index; hmm.py:174)
-  const float* dl = a.delta + ((size_t)b * T + T - 1) * N;
-  float bv = -INFINITY;
-  int bi = 0x7fffffff;
-#pragma unroll
-  for (int k = 0; k < K; ++k) {
-    const int j = l + 64 * k;
-    const bool ok = j < N;
-    const float v = dl[ok ? j : 0];
-    if (ok) argmax_combine(bv, bi, v, j);
-  }
-  wave_argmax(bv, bi);
-  if (chunk == 0 && l == 0 && a.final_score) a.final_score[b] = bv;
-  int s = bi;
-
-  // walk the chunk maps from the last chunk down to chunk+1
-  for (int hi = nc - 1; hi > chunk; hi -= GB) {
-    const int lo = hi - GB + 1 > chunk + 1 ? hi - GB + 1 : chunk + 1;
-    const int cnt = hi - lo + 1;
-    const uint8_t* gsrc = a.G + ((size_t)b * nc + lo) * NP;
-    for (int idx = l; idx < cnt * NP / 16; idx += 64)
-      *reinterpret_cast<uint4*>(&gs[0][0] + idx * 16) = *reinterpret_cast<const uint4*>(gsrc + idx * 16);
-    __syncthreads();
-    for (int cc = hi; cc >= lo; --cc) s = gs[cc - lo][s];
-    __syncthreads();
-  }
-  // this chunk's psi rows, then the walk
-  const int t_lo = chunk * kChunk;
-  const int t_hi = (t_lo + kChunk < T ? t_lo + kChunk : T) - 1;
-  const int rows = t_hi - t_lo + 1;
-  const uint8_t* psrc = a.psi + ((size_t)b * T + t_lo) * NP;
-  for (int idx = l; idx < rows * NP / 16; idx += 64)
-    *reinterpret_cast<uint4*>(&ps[0][0] + idx * 16) = *reinterpret_cast<const uint4*>(psrc + idx * 16);
-  __syncthreads();
-  if (l == 0) {
-    st[t_hi - t_lo] = s;
-    for (int t = t_hi; t > t_lo; --t) {
-      s = ps[t - t_lo][s];
-      st[t - 1 - t_lo] = s;
-    }
-  }
-  __syncthreads();
-  for (int i = l; i < rows; i += 64) a.states[(size_t)b * T + t_lo + i] = st[i];
 }
 
 template <int NP>

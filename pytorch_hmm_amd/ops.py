@@ -10,6 +10,9 @@ shape-only fake implementations; their only real implementation is the HIP libra
   torch.ops.hmm355.viterbi(obs, log_P, init, obs_mode) -> (states, log_delta, final_score)
   torch.ops.hmm355.gmm_diag_logprob(x, means, log_vars, log_w, mix_lse) -> log_probs
   torch.ops.hmm355.hsmm_viterbi(lp, dur_lp, log_T) -> (states, scores)
+  torch.ops.hmm355.tv_forward_backward(log_obs, log_A, log_p0, out_mask)
+      -> (posterior, forward, backward, loglik, lik_ref)
+  torch.ops.hmm355.tv_viterbi(log_obs, log_A, init) -> (states, log_delta)
 """
 from typing import Tuple
 
@@ -148,3 +151,87 @@ def hsmm_viterbi(lp: Tensor, dur_lp: Tensor, log_T: Tensor) -> Tuple[Tensor, Ten
 def _(lp, dur_lp, log_T):
     B, T, S = lp.shape
     return lp.new_empty((B, T), dtype=torch.int64), lp.new_empty(B)
+
+
+# ------------------------------------------------- time-varying transitions (NeuralHMM)
+def _tv_matrix(log_A: Tensor, B: int, T: int, N: int):
+    """(tensor, batch stride, step stride) for the C ABI.  log_A is (N,N) (one matrix for all
+    steps) or (B,T,N,N) with contiguous rows — an expand()ed static matrix keeps its zero
+    strides, so it is never materialised (neural.py:385 expands one (N,N) over (B,T))."""
+    if log_A.dtype != torch.float32:
+        log_A = log_A.float()
+    if log_A.dim() == 2:
+        if tuple(log_A.shape) != (N, N):
+            raise ValueError(f"transition matrix shape {tuple(log_A.shape)} != ({N}, {N})")
+        return log_A.contiguous(), 0, 0
+    if log_A.dim() != 4 or log_A.shape[0] != B or tuple(log_A.shape[2:]) != (N, N):
+        raise ValueError(f"log transition tensor shape {tuple(log_A.shape)} != ({B}, {T}, {N}, {N})")
+    if log_A.shape[1] < T - 1:  # steps 0..T-2 are read (neural.py:419-458)
+        raise IndexError(f"log transition tensor has {log_A.shape[1]} steps, the recursion needs {T - 1}")
+    if log_A.stride(3) != 1 or log_A.stride(2) != N or min(log_A.stride(0), log_A.stride(1)) < 0:
+        log_A = log_A.contiguous()
+    if log_A.stride(0) == 0 and log_A.stride(1) == 0:
+        return log_A, 0, 0
+    if log_A.stride(1) == 0 or log_A.stride(0) == 0:
+        log_A = log_A.contiguous()
+    return log_A, log_A.stride(0), log_A.stride(1)
+
+
+@torch.library.custom_op("hmm355::tv_forward_backward", mutates_args=())
+def tv_forward_backward(log_obs: Tensor, log_A: Tensor, log_p0: Tensor,
+                        out_mask: int) -> Tuple[Tensor, Tensor, Tensor, Tensor, Tensor]:
+    nat.require_gpu(log_obs, log_A, log_p0)
+    log_obs, log_p0 = _f32c(log_obs), _f32c(log_p0)
+    B, T, N = log_obs.shape
+    dev = log_obs.device
+    L = nat.lib()
+    post = torch.empty((B, T, N) if out_mask & FB_POSTERIOR else _EMPTY, device=dev)
+    fwd = torch.empty((B, T, N) if out_mask & FB_FORWARD else _EMPTY, device=dev)
+    bwd = torch.empty((B, T, N) if out_mask & FB_BACKWARD else _EMPTY, device=dev)
+    loglik = torch.empty(B, device=dev)
+    lik_ref = torch.empty(B, device=dev)
+    if B == 0:
+        return post, fwd, bwd, loglik, lik_ref
+    A, sb, st = _tv_matrix(log_A, B, T, N)
+    ws = _workspace(L.hmm355_tv_fb_workspace_bytes(B, T, N), dev)
+    with torch.cuda.device(dev):
+        nat.check(L.hmm355_tv_forward_backward_f32(
+            nat.ptr(log_obs), nat.ptr(A), sb, st, nat.ptr(log_p0), B, T, N, out_mask,
+            nat.ptr(post) if out_mask & FB_POSTERIOR else None,
+            nat.ptr(fwd) if out_mask & FB_FORWARD else None,
+            nat.ptr(bwd) if out_mask & FB_BACKWARD else None,
+            nat.ptr(loglik), nat.ptr(lik_ref), nat.ptr(ws), ws.numel(), nat.stream_of(dev)))
+    return post, fwd, bwd, loglik, lik_ref
+
+
+@tv_forward_backward.register_fake
+def _(log_obs, log_A, log_p0, out_mask):
+    B, T, N = log_obs.shape
+    mk = lambda bit: log_obs.new_empty((B, T, N) if out_mask & bit else _EMPTY)
+    return mk(FB_POSTERIOR), mk(FB_FORWARD), mk(FB_BACKWARD), log_obs.new_empty(B), log_obs.new_empty(B)
+
+
+@torch.library.custom_op("hmm355::tv_viterbi", mutates_args=())
+def tv_viterbi(log_obs: Tensor, log_A: Tensor, init: Tensor) -> Tuple[Tensor, Tensor]:
+    nat.require_gpu(log_obs, log_A, init)
+    log_obs, init = _f32c(log_obs), _f32c(init)
+    B, T, N = log_obs.shape
+    dev = log_obs.device
+    states = torch.empty((B, T), dtype=torch.int64, device=dev)
+    delta = torch.empty((B, T, N), device=dev)
+    if B == 0:
+        return states, delta
+    A, sb, st = _tv_matrix(log_A, B, T, N)
+    L = nat.lib()
+    ws = _workspace(L.hmm355_tv_viterbi_workspace_bytes(B, T, N), dev)
+    with torch.cuda.device(dev):
+        nat.check(L.hmm355_tv_viterbi_f32(
+            nat.ptr(log_obs), nat.ptr(A), sb, st, nat.ptr(init), B, T, N, nat.ptr(states), nat.ptr(delta),
+            nat.ptr(ws), ws.numel(), nat.stream_of(dev)))
+    return states, delta
+
+
+@tv_viterbi.register_fake
+def _(log_obs, log_A, init):
+    B, T, N = log_obs.shape
+    return log_obs.new_empty((B, T), dtype=torch.int64), log_obs.new_empty((B, T, N))

@@ -29,6 +29,7 @@ from pytorch_hmm.hmm import HMMPyTorch  # noqa: E402
 from pytorch_hmm.hmm_layer import HMMLayer, GaussianHMMLayer  # noqa: E402
 from pytorch_hmm.mixture_gaussian import MixtureGaussianHMMLayer  # noqa: E402
 from pytorch_hmm.hsmm import HSMMLayer  # noqa: E402
+from pytorch_hmm.neural import NeuralHMM, ContextualNeuralHMM  # noqa: E402
 from pytorch_hmm.utils import (  # noqa: E402
     create_left_to_right_matrix, create_transition_matrix)
 
@@ -217,6 +218,55 @@ def fx_hsmm(name, S, D, Dmax, B, T, seed):
          states=npf(states), scores=npf(scores), input_sha256=sha(npf(x)))
 
 
+def _neural_capture(m, x, ctx, call_fb, call_vit):
+    """Log-emissions, log-transitions, the FB outputs with log_forward / log_backward (the last
+    two torch.exp arguments, neural.py:401), Viterbi and compute_likelihood of one NeuralHMM."""
+    with torch.no_grad():
+        lo = m.observation_model(x)
+        if m.transition_model is not None and ctx is not None:
+            lt = torch.log(m.transition_model(ctx) + 1e-8)                      # neural.py:379-380
+        else:
+            lt = torch.log(torch.softmax(m.transition_matrix, dim=1) + 1e-8)    # :383-384 (K,K)
+        li = torch.log(torch.softmax(m.initial_logits, dim=0) + 1e-8)          # :388-389
+        with CaptureExp() as cap:
+            post, fwd, bwd = call_fb()
+        lf, lb = cap.args[-2], cap.args[-1]
+        states, delta = call_vit()
+        lik = m.compute_likelihood(x, ctx)
+    return dict(log_obs=npf(lo), log_trans=npf(lt), log_init=npf(li), posterior=npf(post),
+                forward=npf(fwd), backward=npf(bwd), log_forward=npf(lf), log_backward=npf(lb),
+                states=npf(states), log_delta=npf(delta), compute_likelihood=npf(lik))
+
+
+def fx_neural(name, K, D, C, H, B, T, seed, ttype="mlp", otype="gaussian", keep_params=True):
+    """NeuralHMM forward / viterbi_decode / compute_likelihood (neural.py:355-519) in eval mode
+    (dropout off).  C = 0: the static transition_matrix expanded over (B,T) (neural.py:383-385)."""
+    torch.manual_seed(seed)
+    m = NeuralHMM(K, D, context_dim=C, hidden_dim=H, transition_type=ttype, observation_type=otype).eval()
+    x = torch.randn(B, T, D)
+    ctx = torch.randn(B, T, C) if C > 0 else None
+    out = _neural_capture(m, x, ctx, lambda: m(x, ctx), lambda: m.viterbi_decode(x, ctx))
+    sd = {"sd__" + k: npf(v) for k, v in m.state_dict().items()} if keep_params else {}
+    save(name, x=npf(x), ctx=(npf(ctx) if ctx is not None else np.zeros(0, np.float32)),
+         config=np.array([K, D, C, H]), ttype=np.array(ttype), otype=np.array(otype),
+         input_sha256=sha(npf(x)), **out, **sd)
+
+
+def fx_contextual(name, K, D, V, LD, PD, B, T, seed):
+    """ContextualNeuralHMM.forward_with_context (neural.py:522-588), eval mode."""
+    torch.manual_seed(seed)
+    m = ContextualNeuralHMM(K, D, phoneme_vocab_size=V, linguistic_context_dim=LD, prosody_dim=PD).eval()
+    x = torch.randn(B, T, D)
+    ph = torch.randint(0, V, (B, T))
+    pr = torch.randn(B, T, PD)
+    with torch.no_grad():
+        ctx = m.encode_context(ph, pr)
+    out = _neural_capture(m, x, ctx, lambda: m.forward_with_context(x, ph, pr), lambda: m.viterbi_decode(x, ctx))
+    sd = {"sd__" + k: npf(v) for k, v in m.state_dict().items()}
+    save(name, x=npf(x), phonemes=npf(ph), prosody=npf(pr), ctx=npf(ctx), config=np.array([K, D, V, LD, PD]),
+         input_sha256=sha(npf(x)), **out, **sd)
+
+
 def fx_fullsize_ns():
     """North-star shape B=32, T=2000, N=128 (left-to-right 0.7): machine-independent uniform
     inputs (PCG64 -> float32) so the GPU box can regenerate them bit-for-bit.  Stores the
@@ -279,6 +329,13 @@ def main():
         ("hsmm_s5", lambda: fx_hsmm("hsmm_s5", 5, 30, 20, 2, 30, 0)),
         ("hsmm_s2", lambda: fx_hsmm("hsmm_s2", 2, 3, 2, 1, 4, 1)),
         ("hsmm_s8", lambda: fx_hsmm("hsmm_s8", 8, 20, 10, 1, 40, 2)),
+        ("neural_mlp_small", lambda: fx_neural("neural_mlp_small", 5, 8, 12, 64, 2, 20, 0)),
+        ("neural_static", lambda: fx_neural("neural_static", 6, 10, 0, 32, 2, 25, 1)),
+        ("neural_rnn", lambda: fx_neural("neural_rnn", 7, 6, 4, 16, 2, 15, 2, ttype="rnn")),
+        ("neural_mixture", lambda: fx_neural("neural_mixture", 5, 6, 5, 16, 2, 12, 3, otype="mixture")),
+        ("neural_k32", lambda: fx_neural("neural_k32", 32, 16, 8, 64, 2, 24, 4)),
+        ("neural_k128", lambda: fx_neural("neural_k128", 128, 16, 8, 64, 1, 6, 5, keep_params=False)),
+        ("contextual_small", lambda: fx_contextual("contextual_small", 6, 10, 50, 32, 8, 2, 15, 6)),
         ("fullsize_ns", fx_fullsize_ns),
         ("fullsize_mixture", fx_fullsize_mixture),
     ]
