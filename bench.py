@@ -17,6 +17,7 @@ Prints ONE JSON line on rank 0.  Besides the contract fields it carries
 """
 import argparse
 import json
+import math
 import os
 import sys
 import time
@@ -45,7 +46,7 @@ def parse():
                    help="launch every step eagerly instead of replaying one captured HIP graph")
     p.add_argument("--transition", default="left_to_right", choices=["left_to_right", "ergodic"],
                    help="transition matrix of the workload (BASELINE: left_to_right 0.7)")
-    p.add_argument("--workload", default="ns", choices=["ns", "c1", "c2", "c3", "c5"],
+    p.add_argument("--workload", default="ns", choices=["ns", "c1", "c2", "c3", "c5", "neural"],
                    help="ns: the BASELINE metric (default).  c1/c2/c3/c5: BASELINE configs 1, 2, 3, 5 "
                         "(HMMLayer, GaussianHMMLayer, MixtureGaussianHMMLayer, HSMMLayer) through the layers")
     return p.parse_args()
@@ -162,6 +163,42 @@ def layer_workload(args, rank, world, dev):
         desc = {"workload": "MixtureGaussianHMMLayer(128,80,num_components=4) forward (emission + Viterbi)",
                 "batch_per_gpu": B, "seq_len": T, "num_states": S, "num_components": C, "feature_dim": D}
         dom, flops, bytes_ = "gmm_score_kernel", 4.0 * S * C * D * B * T, (4 * D + 4 * S) * B * T
+    elif wl == "neural":
+        # NeuralHMM recursions (neural.py:391-511) at the north-star shape with a transition
+        # matrix per (sequence, step): the network outputs log_obs (B,T,N) and
+        # log_A = log(softmax + 1e-8) (B,T,N,N) (4.2 GB) are resident in HBM; one step =
+        # forward_backward (posteriors, forward, backward) + viterbi_decode, on two streams.
+        B, T, N = args.batch, args.T, args.N
+        lo = torch.randn(B, T, N, device=dev, generator=gx) * 3 - 40
+        if os.environ.get("HMM355_TV_STATIC"):   # diagnostic: one matrix for every step (L2-resident)
+            lA = torch.log(torch.softmax(torch.randn(N, N, device=dev, generator=gx) * 2, dim=-1) + 1e-8)
+        else:
+            lA = torch.log(torch.softmax(torch.randn(B, T, N, N, device=dev, generator=gx) * 2, dim=-1) + 1e-8)
+        only = os.environ.get("HMM355_TV_ONLY", "")   # diagnostic: "fb" or "vit"
+        init = torch.full((N,), -math.log(N), device=dev)
+        layer = (lo, lA, init)
+        s_fb, s_vit = torch.cuda.Stream(dev), torch.cuda.Stream(dev)
+        mask = ph.ops.FB_POSTERIOR | ph.ops.FB_FORWARD | ph.ops.FB_BACKWARD
+
+        def step():
+            cur = torch.cuda.current_stream(dev)
+            s_fb.wait_stream(cur)
+            s_vit.wait_stream(cur)
+            r1 = r2 = None
+            if only != "vit":
+                with torch.cuda.stream(s_fb):
+                    r1 = ph.ops.tv_forward_backward(lo, lA, init, mask)
+            if only != "fb":
+                with torch.cuda.stream(s_vit):
+                    r2 = ph.ops.tv_viterbi(lo, lA, init)
+            cur.wait_stream(s_fb)
+            cur.wait_stream(s_vit)
+            return r1, r2
+        desc = {"workload": "NeuralHMM forward_backward + viterbi_decode, per-step transition matrices",
+                "batch_per_gpu": B, "seq_len": T, "num_states": N}
+        # algorithmic bytes per frame: FB reads its step's matrix and emissions, writes
+        # posterior/forward/backward; Viterbi reads matrix + emissions, writes delta + state
+        dom, flops, bytes_ = "tv_pair", None, (8 * N * N + 24 * N + 8) * B * T
     else:  # c5
         B, T, S, D, Dm = 16, 2000, 64, 80, 40
         layer = ph.HSMMLayer(S, D, max_duration=Dm).to(dev)
@@ -233,7 +270,7 @@ def layer_cpu_baseline(wl, layer, budget):
     g = torch.Generator().manual_seed(7)
     frames, elapsed, reps = 0, 0.0, 0
     with torch.no_grad():
-        sd = {k: v.detach().cpu() for k, v in layer.state_dict().items()}
+        sd = {k: v.detach().cpu() for k, v in layer.state_dict().items()} if wl != "neural" else None
         while reps == 0 or (elapsed < budget and reps < 64):
             t0 = time.perf_counter()
             if wl == "c1":
@@ -254,6 +291,14 @@ def layer_cpu_baseline(wl, layer, budget):
                 lp = O.mixture_log_probs(x, sd["mixture_weights_logits"], sd["means"], sd["log_vars"], t_chunk=250)
                 O.mixture_viterbi(lp, O.mixture_log_transitions(sd["transition_logits"]))
                 n = 2000
+            elif wl == "neural":
+                lo, lA, init = layer
+                b, Tn = frames // 200 % lo.shape[0], 200
+                lo_b, lA_b = lo[b:b + 1, :Tn].cpu().numpy(), lA[b:b + 1, :Tn].cpu().numpy()
+                t0 = time.perf_counter()   # time the restatement only, not the device->host copy
+                O.c_tv_fb64(lo_b, lA_b, init.cpu().numpy())
+                O.c_tv_viterbi(lo_b, lA_b, init.cpu().numpy())
+                n = Tn
             else:
                 x = torch.randn(1, 2000, 80, generator=g)
                 lp = O.hsmm_log_probs(x, sd["observation_means"], sd["observation_log_vars"])
@@ -264,8 +309,10 @@ def layer_cpu_baseline(wl, layer, budget):
             frames += n
             reps += 1
     kind_note = {"c1": "B=2 T=100", "c2": "B=2 of 32, T=2000", "c3": "B=1 of 32, T=2000",
-                 "c5": "B=1 of 16, T=2000; HSMM recursion in the C restatement (1 thread)"}[wl]
-    return {"value": frames / elapsed, "unit": "frames/s", "cores": threads if wl != "c5" else 1, "kind": "port",
+                 "c5": "B=1 of 16, T=2000; HSMM recursion in the C restatement (1 thread)",
+                 "neural": "one sequence x 200 steps; the C restatement (fp64 FB + fp32 Viterbi, 1 thread)"}[wl]
+    return {"value": frames / elapsed, "unit": "frames/s", "cores": threads if wl not in ("c5", "neural") else 1,
+            "kind": "port",
             "sample": f"{reps} x ({kind_note}) oracle restatement of the reference op sequence, {elapsed:.1f}s"}
 
 

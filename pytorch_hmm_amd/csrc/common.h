@@ -108,7 +108,8 @@ __device__ __forceinline__ float row16_sum(float x) {
 
 // (value, index) argmax combine: larger value wins; equal values -> smaller index
 __device__ __forceinline__ void argmax_combine(float& v, int& i, float v2, int i2) {
-  bool take = (v2 > v) || (v2 == v && i2 < i);
+  // bitwise, not short-circuit: || / && here compile to exec-mask branches
+  const bool take = (v2 > v) | ((v2 == v) & (i2 < i));
   v = take ? v2 : v;
   i = take ? i2 : i;
 }

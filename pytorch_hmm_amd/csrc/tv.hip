@@ -43,14 +43,21 @@ namespace hmm355 {
 template <int NP>
 struct TvGeo {
   static constexpr int NT = 512;           // 8 waves
-  static constexpr int SLICE = NP / 8;     // columns (alpha/Viterbi) or rows (beta) per wave
-  static constexpr int QW = NP / 32;       // alpha: column quads per wave
-  static constexpr int RL = 64 / QW;       // alpha: row lanes
-  static constexpr int KA = NP / RL;       // alpha: rows per lane
-  static constexpr int KB = NP / 64;       // beta: rows per lane
-  static constexpr int MB = NP / 32;       // beta: column quads per lane
+  // alpha / Viterbi: wave w = (column block cb = w % CB, row part p = w / CB) holds 32 columns
+  // of RPP rows; lane (q = l & 7, r = l >> 3) the column quad q of rows p*RPP + r + 8k, k < KA,
+  // so every load instruction reads 8 whole 128-B row segments
+  static constexpr int CB = NP / 32;
+  static constexpr int RH = 8 / CB;        // row parts: partial results the readers combine
+  static constexpr int RPP = NP / RH;
+  static constexpr int KA = RPP / 8;
+  // beta: wave w holds rows [NP/8 w, +NP/8) of every column; lane (qq = l & 7, r = l >> 3)
+  static constexpr int SLICE = NP / 8;
+  static constexpr int KB = NP / 64;       // rows per lane
+  static constexpr int MB = NP / 32;       // column quads per lane
   static constexpr int NV = KA;            // float4 per lane per step (= KB * MB)
-  static constexpr int PD = NP == 64 ? 8 : (NP == 128 ? 4 : 1);  // steps in flight
+  static constexpr int PD = NP == 64 ? 8 : (NP == 128 ? 3 : 1);  // steps in flight
+  // alpha / Viterbi LDS per parity: P[RH][NP] partials, I[RH][NP] argmax rows, S[8] wave sums
+  static constexpr int BUF = 2 * RH * NP + 8;
   static_assert(KB * MB == KA, "slice shapes");
 };
 
@@ -69,7 +76,14 @@ struct TvArgs {
 
 enum TvKind : int { kTvAlpha = 0, kTvBeta = 1, kTvVit = 2 };
 
-// one step's slice of the matrix (float4 per entry of dst; -inf outside N x N)
+// one step's slice of the matrix, one float4 per entry of dst.  Every lane issues its loads
+// unconditionally and uses the values as loaded: an out-of-range entry reads a clamped
+// in-range (finite) address, and its contribution vanishes downstream instead of being
+// masked here — padded rows meet u = 0 (alpha), padded columns meet w = 0 (beta) or
+// delta = -inf (Viterbi), and padded outputs are multiplied by E = 0 / added to lo = -inf.
+// Nothing touches a prefetched register before the step that consumes it, and each ring
+// slot is reloaded only after its last use, so the loop-carried registers coalesce (no
+// copies at the back edge) and the compiler's vmcnt waits stay one ring slot deep.
 template <int NP, int KIND, bool VEC>
 __device__ __forceinline__ void tv_load(const TvArgs& a, int b, int kmat, float4 (&dst)[TvGeo<NP>::NV]) {
   using G = TvGeo<NP>;
@@ -84,32 +98,31 @@ __device__ __forceinline__ void tv_load(const TvArgs& a, int b, int kmat, float4
       i = G::SLICE * w + (l >> 3) + 8 * k;
       c0 = 4 * ((l & 7) + 8 * m);
     } else {
-      i = (l / G::QW) + G::RL * v;
-      c0 = G::SLICE * w + 4 * (l % G::QW);
+      i = (w / G::CB) * G::RPP + (l >> 3) + 8 * v;
+      c0 = 32 * (w % G::CB) + 4 * (l & 7);
     }
-    const float* p = base + (size_t)i * N + c0;
+    const float* p = base + (size_t)(i < N ? i : N - 1) * N;
     if (VEC) {
-      if (i < N && c0 < N) dst[v] = *reinterpret_cast<const float4*>(p);
-      else dst[v] = make_float4(-INFINITY, -INFINITY, -INFINITY, -INFINITY);
+      dst[v] = *reinterpret_cast<const float4*>(p + (c0 < N ? c0 : N - 4));
     } else {
-      const bool ri = i < N;
-      dst[v].x = (ri && c0 < N) ? p[0] : -INFINITY;
-      dst[v].y = (ri && c0 + 1 < N) ? p[1] : -INFINITY;
-      dst[v].z = (ri && c0 + 2 < N) ? p[2] : -INFINITY;
-      dst[v].w = (ri && c0 + 3 < N) ? p[3] : -INFINITY;
+      dst[v].x = p[c0 < N ? c0 : N - 1];
+      dst[v].y = p[c0 + 1 < N ? c0 + 1 : N - 1];
+      dst[v].z = p[c0 + 2 < N ? c0 + 2 : N - 1];
+      dst[v].w = p[c0 + 3 < N ? c0 + 3 : N - 1];
     }
   }
 }
 
 __device__ __forceinline__ float f4(const float4& v, int c) { return c == 0 ? v.x : (c == 1 ? v.y : (c == 2 ? v.z : v.w)); }
 
-// alpha / Viterbi: full sum over the row lanes (bits log2(QW)..5 of the lane id)
-template <int QW>
-__device__ __forceinline__ float rowlanes_sum(float x) {
-  if (QW <= 2) x += dpp_f<0x4E>(x);   // xor 2
-  if (QW <= 4) x += dpp_f<0x124>(x);  // row_ror:4
-  if (QW <= 8) x += dpp_f<0x128>(x);  // row_ror:8
-  return rows_sum(x);                 // xor 16, xor 32
+// sum over the whole wave of a value held twice (lanes l and l ^ 8 after the row-lane
+// reduction): the pair sum is exact, so the result is the sum over the 32 distinct values
+__device__ __forceinline__ float wave_sum_pairs(float x) {
+  x += dpp_f<0x128>(x);  // row_ror:8 (the duplicate)
+  x += dpp_f<0xB1>(x);
+  x += dpp_f<0x4E>(x);
+  x += dpp_f<0x124>(x);
+  return 0.5f * rows_sum(x);
 }
 
 // alpha: the four column partials reduced over the row lanes, transposed: lane keeps column
@@ -190,43 +203,114 @@ __device__ void tv_chain(const TvArgs& a, float* lds, int b) {
   constexpr int PD = G::PD;
   const int tid = threadIdx.x, w = tid >> 6, l = tid & 63;
   const int T = a.T, N = a.N;
-  float* vbuf = lds;  // [2][NP]
+  constexpr bool COLS = KIND != kTvBeta;   // alpha / Viterbi layout
 
   // this lane's output index after the reduction, and whether it is the lane that stores it
   int jo;
   bool writer;
+  const int part = w / G::CB, r8 = l >> 3;
   if (KIND == kTvBeta) {
-    const int r = l >> 3;
     int kk = 0;
     if (G::KB == 2) kk = (l >> 2) & 1;
     if (G::KB == 4) kk = 2 * ((l >> 2) & 1) + ((l >> 1) & 1);
-    jo = G::SLICE * w + r + 8 * kk;
+    jo = G::SLICE * w + r8 + 8 * kk;
     writer = G::KB == 1 ? (l & 7) == 0 : (G::KB == 2 ? (l & 3) == 0 : (l & 1) == 0);
   } else {
     const int cc = 2 * (l >> 5) + ((l >> 4) & 1);
-    jo = G::SLICE * w + 4 * (l % G::QW) + cc;
-    writer = ((l / G::QW) & (16 / G::QW - 1)) == 0;
+    jo = 32 * (w % G::CB) + 4 * (l & 7) + cc;
+    writer = (l & 8) == 0;
   }
-  // alpha / Viterbi read the previous vector in row-lane order: pos(i) = (i % RL) * KA + i / RL
-  auto pos = [&](int i) { return KIND == kTvBeta ? i : (i % G::RL) * G::KA + i / G::RL; };
-  const int rl = l / G::QW;  // alpha / Viterbi row lane
+  // alpha / Viterbi partial vectors are stored so that a lane's KA rows are contiguous
+  auto perm = [&](int i) { return (i / G::RPP) * G::RPP + (i % 8) * G::KA + (i % G::RPP) / 8; };
+  // lanes that publish the previous row (alpha: U row; Viterbi: delta + psi row): in the
+  // column-block-0 waves, quad lane q publishes row k = q of its row lane (KA <= 8) or rows
+  // q, q + 8, ... (KA > 8): every row exactly once, one or a few per lane
+  const bool rowout = COLS && (w % G::CB) == 0 && (l & 7) < G::KA;
+  auto Pbuf = [&](int par) { return lds + par * G::BUF; };                           // [RH][NP]
+  auto Ibuf = [&](int par) { return reinterpret_cast<int*>(lds + par * G::BUF + G::RH * NP); };
+  auto Sbuf = [&](int par) { return lds + par * G::BUF + 2 * G::RH * NP; };          // [8]
+  float* vbuf = lds;  // beta: [2][NP]
 
   auto kmat_of = [&](int q) { return KIND == kTvBeta ? T - 1 - q : q - 1; };
   auto tout_of = [&](int q) { return KIND == kTvBeta ? T - 1 - q : q; };
-  // per-step scalar input of this lane: E at the output time (alpha: scales u_t; beta: forms
-  // the next product input w_t = v_t E_t), or the raw log-emission (Viterbi)
+  // the per-step scalar input (masked at use): E at the output time (alpha: scales u_t; beta:
+  // forms the next product input w_t = v_t E_t) or the raw log-emission (Viterbi)
   auto emis_of = [&](int q) -> float {
-    const int t = tout_of(q);
-    if (KIND == kTvVit) return jo < N ? a.lo[((size_t)b * T + t) * N + jo] : -INFINITY;
+    const int t = tout_of(q < T ? q : T - 1);
+    if (KIND == kTvVit) return a.lo[((size_t)b * T + t) * N + (jo < N ? jo : N - 1)];
     return a.E[((size_t)b * T + t) * NP + jo];
+  };
+  // matrix loads for step q (clamped to the last step past the end: issued unconditionally)
+  // (sched_barrier pins the loads where they are issued: left alone, the scheduler sinks them
+  // to the end of the block, next to their uses in the next iteration, and the step that
+  // consumes the slot then waits for nearly every load in flight)
+  auto prefetch = [&](int q, float4 (&rw)[G::NV]) {
+    __builtin_amdgcn_sched_barrier(0);
+    tv_load<NP, KIND, VEC>(a, b, kmat_of(q < T ? q : T - 1), rw);
+    __builtin_amdgcn_sched_barrier(0);
+  };
+  // alpha / Viterbi: this lane's KA rows of the previous vector = combination of the RH partials
+  auto read_rows = [&](int par, float (&y)[G::KA]) {
+    const float* P = Pbuf(par) + part * G::RPP + r8 * G::KA;
+#pragma unroll
+    for (int h = 0; h < G::RH; ++h) {
+      float x[G::KA];
+      if constexpr (G::KA % 4 == 0) {
+#pragma unroll
+        for (int k4 = 0; k4 < G::KA / 4; ++k4) {
+          const float4 v = *reinterpret_cast<const float4*>(P + h * NP + 4 * k4);
+          x[4 * k4] = v.x; x[4 * k4 + 1] = v.y; x[4 * k4 + 2] = v.z; x[4 * k4 + 3] = v.w;
+        }
+      } else {
+#pragma unroll
+        for (int k2 = 0; k2 < G::KA / 2; ++k2) {
+          const float2 v = *reinterpret_cast<const float2*>(P + h * NP + 2 * k2);
+          x[2 * k2] = v.x; x[2 * k2 + 1] = v.y;
+        }
+      }
+#pragma unroll
+      for (int k = 0; k < G::KA; ++k) y[k] = h == 0 ? x[k] : (KIND == kTvVit ? fmaxf(y[k], x[k]) : y[k] + x[k]);
+    }
+  };
+  // publish row t of the vector in buffer `par` (rowout lanes): alpha the U row (sum of the
+  // partials), Viterbi delta (max of the partials) and psi (the index of the first part
+  // attaining it: parts hold increasing row ranges, so that is the first index)
+  auto publish_row = [&](int par, int t) {
+#pragma unroll
+    for (int kq = 0; kq < (G::KA + 7) / 8; ++kq) {
+      const int k = (l & 7) + 8 * kq;
+      if (k < G::KA) {
+        const int off = part * G::RPP + r8 * G::KA + k;
+        const int i = part * G::RPP + r8 + 8 * k;
+        const float* P = Pbuf(par) + off;
+        if (KIND == kTvAlpha) {
+          float u = P[0];
+#pragma unroll
+          for (int h = 1; h < G::RH; ++h) u += P[h * NP];
+          a.rows[((size_t)b * T + t) * NP + i] = u;
+        } else {
+          const int* I = Ibuf(par) + off;
+          float m = P[0];
+          int arg = I[0];
+#pragma unroll
+          for (int h = 1; h < G::RH; ++h) {
+            const float x = P[h * NP];
+            arg = x > m ? I[h * NP] : arg;
+            m = fmaxf(m, x);
+          }
+          if (i < N) a.rows[((size_t)b * T + t) * N + i] = m;
+          a.psi[((size_t)b * T + t) * NP + i] = (uint8_t)arg;
+        }
+      }
+    }
   };
 
   float4 raw[PD][G::NV];
   float eR[PD];
+  if (T > 1) {
 #pragma unroll
-  for (int s = 0; s < PD; ++s) {
-    if (1 + s < T) {
-      tv_load<NP, KIND, VEC>(a, b, kmat_of(1 + s), raw[s]);
+    for (int s = 0; s < PD; ++s) {
+      prefetch(1 + s, raw[s]);
       eR[s] = emis_of(1 + s);
     }
   }
@@ -238,20 +322,29 @@ __device__ void tv_chain(const TvArgs& a, float* lds, int b) {
     if (KIND == kTvAlpha) v0 = jo < N ? __expf(a.init[jj]) * a.E[(size_t)b * T * NP + jo] : 0.f;
     else if (KIND == kTvBeta) v0 = jo < N ? a.E[((size_t)b * T + T - 1) * NP + jo] * (a.binit ? a.binit[(size_t)b * NP + jo] : 1.f) : 0.f;  // w_{T-1} = E_{T-1} v_{T-1}
     else v0 = jo < N ? a.init[jj] + a.lo[(size_t)b * T * N + jo] : -INFINITY;
-    if (writer) {
-      vbuf[pos(jo)] = v0;
-      if (KIND == kTvAlpha) a.rows[(size_t)b * T * NP + jo] = v0;
-      else if (KIND == kTvBeta) a.rows[((size_t)b * T + T - 1) * NP + jo] = jo < N ? (a.binit ? a.binit[(size_t)b * NP + jo] : 1.f) : 0.f;
-      else if (jo < N) a.rows[(size_t)b * T * N + jo] = v0;
+    if (COLS) {
+      // row part 0 carries the vector, the other parts the identity (0 / -inf)
+      const float pv = part == 0 ? v0 : (KIND == kTvAlpha ? 0.f : -INFINITY);
+      if (writer) {
+        Pbuf(0)[part * NP + perm(jo)] = pv;
+        if (KIND == kTvVit) Ibuf(0)[part * NP + perm(jo)] = 0;
+      }
+      if (KIND == kTvAlpha) {
+        const float sw = wave_sum_pairs(pv);
+        if (l == 0) Sbuf(0)[w] = sw;
+      }
+    } else if (writer) {
+      vbuf[jo] = v0;
+      a.rows[((size_t)b * T + T - 1) * NP + jo] = jo < N ? (a.binit ? a.binit[(size_t)b * NP + jo] : 1.f) : 0.f;
     }
   }
   lds_barrier();
 
   auto step = [&](int q, float4 (&rw)[G::NV], float& er) {
-    const float* prev = vbuf + ((q - 1) & 1) * NP;
-    float* cur = vbuf + (q & 1) * NP;
     const int t = tout_of(q);
     if (KIND == kTvBeta) {
+      const float* prev = vbuf + ((q - 1) & 1) * NP;
+      float* cur = vbuf + (q & 1) * NP;
       float wv[G::MB][4];
 #pragma unroll
       for (int m = 0; m < G::MB; ++m) {
@@ -276,39 +369,23 @@ __device__ void tv_chain(const TvArgs& a, float* lds, int b) {
         }
         z[k] = s0 + s1;
       }
-      const float e_t = er;
-      if (q + PD < T) {
-        tv_load<NP, KIND, VEC>(a, b, kmat_of(q + PD), rw);
-        er = emis_of(q + PD);
-      }
+      prefetch(q + PD, rw);
       const float zz = quadlanes_transpose_sum<G::KB>(z, l);
       const float v = zz * __builtin_amdgcn_rcpf(cs);
       if (writer) {
-        cur[jo] = v * e_t;
+        cur[jo] = v * er;
         a.rows[((size_t)b * T + t) * NP + jo] = v;
       }
       if (tid == 0) a.cs[(size_t)b * T + t] = cs;
+      er = emis_of(q + PD);
     } else {
+      const int pp = (q - 1) & 1, cp = q & 1;
       float y[G::KA];
-      const float* src = prev + rl * G::KA;
-      if constexpr (G::KA % 4 == 0) {
-#pragma unroll
-        for (int k4 = 0; k4 < G::KA / 4; ++k4) {
-          const float4 x = *reinterpret_cast<const float4*>(src + 4 * k4);
-          y[4 * k4] = x.x; y[4 * k4 + 1] = x.y; y[4 * k4 + 2] = x.z; y[4 * k4 + 3] = x.w;
-        }
-      } else {
-#pragma unroll
-        for (int k2 = 0; k2 < G::KA / 2; ++k2) {
-          const float2 x = *reinterpret_cast<const float2*>(src + 2 * k2);
-          y[2 * k2] = x.x; y[2 * k2 + 1] = x.y;
-        }
-      }
+      read_rows(pp, y);
       if (KIND == kTvAlpha) {
-        float cs = 0.f;
-#pragma unroll
-        for (int k = 0; k < G::KA; ++k) cs += y[k];
-        cs = rowlanes_sum<G::QW>(cs);
+        const float4 s0 = *reinterpret_cast<const float4*>(Sbuf(pp));
+        const float4 s1 = *reinterpret_cast<const float4*>(Sbuf(pp) + 4);
+        const float cs = ((s0.x + s0.y) + (s0.z + s0.w)) + ((s1.x + s1.y) + (s1.z + s1.w));   // c_{q-1}
         float acc[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
         for (int k = 0; k < G::KA; ++k) {
@@ -318,74 +395,74 @@ __device__ void tv_chain(const TvArgs& a, float* lds, int b) {
           acc[2] = fmaf(y[k], __expf(A.z), acc[2]);
           acc[3] = fmaf(y[k], __expf(A.w), acc[3]);
         }
-        const float e_t = er;
-        if (q + PD < T) {
-          tv_load<NP, KIND, VEC>(a, b, kmat_of(q + PD), rw);
-          er = emis_of(q + PD);
-        }
-        const float z = rowlanes_transpose_sum<G::QW>(acc);
-        const float u = z * (e_t * __builtin_amdgcn_rcpf(cs));
-        if (writer) {
-          cur[pos(jo)] = u;
-          a.rows[((size_t)b * T + t) * NP + jo] = u;
-        }
+        prefetch(q + PD, rw);
+        const float z = rowlanes_transpose_sum<8>(acc);
+        const float u = z * (er * __builtin_amdgcn_rcpf(cs));
+        if (writer) Pbuf(cp)[part * NP + perm(jo)] = u;
+        const float sw = wave_sum_pairs(u);
+        if (l == 0) Sbuf(cp)[w] = sw;
+        if (rowout) publish_row(pp, q - 1);  // u_{q-1} -> the U row of the posterior pass
         if (tid == 0) a.cs[(size_t)b * T + t] = cs;
+        er = emis_of(q + PD);
       } else {
-        // max-plus with the first index: rows r + RL k increase with k, strict > keeps the first
+        // max-plus with the first index: rows increase with k, strict > keeps the first
+        const int i0 = part * G::RPP + r8;
         float bv[4];
         int bi[4];
         {
           const float4 A = rw[0];
           bv[0] = y[0] + A.x; bv[1] = y[0] + A.y; bv[2] = y[0] + A.z; bv[3] = y[0] + A.w;
-          bi[0] = bi[1] = bi[2] = bi[3] = rl;
+          bi[0] = bi[1] = bi[2] = bi[3] = i0;
         }
 #pragma unroll
         for (int k = 1; k < G::KA; ++k) {
           const float4 A = rw[k];
-          const int ii = rl + G::RL * k;
+          const int ii = i0 + 8 * k;
 #pragma unroll
           for (int c = 0; c < 4; ++c) {
             const float s = y[k] + f4(A, c);
-            const bool gt = s > bv[c];
-            bv[c] = gt ? s : bv[c];
-            bi[c] = gt ? ii : bi[c];
+            bi[c] = s > bv[c] ? ii : bi[c];
+            bv[c] = fmaxf(bv[c], s);
           }
         }
-        const float lo_t = er;
-        if (q + PD < T) {
-          tv_load<NP, KIND, VEC>(a, b, kmat_of(q + PD), rw);
-          er = emis_of(q + PD);
-        }
+        prefetch(q + PD, rw);
         float v;
         int vi;
-        rowlanes_transpose_argmax<G::QW>(bv, bi, v, vi);
-        const float d = v + lo_t;
+        rowlanes_transpose_argmax<8>(bv, bi, v, vi);
+        // fl(max + lo) per part: rounding is monotone, so the readers' max over parts is the
+        // reference's fl(max_i(...) + lo)
+        const float d = v + (jo < N ? er : -INFINITY);
         if (writer) {
-          cur[pos(jo)] = d;
-          if (jo < N) a.rows[((size_t)b * T + t) * N + jo] = d;
-          a.psi[((size_t)b * T + t) * NP + jo] = (uint8_t)vi;
+          Pbuf(cp)[part * NP + perm(jo)] = d;
+          Ibuf(cp)[part * NP + perm(jo)] = vi;
         }
+        if (rowout) publish_row(pp, q - 1);
+        er = emis_of(q + PD);
       }
     }
     lds_barrier();
   };
 
-  for (int q0 = 1; q0 < T; q0 += PD) {
+  // full blocks of PD steps (no exit inside the unrolled body), then the tail
+  int q0 = 1;
+  for (; q0 + PD <= T; q0 += PD) {
 #pragma unroll
-    for (int s = 0; s < PD; ++s) {
-      const int q = q0 + s;
-      if (q >= T) break;
-      step(q, raw[s], eR[s]);
-    }
+    for (int s = 0; s < PD; ++s) step(q0 + s, raw[s], eR[s]);
   }
-  if (KIND == kTvAlpha) {
-    // c_{T-1} = sum u_{T-1} (the sequence log-likelihood), kept in slot t = 0 of CA
-    const float* last = vbuf + ((T - 1) & 1) * NP + rl * G::KA;
-    float cs = 0.f;
 #pragma unroll
-    for (int k = 0; k < G::KA; ++k) cs += last[k];
-    cs = rowlanes_sum<G::QW>(cs);
-    if (tid == 0) a.cs[(size_t)b * T] = cs;
+  for (int s = 0; s < PD; ++s)
+    if (q0 + s < T) step(q0 + s, raw[s], eR[s]);
+  if (COLS) {
+    // the last row: combined from its partials
+    const int pl = (T - 1) & 1;
+    if (rowout) publish_row(pl, T - 1);
+    if (KIND == kTvAlpha) {
+      // c_{T-1} = sum u_{T-1} (the sequence log-likelihood), kept in slot t = 0 of CA
+      if (tid == 0) {
+        const float* S = Sbuf(pl);
+        a.cs[(size_t)b * T] = ((S[0] + S[1]) + (S[2] + S[3])) + ((S[4] + S[5]) + (S[6] + S[7]));
+      }
+    }
   }
 }
 
@@ -430,40 +507,44 @@ __global__ void __launch_bounds__(256) tv_emis_kernel(const float* __restrict__ 
   }
 }
 
-// LA_t = M_0 + sum_{s=1..t} (log CA_s + M_s);  LB_t = bscale + sum_{s=t..T-2} (log CB_s + M_{s+1});
-// loglik = LA_{T-1} + log CA_0 (CA_0 holds sum u_{T-1}).  One wave per sequence, fp64.
+// LA_t = M_0 + sum_{s=1..t} (log CA_s + M_s)  (block 2b), loglik = LA_{T-1} + log CA_0 (CA_0
+// holds sum u_{T-1});  LB_t = bscale + sum_{s=t..T-2} (log CB_s + M_{s+1})  (block 2b+1).
+// One wave per (sequence, direction), fp64 running sums.
 __global__ void __launch_bounds__(64) tv_scan_kernel(const float* __restrict__ CA, const float* __restrict__ CB,
                                                      const float* __restrict__ M, float* __restrict__ LA,
                                                      float* __restrict__ LB, float* __restrict__ loglik,
                                                      const float* __restrict__ bscale, int T) {
-  const int b = blockIdx.x, l = threadIdx.x;
+  const int b = blockIdx.x >> 1, l = threadIdx.x;
   const size_t o = (size_t)b * T;
-  double base = 0.0;
-  for (int t0 = 0; t0 < T; t0 += 64) {
-    const int t = t0 + l;
-    double x = 0.0;
-    if (t < T) x = t == 0 ? (double)M[o] : (double)__logf(CA[o + t]) + (double)M[o + t];
+  if ((blockIdx.x & 1) == 0) {
+    double base = 0.0;
+    for (int t0 = 0; t0 < T; t0 += 64) {
+      const int t = t0 + l;
+      double x = 0.0;
+      if (t < T) x = t == 0 ? (double)M[o] : (double)__logf(CA[o + t]) + (double)M[o + t];
 #pragma unroll
-    for (int off = 1; off < 64; off <<= 1) {
-      const double y = __shfl_up(x, off);
-      if (l >= off) x += y;
+      for (int off = 1; off < 64; off <<= 1) {
+        const double y = __shfl_up(x, off);
+        if (l >= off) x += y;
+      }
+      if (t < T) LA[o + t] = (float)(base + x);
+      base += __shfl(x, 63);
     }
-    if (t < T) LA[o + t] = (float)(base + x);
-    base += __shfl(x, 63);
-  }
-  if (l == 0 && loglik) loglik[b] = (float)(base + (double)__logf(CA[o]));
-  base = bscale ? (double)bscale[b] : 0.0;  // LB_{T-1} = log of the terminal vector's scale
-  for (int t1 = T; t1 > 0; t1 -= 64) {
-    const int t = t1 - 1 - l;  // descending
-    double x = 0.0;
-    if (t >= 0 && t <= T - 2) x = (double)__logf(CB[o + t]) + (double)M[o + t + 1];
+    if (l == 0 && loglik) loglik[b] = (float)(base + (double)__logf(CA[o]));
+  } else {
+    double base = bscale ? (double)bscale[b] : 0.0;  // LB_{T-1} = log of the terminal vector's scale
+    for (int t1 = T; t1 > 0; t1 -= 64) {
+      const int t = t1 - 1 - l;  // descending
+      double x = 0.0;
+      if (t >= 0 && t <= T - 2) x = (double)__logf(CB[o + t]) + (double)M[o + t + 1];
 #pragma unroll
-    for (int off = 1; off < 64; off <<= 1) {
-      const double y = __shfl_up(x, off);
-      if (l >= off) x += y;
+      for (int off = 1; off < 64; off <<= 1) {
+        const double y = __shfl_up(x, off);
+        if (l >= off) x += y;
+      }
+      if (t >= 0) LB[o + t] = (float)(base + x);
+      base += __shfl(x, 63);
     }
-    if (t >= 0) LB[o + t] = (float)(base + x);
-    base += __shfl(x, 63);
   }
 }
 
@@ -539,7 +620,7 @@ static hipError_t launch_tv_fb(const TvArgs& fa, const TvArgs& fb, const PostArg
   }
   e = hipGetLastError();
   if (e != hipSuccess) return e;
-  hipLaunchKernelGGL(tv_scan_kernel, dim3(fa.B), dim3(64), 0, st, w.CA, w.CB, w.M, w.LA, w.LB, loglik, bscale,
+  hipLaunchKernelGGL(tv_scan_kernel, dim3(2 * fa.B), dim3(64), 0, st, w.CA, w.CB, w.M, w.LA, w.LB, loglik, bscale,
                      fa.T);
   e = hipGetLastError();
   if (e != hipSuccess) return e;
