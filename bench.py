@@ -46,7 +46,7 @@ def parse():
                    help="launch every step eagerly instead of replaying one captured HIP graph")
     p.add_argument("--transition", default="left_to_right", choices=["left_to_right", "ergodic"],
                    help="transition matrix of the workload (BASELINE: left_to_right 0.7)")
-    p.add_argument("--workload", default="ns", choices=["ns", "c1", "c2", "c3", "c5", "neural"],
+    p.add_argument("--workload", default="ns", choices=["ns", "c1", "c2", "c3", "c5", "neural", "smk"],
                    help="ns: the BASELINE metric (default).  c1/c2/c3/c5: BASELINE configs 1, 2, 3, 5 "
                         "(HMMLayer, GaussianHMMLayer, MixtureGaussianHMMLayer, HSMMLayer) through the layers")
     return p.parse_args()
@@ -199,6 +199,19 @@ def layer_workload(args, rank, world, dev):
         # algorithmic bytes per frame: FB reads its step's matrix and emissions, writes
         # posterior/forward/backward; Viterbi reads matrix + emissions, writes delta + state
         dom, flops, bytes_ = "tv_pair", None, (8 * N * N + 24 * N + 8) * B * T
+    elif wl == "smk":
+        # SemiMarkovHMM.viterbi_decode (semi_markov.py:455-570) batched over the C5 shape
+        # (the BASELINE C5 text names semi_markov.py): quad scorer + segment Viterbi + backtrace
+        from pytorch_hmm_amd.semi_markov import SemiMarkovHMM
+        B, T, S, D, Dm = 16, 2000, 64, 80, 40
+        layer = SemiMarkovHMM(S, D, max_duration=Dm).to(dev)
+        x = torch.randn(B, T, D, device=dev, generator=gx)
+
+        def step():
+            return layer.viterbi_decode_batch(x)
+        desc = {"workload": "SemiMarkovHMM(64,80,max_duration=40) viterbi_decode (segment Viterbi)",
+                "batch_per_gpu": B, "seq_len": T, "num_states": S, "max_duration": Dm, "feature_dim": D}
+        dom, flops, bytes_ = "smk_fwd_kernel", 2.0 * (S * S * Dm + S * S) * B * T, (4 * D + 8) * B * T
     else:  # c5
         B, T, S, D, Dm = 16, 2000, 64, 80, 40
         layer = ph.HSMMLayer(S, D, max_duration=Dm).to(dev)
@@ -299,6 +312,16 @@ def layer_cpu_baseline(wl, layer, budget):
                 O.c_tv_fb64(lo_b, lA_b, init.cpu().numpy())
                 O.c_tv_viterbi(lo_b, lA_b, init.cpu().numpy())
                 n = Tn
+            elif wl == "smk":
+                # the literal (t, s, d, s', d') recursion of semi_markov.py:455-570 in C; the
+                # reference's Python loop runs ~15 us per candidate, i.e. hours
+                Tn = 100
+                x = torch.randn(Tn, 80, generator=g).numpy()
+                cs, var = layer._gaussian_tables()
+                q = O.c_smk_quad(x, sd["observation_means"].numpy(), var.numpy())
+                O.c_smk_viterbi(q, cs.numpy(), layer._log_initial().numpy(), layer._log_transitions().numpy(),
+                                layer.duration_model.candidate_table().cpu().numpy())
+                n = Tn
             else:
                 x = torch.randn(1, 2000, 80, generator=g)
                 lp = O.hsmm_log_probs(x, sd["observation_means"], sd["observation_log_vars"])
@@ -310,8 +333,9 @@ def layer_cpu_baseline(wl, layer, budget):
             reps += 1
     kind_note = {"c1": "B=2 T=100", "c2": "B=2 of 32, T=2000", "c3": "B=1 of 32, T=2000",
                  "c5": "B=1 of 16, T=2000; HSMM recursion in the C restatement (1 thread)",
+                 "smk": "one sequence x 100 frames; the literal segment Viterbi in C (1 thread)",
                  "neural": "one sequence x 200 steps; the C restatement (fp64 FB + fp32 Viterbi, 1 thread)"}[wl]
-    return {"value": frames / elapsed, "unit": "frames/s", "cores": threads if wl not in ("c5", "neural") else 1,
+    return {"value": frames / elapsed, "unit": "frames/s", "cores": threads if wl not in ("c5", "neural", "smk") else 1,
             "kind": "port",
             "sample": f"{reps} x ({kind_note}) oracle restatement of the reference op sequence, {elapsed:.1f}s"}
 

@@ -177,6 +177,50 @@ int hmm355_tv_viterbi_f32(const float* log_obs, const float* log_A, long long a_
                           int64_t* states, float* log_delta, void* workspace,
                           size_t workspace_bytes, void* stream);
 
+/* ---------------------------------------------------------------------------------
+ * Explicit-duration (semi-Markov) HMM, indexed by segment END time.  Replace
+ * SemiMarkovHMM.viterbi_decode (semi_markov.py:455-570), the segment observation score
+ * SemiMarkovHMM._compute_segment_observation_logprob (semi_markov.py:411-435) and the
+ * segment forward SemiMarkovHMM._unsupervised_forward (semi_markov.py:308-383, whose
+ * intended logaddexp recursion this computes; the reference raises TypeError there).
+ *
+ * hmm355_semimarkov_quad_f32: per-frame Mahalanobis term
+ *   quad[b,t,s] = sum_k ((x[b,t,k] - mu[s,k])^2) / var[s,k]   (k ascending, fp32)
+ *   x (B,T,Df); means_t, vars_t are (Df,S) (transposed); var = exp(logvar) formed by the
+ *   caller with the reference's torch op (semi_markov.py:418).
+ * hmm355_semimarkov_viterbi_f32 / _forward_f32: the segment recursions over
+ *   quad (B,T,S); seg_const (S) or NULL.  Segment score of frames [st, t] in state s:
+ *     seg_const != NULL (gaussian): seg_const[s] - 0.5 * Q   (the reference adds the
+ *        constant -0.5*sum(logvar) - 0.5*D*log(2 pi) once per SEGMENT, :420-424)
+ *     seg_const == NULL (additive, observation_model='neural'): Q
+ *   with Q = quad[st] + quad[st+1] + ... + quad[t] (left to right).
+ *   log_init (S) = log(softmax(initial_logits) + 1e-8); log_T (S,S) = log(softmax(
+ *   transition_logits) + 1e-8) (self-transitions are excluded by the recursion);
+ *   dur_lp (S,Dmax) = DurationModel log-probabilities for d = 1..Dmax.
+ * Viterbi outputs: segments right-aligned in (B,T) int64 seg_states / seg_durs, the last
+ *   seg_count[b] entries of row b in time order; scores (B) = best final delta.  Candidate
+ *   order (s' outer, d' inner, strict >) and fp32 addition order ((prev + logT) then
+ *   (best + obs) + dur) are the reference's, so segmentations are bit-identical given
+ *   identical fp32 quad/table inputs.
+ * Forward outputs: log_prob (B) = LSE over (s,d) of log alpha[T-1]; log_alpha (B,T,S,Dmax)
+ *   optional (NULL = not written), -inf where a segment is impossible.
+ * 1 <= S <= 64, 1 <= Dmax <= 63.
+ * ------------------------------------------------------------------------------ */
+size_t hmm355_semimarkov_workspace_bytes(int B, int T, int S, int Dmax);
+int hmm355_semimarkov_quad_f32(const float* x, const float* means_t, const float* vars_t, int B,
+                               int T, int Df, int S, float* quad, void* stream);
+int hmm355_semimarkov_viterbi_f32(const float* quad, const float* seg_const,
+                                  const float* log_init, const float* log_T,
+                                  const float* dur_lp, int B, int T, int S, int Dmax,
+                                  int64_t* seg_states, int64_t* seg_durs, int* seg_count,
+                                  float* scores, void* workspace, size_t workspace_bytes,
+                                  void* stream);
+int hmm355_semimarkov_forward_f32(const float* quad, const float* seg_const,
+                                  const float* log_init, const float* log_T,
+                                  const float* dur_lp, int B, int T, int S, int Dmax,
+                                  float* log_alpha, float* log_prob, void* workspace,
+                                  size_t workspace_bytes, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -371,3 +371,130 @@ void hsmm_viterbi_fast(const float* lp, const float* dur, const float* logT, int
     *score = best;
     free(Mst); free(psi_s); free(psi_d); free(prevd); free(x); free(dmax);
 }
+
+/* ------------------------------------------------ explicit-duration (semi-Markov) HMM
+ * SemiMarkovHMM (semi_markov.py:195-633), segments indexed by END time.
+ *   smk_quad_f32            per-frame q[t][s] = sum_k ((x - mu)^2) / var, k ascending
+ *                           (semi_markov.py:422-424 per frame; the reference's torch-CPU sum
+ *                           order over k is ISA-dependent).
+ *   smk_viterbi_literal     semi_markov.py:455-570 as written: init (:495-507), the
+ *                           (t, s, d, s', d') loop with strict > (:513-545), the final
+ *                           (s, d) search (:548-556) and the backtrack (:558-568).  Segment
+ *                           score o = cs[s] - 0.5*Q (gaussian, constant once per segment,
+ *                           :416-424) or Q (cs == NULL: additive per-frame scores), with
+ *                           Q = q[st] + q[st+1] + ... + q[t] left to right.
+ *   smk_forward_f64         the segment forward the reference means at :308-383 (logaddexp
+ *                           over the same candidates; it raises TypeError as written), in
+ *                           float64 as a tolerance reference.
+ */
+void smk_quad_f32(const float* x, const float* mu, const float* var, int T, int D, int S, float* q) {
+    for (int t = 0; t < T; ++t)
+        for (int s = 0; s < S; ++s) {
+            float acc = 0.f;
+            for (int k = 0; k < D; ++k) {
+                float d = x[(size_t)t * D + k] - mu[(size_t)s * D + k];
+                acc = acc + (d * d) / var[(size_t)s * D + k];
+            }
+            q[(size_t)t * S + s] = acc;
+        }
+}
+
+static float smk_obs(const float* q, const float* cs, int S, int st, int t, int s) {
+    float Q = q[(size_t)st * S + s];
+    for (int k = st + 1; k <= t; ++k) Q = Q + q[(size_t)k * S + s];
+    return cs ? cs[s] - 0.5f * Q : Q;
+}
+
+/* seg_s / seg_d receive the segments in time order; returns the segment count. */
+int smk_viterbi_literal(const float* q, const float* cs, const float* li, const float* logT,
+                        const float* dur, int T, int S, int Dm, int64_t* seg_s, int64_t* seg_d,
+                        float* score) {
+    size_t n = (size_t)T * S * Dm;
+    float* delta = (float*)malloc(sizeof(float) * n);
+    int* psi_s = (int*)calloc(n, sizeof(int));
+    int* psi_d = (int*)malloc(sizeof(int) * n);
+    for (size_t i = 0; i < n; ++i) { delta[i] = -INFINITY; psi_d[i] = 1; }
+#define DL(t, s, d) delta[((size_t)(t) * S + (s)) * Dm + (d) - 1]
+    for (int s = 0; s < S; ++s)
+        for (int d = 1; d <= (Dm < T ? Dm : T); ++d)
+            DL(d - 1, s, d) = (li[s] + smk_obs(q, cs, S, 0, d - 1, s)) + dur[(size_t)s * Dm + d - 1];
+    for (int t = 0; t < T; ++t)
+        for (int s = 0; s < S; ++s)
+            for (int d = 1; d <= (Dm < t + 1 ? Dm : t + 1); ++d) {
+                if (t - d < 0) continue;
+                float best = -INFINITY;
+                int bs = 0, bd = 1;
+                int pdl = Dm < t - d + 1 ? Dm : t - d + 1;
+                for (int sp = 0; sp < S; ++sp) {
+                    if (sp == s) continue;
+                    for (int dp = 1; dp <= pdl; ++dp) {
+                        float tot = DL(t - d, sp, dp) + logT[(size_t)sp * S + s];
+                        if (tot > best) { best = tot; bs = sp; bd = dp; }
+                    }
+                }
+                if (best > -INFINITY) {
+                    DL(t, s, d) = (best + smk_obs(q, cs, S, t - d + 1, t, s)) + dur[(size_t)s * Dm + d - 1];
+                    psi_s[((size_t)t * S + s) * Dm + d - 1] = bs;
+                    psi_d[((size_t)t * S + s) * Dm + d - 1] = bd;
+                }
+            }
+    float bf = -INFINITY;
+    int fs = 0, fd = 1;
+    for (int s = 0; s < S; ++s)
+        for (int d = 1; d <= (Dm < T ? Dm : T); ++d)
+            if (DL(T - 1, s, d) > bf) { bf = DL(T - 1, s, d); fs = s; fd = d; }
+    *score = bf;
+    int cnt = 0, ct = T - 1, cs_ = fs, cd = fd;
+    int64_t* rs = (int64_t*)malloc(sizeof(int64_t) * T);
+    int64_t* rd = (int64_t*)malloc(sizeof(int64_t) * T);
+    while (ct >= 0) {
+        rs[cnt] = cs_; rd[cnt] = cd; ++cnt;
+        if (ct - cd >= 0) {
+            size_t i = ((size_t)ct * S + cs_) * Dm + cd - 1;
+            int ns = psi_s[i], nd = psi_d[i];
+            ct -= cd; cs_ = ns; cd = nd;
+        } else break;
+    }
+    for (int k = 0; k < cnt; ++k) { seg_s[k] = rs[cnt - 1 - k]; seg_d[k] = rd[cnt - 1 - k]; }
+#undef DL
+    free(rs); free(rd); free(delta); free(psi_s); free(psi_d);
+    return cnt;
+}
+
+static double lse_acc(double a, double b) {
+    if (a == -INFINITY) return b;
+    if (b == -INFINITY) return a;
+    double m = a > b ? a : b;
+    return m + log(exp(a - m) + exp(b - m));
+}
+
+/* log_alpha (T,S,Dm) float64; returns log P(o) */
+double smk_forward_f64(const float* q, const float* cs, const float* li, const float* logT,
+                       const float* dur, int T, int S, int Dm, double* la) {
+    size_t n = (size_t)T * S * Dm;
+    for (size_t i = 0; i < n; ++i) la[i] = -INFINITY;
+#define LA(t, s, d) la[((size_t)(t) * S + (s)) * Dm + (d) - 1]
+    for (int t = 0; t < T; ++t)
+        for (int s = 0; s < S; ++s)
+            for (int d = 1; d <= (Dm < t + 1 ? Dm : t + 1); ++d) {
+                int st = t - d + 1;
+                double Q = q[(size_t)st * S + s];
+                for (int k = st + 1; k <= t; ++k) Q += q[(size_t)k * S + s];
+                double o = cs ? (double)cs[s] - 0.5 * Q : Q;
+                double u = dur[(size_t)s * Dm + d - 1];
+                if (st == 0) { LA(t, s, d) = (double)li[s] + o + u; continue; }
+                double acc = -INFINITY;
+                int pdl = Dm < st ? Dm : st;
+                for (int sp = 0; sp < S; ++sp) {
+                    if (sp == s) continue;
+                    for (int dp = 1; dp <= pdl; ++dp)
+                        acc = lse_acc(acc, LA(st - 1, sp, dp) + (double)logT[(size_t)sp * S + s]);
+                }
+                if (acc > -INFINITY) LA(t, s, d) = acc + o + u;
+            }
+    double tot = -INFINITY;
+    for (int s = 0; s < S; ++s)
+        for (int d = 1; d <= (Dm < T ? Dm : T); ++d) tot = lse_acc(tot, LA(T - 1, s, d));
+#undef LA
+    return tot;
+}

@@ -299,6 +299,11 @@ def c_oracle():
     lib.tv_fb_f64.argtypes = [P, P, L, L, P, I, I, I, P, P, P, P]
     lib.hsmm_viterbi_literal.argtypes = [P, P, P, I, I, I, P, P]
     lib.hsmm_viterbi_fast.argtypes = [P, P, P, I, I, I, P, P]
+    lib.smk_quad_f32.argtypes = [P, P, P, I, I, I, P]
+    lib.smk_viterbi_literal.argtypes = [P, P, P, P, P, I, I, I, P, P, P]
+    lib.smk_viterbi_literal.restype = I
+    lib.smk_forward_f64.argtypes = [P, P, P, P, P, I, I, I, P]
+    lib.smk_forward_f64.restype = ctypes.c_double
     _lib = lib
     return lib
 
@@ -386,6 +391,42 @@ def c_hsmm(lp, dur_lp, log_T, literal=False):
         fn(_p(lpb), _p(du), _p(lT), T, S, Dm, _p(sb), _p(sc))
         states[b], scores[b] = sb, sc[0]
     return states, scores
+
+
+def c_smk_quad(x, means, var):
+    """x (T,D), means/var (S,D) -> q (T,S) float32 (k ascending)."""
+    x, mu, va = _f32(x), _f32(means), _f32(var)
+    T, D = x.shape
+    S = mu.shape[0]
+    q = np.zeros((T, S), np.float32)
+    c_oracle().smk_quad_f32(_p(x), _p(mu), _p(va), T, D, S, _p(q))
+    return q
+
+
+def c_smk_viterbi(q, seg_const, log_init, log_T, dur_lp):
+    """One sequence: q (T,S) -> (segment states, segment durations, score) (semi_markov.py:455-570)."""
+    q = _f32(q)
+    T, S = q.shape
+    Dm = dur_lp.shape[1]
+    cs = None if seg_const is None else _f32(seg_const)
+    ss = np.zeros(T, np.int64)
+    sd = np.zeros(T, np.int64)
+    sc = np.zeros(1, np.float32)
+    n = c_oracle().smk_viterbi_literal(_p(q), None if cs is None else _p(cs), _p(_f32(log_init)),
+                                       _p(_f32(log_T)), _p(_f32(dur_lp)), T, S, Dm, _p(ss), _p(sd), _p(sc))
+    return ss[:n], sd[:n], sc[0]
+
+
+def c_smk_forward64(q, seg_const, log_init, log_T, dur_lp):
+    """One sequence: -> (log P(o), log alpha (T,S,Dmax) float64)."""
+    q = _f32(q)
+    T, S = q.shape
+    Dm = dur_lp.shape[1]
+    cs = None if seg_const is None else _f32(seg_const)
+    la = np.zeros((T, S, Dm))
+    tot = c_oracle().smk_forward_f64(_p(q), None if cs is None else _p(cs), _p(_f32(log_init)),
+                                     _p(_f32(log_T)), _p(_f32(dur_lp)), T, S, Dm, _p(la))
+    return tot, la
 
 
 def uniform_obs(seed, shape, lo=0.0, hi=1.0):

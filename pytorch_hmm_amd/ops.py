@@ -14,7 +14,7 @@ shape-only fake implementations; their only real implementation is the HIP libra
       -> (posterior, forward, backward, loglik, lik_ref)
   torch.ops.hmm355.tv_viterbi(log_obs, log_A, init) -> (states, log_delta)
 """
-from typing import Tuple
+from typing import Optional, Tuple
 
 import torch
 from torch import Tensor
@@ -235,3 +235,96 @@ def tv_viterbi(log_obs: Tensor, log_A: Tensor, init: Tensor) -> Tuple[Tensor, Te
 def _(log_obs, log_A, init):
     B, T, N = log_obs.shape
     return log_obs.new_empty((B, T), dtype=torch.int64), log_obs.new_empty((B, T, N))
+
+
+# ------------------------------------------------------- explicit-duration (semi-Markov)
+@torch.library.custom_op("hmm355::semimarkov_quad", mutates_args=())
+def semimarkov_quad(x: Tensor, means_t: Tensor, vars_t: Tensor) -> Tensor:
+    """(B,T,Df) frames, (Df,S) means / variances -> (B,T,S) sum_k (x-mu)^2/var (k ascending)."""
+    nat.require_gpu(x, means_t, vars_t)
+    x, means_t, vars_t = _f32c(x), _f32c(means_t), _f32c(vars_t)
+    B, T, Df = x.shape
+    S = means_t.shape[1]
+    if means_t.shape[0] != Df or tuple(vars_t.shape) != tuple(means_t.shape):
+        raise ValueError(f"feature dim mismatch: x has {Df}, means {tuple(means_t.shape)}, "
+                         f"variances {tuple(vars_t.shape)} (expected ({Df}, S))")
+    q = torch.empty((B, T, S), device=x.device)
+    with torch.cuda.device(x.device):
+        nat.check(nat.lib().hmm355_semimarkov_quad_f32(
+            nat.ptr(x), nat.ptr(means_t), nat.ptr(vars_t), B, T, Df, S, nat.ptr(q),
+            nat.stream_of(x.device)))
+    return q
+
+
+@semimarkov_quad.register_fake
+def _(x, means_t, vars_t):
+    return x.new_empty((x.shape[0], x.shape[1], means_t.shape[1]))
+
+
+def _smk_args(quad, seg_const, log_init, log_T, dur_lp):
+    nat.require_gpu(quad, seg_const, log_init, log_T, dur_lp)
+    quad, log_init, log_T, dur_lp = _f32c(quad), _f32c(log_init), _f32c(log_T), _f32c(dur_lp)
+    seg_const = None if seg_const is None else _f32c(seg_const)
+    B, T, S = quad.shape
+    if tuple(log_T.shape) != (S, S) or log_init.shape != (S,) or dur_lp.shape[0] != S:
+        raise ValueError(f"parameter shapes {tuple(log_init.shape)}, {tuple(log_T.shape)}, "
+                         f"{tuple(dur_lp.shape)} do not match {S} states")
+    if seg_const is not None and seg_const.shape != (S,):
+        raise ValueError(f"segment constant shape {tuple(seg_const.shape)} != ({S},)")
+    return quad, seg_const, log_init, log_T, dur_lp, B, T, S, dur_lp.shape[1]
+
+
+@torch.library.custom_op("hmm355::semimarkov_viterbi", mutates_args=())
+def semimarkov_viterbi(quad: Tensor, seg_const: Optional[Tensor], log_init: Tensor, log_T: Tensor,
+                       dur_lp: Tensor) -> Tuple[Tensor, Tensor, Tensor, Tensor]:
+    """-> seg_states (B,T) int64, seg_durs (B,T) int64 (right-aligned), seg_count (B) int32,
+    scores (B)."""
+    quad, seg_const, log_init, log_T, dur_lp, B, T, S, Dm = _smk_args(quad, seg_const, log_init, log_T, dur_lp)
+    dev = quad.device
+    seg_s = torch.empty((B, T), dtype=torch.int64, device=dev)
+    seg_d = torch.empty((B, T), dtype=torch.int64, device=dev)
+    cnt = torch.zeros(B, dtype=torch.int32, device=dev)
+    scores = torch.empty(B, device=dev)
+    if B == 0:
+        return seg_s, seg_d, cnt, scores
+    L = nat.lib()
+    ws = _workspace(L.hmm355_semimarkov_workspace_bytes(B, T, S, Dm), dev)
+    with torch.cuda.device(dev):
+        nat.check(L.hmm355_semimarkov_viterbi_f32(
+            nat.ptr(quad), nat.ptr(seg_const), nat.ptr(log_init), nat.ptr(log_T), nat.ptr(dur_lp),
+            B, T, S, Dm, nat.ptr(seg_s), nat.ptr(seg_d), nat.ptr(cnt), nat.ptr(scores),
+            nat.ptr(ws), ws.numel(), nat.stream_of(dev)))
+    return seg_s, seg_d, cnt, scores
+
+
+@semimarkov_viterbi.register_fake
+def _(quad, seg_const, log_init, log_T, dur_lp):
+    B, T, _ = quad.shape
+    return (quad.new_empty((B, T), dtype=torch.int64), quad.new_empty((B, T), dtype=torch.int64),
+            quad.new_empty(B, dtype=torch.int32), quad.new_empty(B))
+
+
+@torch.library.custom_op("hmm355::semimarkov_forward", mutates_args=())
+def semimarkov_forward(quad: Tensor, seg_const: Optional[Tensor], log_init: Tensor, log_T: Tensor,
+                       dur_lp: Tensor, want_alpha: bool) -> Tuple[Tensor, Tensor]:
+    """-> log_prob (B), log_alpha (B,T,S,Dmax) (empty (0,) unless want_alpha)."""
+    quad, seg_const, log_init, log_T, dur_lp, B, T, S, Dm = _smk_args(quad, seg_const, log_init, log_T, dur_lp)
+    dev = quad.device
+    lp = torch.empty(B, device=dev)
+    alpha = torch.empty((B, T, S, Dm) if want_alpha else (0,), device=dev)
+    if B == 0:
+        return lp, alpha
+    L = nat.lib()
+    ws = _workspace(L.hmm355_semimarkov_workspace_bytes(B, T, S, Dm), dev)
+    with torch.cuda.device(dev):
+        nat.check(L.hmm355_semimarkov_forward_f32(
+            nat.ptr(quad), nat.ptr(seg_const), nat.ptr(log_init), nat.ptr(log_T), nat.ptr(dur_lp),
+            B, T, S, Dm, nat.ptr(alpha) if want_alpha else None, nat.ptr(lp),
+            nat.ptr(ws), ws.numel(), nat.stream_of(dev)))
+    return lp, alpha
+
+
+@semimarkov_forward.register_fake
+def _(quad, seg_const, log_init, log_T, dur_lp, want_alpha):
+    B, T, S = quad.shape
+    return quad.new_empty(B), quad.new_empty((B, T, S, dur_lp.shape[1]) if want_alpha else (0,))

@@ -29,6 +29,7 @@ from pytorch_hmm.hmm import HMMPyTorch  # noqa: E402
 from pytorch_hmm.hmm_layer import HMMLayer, GaussianHMMLayer  # noqa: E402
 from pytorch_hmm.mixture_gaussian import MixtureGaussianHMMLayer  # noqa: E402
 from pytorch_hmm.hsmm import HSMMLayer  # noqa: E402
+from pytorch_hmm.semi_markov import SemiMarkovHMM  # noqa: E402
 from pytorch_hmm.neural import NeuralHMM, ContextualNeuralHMM  # noqa: E402
 from pytorch_hmm.utils import (  # noqa: E402
     create_left_to_right_matrix, create_transition_matrix)
@@ -218,6 +219,47 @@ def fx_hsmm(name, S, D, Dmax, B, T, seed):
          states=npf(states), scores=npf(scores), input_sha256=sha(npf(x)))
 
 
+def fx_semimarkov(name, S, D, Dmax, T, nseq, seed, dist="gamma", min_duration=1, obs_model="gaussian"):
+    """SemiMarkovHMM.viterbi_decode (semi_markov.py:455-570), its per-candidate duration
+    log-probabilities (duration_model(tensor([s]), tensor([d]))[0], :502-505), the segment
+    constant (:416-421), DurationModel.forward over all durations (:81-98) and the supervised
+    forward of the decoded segmentation (:280-306).  Eval mode (the neural observation model
+    has dropout)."""
+    torch.manual_seed(seed)
+    m = SemiMarkovHMM(S, D, max_duration=Dmax, duration_distribution=dist, observation_model=obs_model,
+                      min_duration=min_duration)
+    m.eval()
+    x = torch.randn(nseq, T, D)
+    with torch.no_grad():
+        dur = torch.full((S, Dmax), float("nan"))
+        for s_ in range(S):
+            for d in range(1, Dmax + 1):
+                dur[s_, d - 1] = m.duration_model(torch.tensor([s_]), torch.tensor([d]))[0]
+        dist_all = m.duration_model(torch.arange(S))
+        if obs_model == "gaussian":
+            cs = torch.stack([-0.5 * torch.sum(m.observation_logvars[s_]) - 0.5 * D * math.log(2 * math.pi)
+                              for s_ in range(S)])
+        else:
+            cs = torch.zeros(S)
+        t0 = time.time()
+        seg_states, seg_durs, scores, counts, sup = [], [], [], [], []
+        for b in range(nseq):
+            st, du, sc = m.viterbi_decode(x[b])
+            seg_states.append(npf(st)); seg_durs.append(npf(du)); scores.append(float(sc))
+            counts.append(len(st))
+            r = m(x[b:b + 1], st.unsqueeze(0), du.unsqueeze(0))
+            sup.append([float(r[k]) for k in ("log_probability", "log_observation", "log_duration", "log_transition")])
+    print(f"    semimarkov {name}: {time.time()-t0:.1f}s")
+    K = max(counts)
+    pad = lambda a: np.concatenate([a, -np.ones(K - len(a), np.int64)])
+    params = {"param__" + k.replace(".", "__"): npf(v) for k, v in m.state_dict().items()}
+    save(name, x=npf(x), dur_candidates=npf(dur), dur_distribution=npf(dist_all), seg_const=npf(cs),
+         seg_states=np.stack([pad(a) for a in seg_states]), seg_durs=np.stack([pad(a) for a in seg_durs]),
+         seg_count=np.array(counts), scores=np.array(scores, np.float32), supervised=np.array(sup, np.float32),
+         config=np.array([S, D, Dmax, T, nseq, min_duration]), dist=np.array(dist), obs_model=np.array(obs_model),
+         input_sha256=sha(npf(x)), **params)
+
+
 def _neural_capture(m, x, ctx, call_fb, call_vit):
     """Log-emissions, log-transitions, the FB outputs with log_forward / log_backward (the last
     two torch.exp arguments, neural.py:401), Viterbi and compute_likelihood of one NeuralHMM."""
@@ -329,6 +371,13 @@ def main():
         ("hsmm_s5", lambda: fx_hsmm("hsmm_s5", 5, 30, 20, 2, 30, 0)),
         ("hsmm_s2", lambda: fx_hsmm("hsmm_s2", 2, 3, 2, 1, 4, 1)),
         ("hsmm_s8", lambda: fx_hsmm("hsmm_s8", 8, 20, 10, 1, 40, 2)),
+        ("smk_gamma", lambda: fx_semimarkov("smk_gamma", 4, 6, 10, 30, 2, 0)),
+        ("smk_poisson", lambda: fx_semimarkov("smk_poisson", 5, 8, 8, 40, 1, 1, dist="poisson", min_duration=2)),
+        ("smk_gaussian", lambda: fx_semimarkov("smk_gaussian", 6, 5, 12, 48, 1, 2, dist="gaussian")),
+        ("smk_neuraldur", lambda: fx_semimarkov("smk_neuraldur", 4, 6, 6, 20, 2, 3, dist="neural")),
+        ("smk_neuralobs", lambda: fx_semimarkov("smk_neuralobs", 3, 4, 5, 15, 1, 4, obs_model="neural")),
+        ("smk_s8", lambda: fx_semimarkov("smk_s8", 8, 16, 16, 96, 1, 6)),
+        ("smk_short", lambda: fx_semimarkov("smk_short", 3, 4, 10, 4, 2, 5)),
         ("neural_mlp_small", lambda: fx_neural("neural_mlp_small", 5, 8, 12, 64, 2, 20, 0)),
         ("neural_static", lambda: fx_neural("neural_static", 6, 10, 0, 32, 2, 25, 1)),
         ("neural_rnn", lambda: fx_neural("neural_rnn", 7, 6, 4, 16, 2, 15, 2, ttype="rnn")),
