@@ -46,7 +46,7 @@ def parse():
                    help="launch every step eagerly instead of replaying one captured HIP graph")
     p.add_argument("--transition", default="left_to_right", choices=["left_to_right", "ergodic"],
                    help="transition matrix of the workload (BASELINE: left_to_right 0.7)")
-    p.add_argument("--workload", default="ns", choices=["ns", "c1", "c2", "c3", "c5", "neural", "smk"],
+    p.add_argument("--workload", default="ns", choices=["ns", "c1", "c2", "c3", "c5", "neural", "smk", "stream"],
                    help="ns: the BASELINE metric (default).  c1/c2/c3/c5: BASELINE configs 1, 2, 3, 5 "
                         "(HMMLayer, GaussianHMMLayer, MixtureGaussianHMMLayer, HSMMLayer) through the layers")
     return p.parse_args()
@@ -212,6 +212,31 @@ def layer_workload(args, rank, world, dev):
         desc = {"workload": "SemiMarkovHMM(64,80,max_duration=40) viterbi_decode (segment Viterbi)",
                 "batch_per_gpu": B, "seq_len": T, "num_states": S, "max_duration": Dm, "feature_dim": D}
         dom, flops, bytes_ = "smk_fwd_kernel", 2.0 * (S * S * Dm + S * S) * B * T, (4 * D + 8) * B * T
+    elif wl == "stream":
+        # StreamingHMMProcessor decode (streaming.py:267-377) for many concurrent streams: one
+        # 160-frame chunk (the reference's default chunk_size) per stream, emission net
+        # (Linear-ReLU-Linear-LogSoftmax) + greedy chain + beam search (K = 8), N = 64 states
+        from pytorch_hmm_amd.streaming import StreamingHMMProcessor
+        B, T, N, D, K = 256, 160, 64, 80, 8
+        layer = StreamingHMMProcessor(N, D, beam_width=K).to(dev).eval()
+        x = torch.randn(B, T, D, device=dev, generator=gx)
+        log_T = layer._log_transitions()
+        prev = torch.full((B,), -1, dtype=torch.int32, device=dev)
+        hs0 = torch.full((B, ph.ops.STREAM_SLOTS), float("-inf"), device=dev)
+        hs0[:, :K] = -math.log(N)
+        hl0 = torch.zeros((B, ph.ops.STREAM_SLOTS), dtype=torch.int32, device=dev)
+        hl0[:, :K] = torch.arange(K, dtype=torch.int32, device=dev)
+        first = torch.ones(B, dtype=torch.int32, device=dev)
+
+        def step():
+            emis = layer.emission_net(x)
+            g = ph.ops.stream_greedy(emis, log_T, prev, math.log(N))
+            hs, hl = hs0.clone(), hl0.clone()
+            cnt = torch.full((B,), K, dtype=torch.int32, device=dev)
+            return g, ph.ops.stream_beam(emis, log_T, K, hs, hl, cnt, first, live_max=K)
+        desc = {"workload": "StreamingHMMProcessor chunk decode (emission net + greedy + beam K=8), concurrent streams",
+                "batch_per_gpu": B, "seq_len": T, "num_states": N, "feature_dim": D, "beam_width": K}
+        dom, flops, bytes_ = "stream_beam_kernel", None, (4 * D + 8 * N + 16 + 4 * K) * B * T
     else:  # c5
         B, T, S, D, Dm = 16, 2000, 64, 80, 40
         layer = ph.HSMMLayer(S, D, max_duration=Dm).to(dev)
@@ -312,6 +337,17 @@ def layer_cpu_baseline(wl, layer, budget):
                 O.c_tv_fb64(lo_b, lA_b, init.cpu().numpy())
                 O.c_tv_viterbi(lo_b, lA_b, init.cpu().numpy())
                 n = Tn
+            elif wl == "stream":
+                # greedy + beam (K = 8) over one 160-frame chunk of one stream, C restatement of
+                # streaming.py:267-377 (the reference's Python beam loop runs K*N tensor ops per frame)
+                N, K = 64, 8
+                x = torch.randn(160, 80, generator=g)
+                emis = torch.func.functional_call(layer.emission_net, {k[len("emission_net."):]: v for k, v in sd.items()
+                                                                       if k.startswith("emission_net.")}, (x,)).numpy()
+                lT = torch.log(torch.softmax(sd["transition_logits"], dim=-1) + 1e-8).numpy()
+                O.c_stream_greedy(emis, lT, -1, math.log(N))
+                O.c_stream_beam(emis, lT, K, np.full(K, -math.log(N), np.float32), np.arange(K), True)
+                n = 160
             elif wl == "smk":
                 # the literal (t, s, d, s', d') recursion of semi_markov.py:455-570 in C; the
                 # reference's Python loop runs ~15 us per candidate, i.e. hours
@@ -333,9 +369,10 @@ def layer_cpu_baseline(wl, layer, budget):
             reps += 1
     kind_note = {"c1": "B=2 T=100", "c2": "B=2 of 32, T=2000", "c3": "B=1 of 32, T=2000",
                  "c5": "B=1 of 16, T=2000; HSMM recursion in the C restatement (1 thread)",
+                 "stream": "one stream x 160 frames; emission net (torch-CPU) + greedy + beam K=8 in C (1 thread)",
                  "smk": "one sequence x 100 frames; the literal segment Viterbi in C (1 thread)",
                  "neural": "one sequence x 200 steps; the C restatement (fp64 FB + fp32 Viterbi, 1 thread)"}[wl]
-    return {"value": frames / elapsed, "unit": "frames/s", "cores": threads if wl not in ("c5", "neural", "smk") else 1,
+    return {"value": frames / elapsed, "unit": "frames/s", "cores": threads if wl not in ("c5", "neural", "smk", "stream") else 1,
             "kind": "port",
             "sample": f"{reps} x ({kind_note}) oracle restatement of the reference op sequence, {elapsed:.1f}s"}
 

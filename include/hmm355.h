@@ -221,6 +221,33 @@ int hmm355_semimarkov_forward_f32(const float* quad, const float* seg_const,
                                   float* log_alpha, float* log_prob, void* workspace,
                                   size_t workspace_bytes, void* stream);
 
+/* ---------------------------------------------------------------------------------
+ * Streaming decoders of StreamingHMMProcessor, one chunk of B independent streams.
+ *   emis (B,T,N): the emission network's log-probabilities; log_T (N,N) =
+ *   log(softmax(transition_logits) + 1e-8).  1 <= N <= 128.
+ * hmm355_stream_greedy_f32 replaces _greedy_decode (streaming.py:267-320):
+ *   s_t = argmax_j (log_T[s_{t-1}][j] + emis[t][j]), first index on ties; the chain starts
+ *   from prev_state[b], or, when prev_state[b] < 0 (the stream's first chunk), from
+ *   emis[0][j] - log_n with log_n = log(N) in fp32.  states (B,T) int64, scores (B,T) the
+ *   chosen step scores (the reference returns exp(scores)).
+ * hmm355_stream_beam_f32 replaces _beam_search_decode (streaming.py:322-377):
+ *   hyp_score / hyp_last (B,16) and hyp_count (B) (<= 16) hold each stream's hypotheses in
+ *   rank order and are updated in place (a stream may carry more hypotheses than the new K,
+ *   after its beam width was lowered, streaming.py:459-461); first[b] != 0 applies the empty-path rule of the stream's first
+ *   frame (score + emis, no transition).  Each step keeps the K best of the hyp_count * N
+ *   expansions by score descending, ties by expansion index h*N + j ascending (Python's
+ *   stable sort), score = (score_h + log_T[last_h][j]) + emis[t][j] in fp32.
+ *   parent / hstate (B,T,K) int16: new hypothesis r at step t came from hypothesis
+ *   parent[t][r] of step t-1 and entered state hstate[t][r].  states (B,T) int64: the best
+ *   hypothesis' last T states.  1 <= K <= 16; live_max (<= 16) bounds every hyp_count[b].
+ * ------------------------------------------------------------------------------ */
+int hmm355_stream_greedy_f32(const float* emis, const float* log_T, const int* prev_state,
+                             float log_n, int B, int T, int N, int64_t* states, float* scores,
+                             void* stream);
+int hmm355_stream_beam_f32(const float* emis, const float* log_T, int B, int T, int N, int K,
+                           int live_max, float* hyp_score, int* hyp_last, int* hyp_count, const int* first,
+                           int16_t* parent, int16_t* hstate, int64_t* states, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

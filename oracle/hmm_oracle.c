@@ -498,3 +498,65 @@ double smk_forward_f64(const float* q, const float* cs, const float* li, const f
 #undef LA
     return tot;
 }
+
+/* ------------------------------------------------------------- streaming decoders
+ *   stream_greedy_f32  StreamingHMMProcessor._greedy_decode (streaming.py:267-320):
+ *                      s_t = first argmax_j (logT[s_{t-1}][j] + e_t[j]); prev < 0 starts
+ *                      from e_0[j] - log_n (:295-298).
+ *   stream_beam_f32    _beam_search_decode (streaming.py:322-377) as written: expand every
+ *                      hypothesis to every state in (h, j) order, sort by score descending
+ *                      keeping insertion order for ties (Python's stable sort), keep K.
+ *                      hs/hl hold the hypotheses (in/out, *kc of them); paths are tracked
+ *                      as (parent, state) per step, like the kernel's outputs.
+ */
+void stream_greedy_f32(const float* e, const float* logT, int prev, float log_n, int T, int N,
+                       int64_t* states, float* scores) {
+    int sp = prev;
+    for (int t = 0; t < T; ++t) {
+        float best = 0.f;
+        int bi = -1;
+        for (int j = 0; j < N; ++j) {
+            float v = sp < 0 ? e[(size_t)t * N + j] - log_n : logT[(size_t)sp * N + j] + e[(size_t)t * N + j];
+            if (bi < 0 || v > best) { best = v; bi = j; }
+        }
+        states[t] = bi; scores[t] = best; sp = bi;
+    }
+}
+
+typedef struct { float v; int idx; } smk_cand_t;
+static int cand_cmp(const void* a, const void* b) {
+    const smk_cand_t* x = (const smk_cand_t*)a;
+    const smk_cand_t* y = (const smk_cand_t*)b;
+    if (x->v > y->v) return -1;
+    if (x->v < y->v) return 1;
+    return (x->idx > y->idx) - (x->idx < y->idx);
+}
+
+void stream_beam_f32(const float* e, const float* logT, int T, int N, int K, float* hs, int* hl,
+                     int* kc_io, int first, int16_t* parent, int16_t* hstate) {
+    int kc = *kc_io;
+    smk_cand_t* c = (smk_cand_t*)malloc(sizeof(smk_cand_t) * (size_t)(kc > K ? kc : K) * N);
+    float* ns = (float*)malloc(sizeof(float) * K);
+    int* nl = (int*)malloc(sizeof(int) * K);
+    for (int t = 0; t < T; ++t) {
+        int n = 0;
+        for (int h = 0; h < kc; ++h)
+            for (int j = 0; j < N; ++j) {
+                float v = first ? hs[h] + e[(size_t)t * N + j]
+                                : (hs[h] + logT[(size_t)hl[h] * N + j]) + e[(size_t)t * N + j];
+                c[n].v = v; c[n].idx = h * N + j; ++n;
+            }
+        qsort(c, n, sizeof(smk_cand_t), cand_cmp);
+        int kn = n < K ? n : K;
+        for (int r = 0; r < kn; ++r) {
+            ns[r] = c[r].v; nl[r] = c[r].idx % N;
+            parent[(size_t)t * K + r] = (int16_t)(c[r].idx / N);
+            hstate[(size_t)t * K + r] = (int16_t)nl[r];
+        }
+        for (int r = 0; r < kn; ++r) { hs[r] = ns[r]; hl[r] = nl[r]; }
+        kc = kn;
+        first = 0;
+    }
+    *kc_io = kc;
+    free(c); free(ns); free(nl);
+}

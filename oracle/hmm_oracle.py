@@ -304,6 +304,8 @@ def c_oracle():
     lib.smk_viterbi_literal.restype = I
     lib.smk_forward_f64.argtypes = [P, P, P, P, P, I, I, I, P]
     lib.smk_forward_f64.restype = ctypes.c_double
+    lib.stream_greedy_f32.argtypes = [P, P, I, ctypes.c_float, I, I, P, P]
+    lib.stream_beam_f32.argtypes = [P, P, I, I, I, P, P, P, I, P, P]
     _lib = lib
     return lib
 
@@ -427,6 +429,32 @@ def c_smk_forward64(q, seg_const, log_init, log_T, dur_lp):
     tot = c_oracle().smk_forward_f64(_p(q), None if cs is None else _p(cs), _p(_f32(log_init)),
                                      _p(_f32(log_T)), _p(_f32(dur_lp)), T, S, Dm, _p(la))
     return tot, la
+
+
+def c_stream_greedy(emis, log_T, prev, log_n):
+    """emis (T,N) -> states (T,) int64, scores (T,) float32 (streaming.py:267-320)."""
+    e = _f32(emis)
+    T, N = e.shape
+    st = np.zeros(T, np.int64)
+    sc = np.zeros(T, np.float32)
+    c_oracle().stream_greedy_f32(_p(e), _p(_f32(log_T)), int(prev), float(np.float32(log_n)), T, N, _p(st), _p(sc))
+    return st, sc
+
+
+def c_stream_beam(emis, log_T, K, hyp_scores, hyp_last, first):
+    """One chunk of streaming.py:322-377.  Returns (new scores, new last states, parent (T,K),
+    state (T,K)); hypothesis r at step t came from parent[t, r] and entered state[t, r]."""
+    e = _f32(emis)
+    T, N = e.shape
+    kc = len(hyp_scores)
+    hs = np.zeros(max(K, kc), np.float32); hs[:kc] = hyp_scores
+    hl = np.zeros(max(K, kc), np.int32); hl[:kc] = hyp_last
+    kio = np.array([kc], np.int32)
+    par = np.zeros((T, K), np.int16)
+    hst = np.zeros((T, K), np.int16)
+    c_oracle().stream_beam_f32(_p(e), _p(_f32(log_T)), T, N, K, _p(hs), _p(hl), _p(kio), int(first), _p(par), _p(hst))
+    k = int(kio[0])
+    return hs[:k].copy(), hl[:k].copy(), par, hst
 
 
 def uniform_obs(seed, shape, lo=0.0, hi=1.0):

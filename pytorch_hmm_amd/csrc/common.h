@@ -124,6 +124,28 @@ __device__ __forceinline__ void wave_argmax(float& v, int& i) {
   }
 }
 
+// full-wave (value, index) argmax on DPP + permlane swaps (no LDS round trips): the four
+// in-row levels by quad_perm / row_ror, then the two cross-row levels by permlane16/32 swaps.
+// Every lane ends with the wave's (max value, smallest index attaining it).
+__device__ __forceinline__ void wave_argmax_dpp(float& v, int& i) {
+  argmax_combine(v, i, dpp_f<0xB1>(v), dpp_i<0xB1>(i));
+  argmax_combine(v, i, dpp_f<0x4E>(v), dpp_i<0x4E>(i));
+  argmax_combine(v, i, dpp_f<0x124>(v), dpp_i<0x124>(i));
+  argmax_combine(v, i, dpp_f<0x128>(v), dpp_i<0x128>(i));
+  float a = v, b = v;
+  int ia = i, ib = i;
+  permlane16_swap(a, b);
+  permlane16_swap_i(ia, ib);
+  argmax_combine(a, ia, b, ib);
+  float c = a, d = a;
+  int ic = ia, id = ia;
+  permlane32_swap(c, d);
+  permlane32_swap_i(ic, id);
+  argmax_combine(c, ic, d, id);
+  v = c;
+  i = ic;
+}
+
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll
   for (int off = 32; off >= 1; off >>= 1) v += __shfl_xor(v, off);

@@ -328,3 +328,59 @@ def semimarkov_forward(quad: Tensor, seg_const: Optional[Tensor], log_init: Tens
 def _(quad, seg_const, log_init, log_T, dur_lp, want_alpha):
     B, T, S = quad.shape
     return quad.new_empty(B), quad.new_empty((B, T, S, dur_lp.shape[1]) if want_alpha else (0,))
+
+
+# ------------------------------------------------------------------ streaming decoders
+STREAM_SLOTS = 16   # hypothesis slots per stream (max beam width)
+
+@torch.library.custom_op("hmm355::stream_greedy", mutates_args=())
+def stream_greedy(emis: Tensor, log_T: Tensor, prev_state: Tensor, log_n: float) -> Tuple[Tensor, Tensor]:
+    """(B,T,N) emission log-probs -> greedy chain states (B,T) int64 and step scores (B,T).
+    prev_state (B) int32: the stream's last decoded state, or -1 for its first chunk."""
+    nat.require_gpu(emis, log_T, prev_state)
+    emis, log_T = _f32c(emis), _f32c(log_T)
+    prev_state = prev_state.to(torch.int32).contiguous()
+    B, T, N = emis.shape
+    states = torch.empty((B, T), dtype=torch.int64, device=emis.device)
+    scores = torch.empty((B, T), device=emis.device)
+    with torch.cuda.device(emis.device):
+        nat.check(nat.lib().hmm355_stream_greedy_f32(
+            nat.ptr(emis), nat.ptr(log_T), nat.ptr(prev_state), float(log_n), B, T, N,
+            nat.ptr(states), nat.ptr(scores), nat.stream_of(emis.device)))
+    return states, scores
+
+
+@stream_greedy.register_fake
+def _(emis, log_T, prev_state, log_n):
+    B, T, _ = emis.shape
+    return emis.new_empty((B, T), dtype=torch.int64), emis.new_empty((B, T))
+
+
+def stream_beam(emis: Tensor, log_T: Tensor, beam_width: int, hyp_score: Tensor, hyp_last: Tensor,
+                hyp_count: Tensor, first: Tensor, live_max: int = STREAM_SLOTS):
+    """One chunk of beam search for B streams.  hyp_score (B,16) fp32, hyp_last (B,16) int32
+    and hyp_count (B) int32 are the streams' hypotheses (rank order, STREAM_SLOTS slots),
+    updated IN PLACE; K = beam_width <= 16;
+    first (B) int32 marks streams whose paths are still empty; live_max bounds hyp_count.  Returns (best-path states
+    (B,T) int64, parent (B,T,K) int16, state (B,T,K) int16): new hypothesis r at step t came
+    from hypothesis parent[t, r] of step t-1 and entered state[t, r]."""
+    nat.require_gpu(emis, log_T, hyp_score, hyp_last, hyp_count, first)
+    emis, log_T = _f32c(emis), _f32c(log_T)
+    B, T, N = emis.shape
+    K = int(beam_width)
+    for name, ten, dt in (("hyp_score", hyp_score, torch.float32), ("hyp_last", hyp_last, torch.int32),
+                          ("hyp_count", hyp_count, torch.int32), ("first", first, torch.int32)):
+        if ten.dtype != dt or not ten.is_contiguous():
+            raise ValueError(f"{name} must be a contiguous {dt} tensor")
+    if tuple(hyp_score.shape) != (B, STREAM_SLOTS) or tuple(hyp_last.shape) != (B, STREAM_SLOTS):
+        raise ValueError(f"hypothesis tensors must be ({B}, {STREAM_SLOTS})")
+    dev = emis.device
+    states = torch.empty((B, T), dtype=torch.int64, device=dev)
+    parent = torch.empty((B, T, K), dtype=torch.int16, device=dev)
+    hstate = torch.empty((B, T, K), dtype=torch.int16, device=dev)
+    with torch.cuda.device(dev):
+        nat.check(nat.lib().hmm355_stream_beam_f32(
+            nat.ptr(emis), nat.ptr(log_T), B, T, N, K, int(live_max), nat.ptr(hyp_score), nat.ptr(hyp_last),
+            nat.ptr(hyp_count), nat.ptr(first), nat.ptr(parent), nat.ptr(hstate), nat.ptr(states),
+            nat.stream_of(dev)))
+    return states, parent, hstate

@@ -1,0 +1,319 @@
+"""Real-time streaming decoder — drop-in for the reference's streaming.py (§8(f) row 4).
+
+``StreamingHMMProcessor`` (streaming.py:35-503) keeps the reference's constructor,
+parameter names (``transition_logits``, ``emission_net``) and chunk/buffer behaviour.  Its two
+per-frame Python loops run as gfx950 kernels (csrc/stream.hip): ``_greedy_decode``
+(streaming.py:267-320) as one wave-argmax chain per chunk and ``_beam_search_decode``
+(streaming.py:322-377) as K rounds of wave argmax per frame over the hypotheses'
+expansions, with the reference's stable tie order.  The emission network stays a torch
+module (two GEMMs on hipBLASLt); the chunk buffering and bookkeeping are host logic, as in
+the reference.  ``AdaptiveLatencyController`` (streaming.py:506-593) is mirrored as is.
+"""
+import queue
+import threading
+import time
+import warnings
+from collections import deque
+from dataclasses import dataclass
+from typing import Any, Dict, Optional, Tuple
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from . import ops
+
+
+@dataclass
+class StreamingResult:
+    """Result of one processed chunk (streaming.py:23-32)."""
+    decoded_states: Optional[torch.Tensor]
+    confidence: float
+    processing_time_ms: float
+    buffer_size: int
+    chunk_id: int
+    status: str
+    metadata: Dict[str, Any]
+
+
+class StreamingHMMProcessor(nn.Module):
+    def __init__(self, num_states: int, feature_dim: int, chunk_size: int = 160, overlap_size: int = 80,
+                 lookahead_frames: int = 5, max_delay_frames: int = 50, use_beam_search: bool = True,
+                 beam_width: int = 8, buffer_size: int = 1000):
+        super().__init__()
+        self.num_states = num_states
+        self.feature_dim = feature_dim
+        self.chunk_size = chunk_size
+        self.overlap_size = overlap_size
+        self.lookahead_frames = lookahead_frames
+        self.max_delay_frames = max_delay_frames
+        self.use_beam_search = use_beam_search
+        self.beam_width = beam_width
+        self.buffer_size = buffer_size
+        self.transition_logits = nn.Parameter(torch.randn(num_states, num_states) * 0.1)
+        self.emission_net = nn.Sequential(
+            nn.Linear(feature_dim, 128), nn.ReLU(), nn.Dropout(0.1), nn.Linear(128, num_states),
+            nn.LogSoftmax(dim=-1))
+        self.reset_streaming_state()
+        self.processing_times = deque(maxlen=1000)
+        self.chunk_counter = 0
+        self.total_frames_processed = 0
+        self.processing_queue = queue.Queue(maxsize=self.buffer_size)
+        self.result_queue = queue.Queue(maxsize=self.buffer_size)
+        self.is_processing = False
+        self.processing_thread = None
+
+    # -- stream state (streaming.py:102-117) ------------------------------------------------
+    def reset_streaming_state(self):
+        self.feature_buffer = deque(maxlen=self.max_delay_frames + self.lookahead_frames)
+        self.viterbi_states = []
+        self.viterbi_scores = []
+        self.beam_hypotheses = []
+        self.last_output_frame = -1
+        self.chunk_counter = 0
+        self.total_frames_processed = 0
+        if self.use_beam_search:
+            init = -torch.log(torch.tensor(self.num_states, dtype=torch.float))
+            self.beam_hypotheses = [(init, [], s) for s in range(min(self.beam_width, self.num_states))]
+
+    def get_transition_matrix(self) -> torch.Tensor:
+        return F.softmax(self.transition_logits, dim=-1)
+
+    def _log_transitions(self):
+        """log(softmax + 1e-8) (streaming.py:289-290), formed on a CPU copy — the reference's
+        path is torch-CPU — so the kernels see its bits."""
+        lt = torch.log(F.softmax(self.transition_logits.detach().cpu(), dim=-1) + 1e-8)
+        return lt.to(self.transition_logits.device)
+
+    # -- async helpers (streaming.py:123-181) -----------------------------------------------
+    def start_async_processing(self):
+        if self.is_processing:
+            return
+        self.is_processing = True
+        self.processing_thread = threading.Thread(target=self._async_processing_loop, daemon=True)
+        self.processing_thread.start()
+
+    def stop_async_processing(self):
+        self.is_processing = False
+        if self.processing_thread:
+            self.processing_thread.join()
+
+    def _async_processing_loop(self):
+        while self.is_processing:
+            try:
+                chunk = self.processing_queue.get(timeout=0.1)
+                result = self.process_chunk(chunk)
+                if not self.result_queue.full():
+                    self.result_queue.put(result)
+                self.processing_queue.task_done()
+            except queue.Empty:
+                continue
+            except Exception as e:  # noqa: BLE001 — the reference warns and keeps serving
+                warnings.warn(f"Error in async processing: {e}")
+
+    def add_audio_chunk_async(self, audio_chunk: torch.Tensor) -> bool:
+        try:
+            self.processing_queue.put_nowait(audio_chunk)
+            return True
+        except queue.Full:
+            return False
+
+    def get_result_async(self) -> Optional[StreamingResult]:
+        try:
+            return self.result_queue.get_nowait()
+        except queue.Empty:
+            return None
+
+    # -- chunk processing (streaming.py:183-265) --------------------------------------------
+    def process_chunk(self, audio_chunk: torch.Tensor) -> StreamingResult:
+        t0 = time.time()
+        for frame in audio_chunk:
+            self.feature_buffer.append(frame)
+        available = len(self.feature_buffer)
+        required = self.chunk_size + self.lookahead_frames
+        if available < required:
+            return StreamingResult(None, 0.0, (time.time() - t0) * 1000, available, self.chunk_counter,
+                                   "buffering", {"frames_needed": required - available})
+        start = max(0, self.last_output_frame + 1)
+        end = available - self.lookahead_frames
+        if end <= start:
+            return StreamingResult(None, 0.0, (time.time() - t0) * 1000, available, self.chunk_counter,
+                                   "waiting_for_lookahead", {})
+        features = torch.stack(list(self.feature_buffer)[start:end])
+        states, conf = self._decode(features)
+        self.last_output_frame = end - 1
+        self.total_frames_processed += len(features)
+        dt = (time.time() - t0) * 1000
+        self.processing_times.append(dt)
+        self.chunk_counter += 1
+        rtf = (len(features) * 1000 / 100) / dt if dt > 0 else float("inf")
+        return StreamingResult(states, conf.mean().item() if conf is not None else 0.0, dt, available,
+                               self.chunk_counter, "decoded",
+                               {"frames_processed": len(features), "real_time_factor": rtf,
+                                "buffer_utilization": available / self.feature_buffer.maxlen})
+
+    def _decode(self, features):
+        return self._beam_search_decode(features) if self.use_beam_search else self._greedy_decode(features)
+
+    def flush_buffer(self) -> Optional[StreamingResult]:
+        if len(self.feature_buffer) == 0:
+            return None
+        states, conf = self._decode(torch.stack(list(self.feature_buffer)))
+        self.chunk_counter += 1
+        return StreamingResult(states, conf.mean().item() if conf is not None else 0.0, 0.0, 0, self.chunk_counter,
+                               "flushed", {"final_chunk": True})
+
+    # -- decoders (streaming.py:267-377) on the GPU -----------------------------------------
+    def _greedy_decode(self, features: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor]:
+        """One greedy chain over the chunk; continues from the stream's last state."""
+        with torch.no_grad():
+            emis = self.emission_net(features)
+            prev = self.viterbi_states[-1] if self.viterbi_states else -1
+            prev_t = torch.tensor([prev], dtype=torch.int32, device=emis.device)
+            log_n = float(torch.log(torch.tensor(self.num_states)))
+            states, scores = ops.stream_greedy(emis.unsqueeze(0), self._log_transitions(), prev_t, log_n)
+            states, scores = states[0], scores[0]
+            self.viterbi_states.extend(states.tolist())
+            self.viterbi_scores.extend(scores.tolist())
+            if len(self.viterbi_states) > self.max_delay_frames:
+                excess = len(self.viterbi_states) - self.max_delay_frames
+                self.viterbi_states = self.viterbi_states[excess:]
+                self.viterbi_scores = self.viterbi_scores[excess:]
+        return states, torch.exp(scores)
+
+    def _beam_search_decode(self, features: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor]:
+        """Beam search over the chunk; the hypotheses (score, path, last state) carry over."""
+        T = features.shape[0]
+        with torch.no_grad():
+            emis = self.emission_net(features)
+            dev = emis.device
+            K = self.beam_width
+            hyps = self.beam_hypotheses
+            kc = len(hyps)
+            if not 1 <= K <= ops.STREAM_SLOTS or kc > ops.STREAM_SLOTS:
+                raise ValueError(f"beam_width must be in [1, {ops.STREAM_SLOTS}] on this path, got {K}")
+            hs = torch.full((1, ops.STREAM_SLOTS), float("-inf"), device=dev)
+            hl = torch.zeros((1, ops.STREAM_SLOTS), dtype=torch.int32, device=dev)
+            if kc:
+                hs[0, :kc] = torch.stack([torch.as_tensor(h[0], dtype=torch.float32) for h in hyps]).to(dev)
+                hl[0, :kc] = torch.tensor([h[2] for h in hyps], dtype=torch.int32, device=dev)
+            cnt = torch.tensor([kc], dtype=torch.int32, device=dev)
+            first = torch.tensor([int(kc > 0 and all(len(h[1]) == 0 for h in hyps))], dtype=torch.int32, device=dev)
+            states, parent, hstate = ops.stream_beam(emis.unsqueeze(0), self._log_transitions(), K, hs, hl, cnt, first,
+                                                     live_max=max(kc, 1))
+            # rebuild the hypotheses' paths: new hypothesis r descends from old hypothesis h0
+            kn = int(cnt.item())
+            par, hst = parent[0].cpu().tolist(), hstate[0].cpu().tolist()
+            new = []
+            for r in range(kn):
+                tail, rr = [], r
+                for t in range(T - 1, -1, -1):
+                    tail.append(hst[t][rr])
+                    rr = par[t][rr]
+                tail.reverse()
+                new.append((hs[0, r], hyps[rr][1] + tail, hl[0, r].item()))
+            self.beam_hypotheses = new
+            best_score, best_path, _ = new[0]
+            st = states[0] if len(best_path) >= T else torch.tensor(best_path, dtype=torch.long, device=dev)
+            conf = torch.full((T,), float(torch.exp(best_score.cpu() / len(best_path))), device=dev)
+        return st, conf
+
+    # -- monitoring (streaming.py:409-503) ---------------------------------------------------
+    def get_performance_stats(self) -> Dict[str, float]:
+        if not self.processing_times:
+            return {"message": "No processing data available"}
+        times = list(self.processing_times)
+        avg = sum(times) / len(times)
+        frame_ms = self.chunk_size * 1000 / 100
+        return {
+            "total_chunks_processed": self.chunk_counter,
+            "total_frames_processed": self.total_frames_processed,
+            "avg_processing_time_ms": avg, "max_processing_time_ms": max(times),
+            "min_processing_time_ms": min(times),
+            "std_processing_time_ms": torch.tensor(times).std().item(),
+            "real_time_factor": frame_ms / avg if avg > 0 else float("inf"),
+            "throughput_fps": self.total_frames_processed / (sum(times) / 1000) if times else 0,
+            "buffer_utilization": len(self.feature_buffer) / self.feature_buffer.maxlen,
+            "chunk_size": self.chunk_size, "lookahead_frames": self.lookahead_frames,
+            "beam_width": self.beam_width if self.use_beam_search else 1,
+            "processing_mode": "beam_search" if self.use_beam_search else "greedy",
+        }
+
+    def optimize_for_latency(self, target_latency_ms: float = 50.0):
+        stats = self.get_performance_stats()
+        if "avg_processing_time_ms" not in stats:
+            warnings.warn("No performance data available for optimization")
+            return
+        cur = stats["avg_processing_time_ms"]
+        if cur > target_latency_ms:
+            if self.use_beam_search and self.beam_width > 2:
+                self.beam_width = max(2, self.beam_width - 1)
+                print(f"Reduced beam width to {self.beam_width}")
+            elif self.use_beam_search:
+                self.use_beam_search = False
+                print("Switched to greedy decoding for lower latency")
+            elif self.chunk_size > 80:
+                self.chunk_size = max(80, int(self.chunk_size * 0.8))
+                print(f"Reduced chunk size to {self.chunk_size}")
+        elif cur < target_latency_ms * 0.5:
+            if not self.use_beam_search:
+                self.use_beam_search = True
+                self.beam_width = 4
+                print("Enabled beam search for better accuracy")
+            elif self.beam_width < 8:
+                self.beam_width += 1
+                print(f"Increased beam width to {self.beam_width}")
+
+    def get_latency_breakdown(self) -> Dict[str, float]:
+        stats = self.get_performance_stats()
+        if "avg_processing_time_ms" not in stats:
+            return {}
+        tot = stats["avg_processing_time_ms"]
+        shares = {"feature_extraction": 0.1, "emission_computation": 0.3, "transition_computation": 0.1,
+                  "viterbi_decoding": 0.4, "bookkeeping": 0.1}
+        out = {k: tot * v for k, v in shares.items()}
+        out["total"] = tot
+        return out
+
+
+class AdaptiveLatencyController:
+    """Chunk-size / beam recommendations from recent latencies (streaming.py:506-593)."""
+
+    def __init__(self, initial_chunk_size: int = 160, min_chunk_size: int = 80, max_chunk_size: int = 320,
+                 target_latency_ms: float = 50.0, adaptation_rate: float = 0.1):
+        self.chunk_size = initial_chunk_size
+        self.min_chunk_size = min_chunk_size
+        self.max_chunk_size = max_chunk_size
+        self.target_latency_ms = target_latency_ms
+        self.adaptation_rate = adaptation_rate
+        self.latency_history = deque(maxlen=100)
+        self.adjustment_cooldown = 0
+        self.last_adjustment_time = 0
+
+    def update(self, processing_time_ms: float, buffer_size: int) -> Dict[str, Any]:
+        self.latency_history.append(processing_time_ms)
+        now = time.time()
+        if now - self.last_adjustment_time < 1.0 or len(self.latency_history) < 10:
+            return {}
+        recent = list(self.latency_history)[-20:]
+        avg = sum(recent) / len(recent)
+        var = torch.tensor(recent).var().item()
+        rec = {}
+        if avg > self.target_latency_ms * 1.2:
+            if self.chunk_size > self.min_chunk_size:
+                self.chunk_size = max(self.min_chunk_size, int(self.chunk_size * (1 - self.adaptation_rate)))
+                rec["chunk_size"] = self.chunk_size
+            rec["beam_width"] = max(1, int(4 * 0.8))
+            rec["use_beam_search"] = not avg > self.target_latency_ms * 2
+        elif avg < self.target_latency_ms * 0.6 and var < 10.0:
+            if self.chunk_size < self.max_chunk_size and buffer_size > 100:
+                self.chunk_size = min(self.max_chunk_size, int(self.chunk_size * (1 + self.adaptation_rate)))
+                rec["chunk_size"] = self.chunk_size
+            rec["beam_width"] = min(8, 6)
+            rec["use_beam_search"] = True
+        elif var > 25.0:
+            rec["use_beam_search"] = False
+            rec["chunk_size"] = max(self.min_chunk_size, int(self.chunk_size * 0.9))
+        if rec:
+            self.last_adjustment_time = now
+        return rec

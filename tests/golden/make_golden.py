@@ -30,6 +30,7 @@ from pytorch_hmm.hmm_layer import HMMLayer, GaussianHMMLayer  # noqa: E402
 from pytorch_hmm.mixture_gaussian import MixtureGaussianHMMLayer  # noqa: E402
 from pytorch_hmm.hsmm import HSMMLayer  # noqa: E402
 from pytorch_hmm.semi_markov import SemiMarkovHMM  # noqa: E402
+from pytorch_hmm.streaming import StreamingHMMProcessor  # noqa: E402
 from pytorch_hmm.neural import NeuralHMM, ContextualNeuralHMM  # noqa: E402
 from pytorch_hmm.utils import (  # noqa: E402
     create_left_to_right_matrix, create_transition_matrix)
@@ -260,6 +261,49 @@ def fx_semimarkov(name, S, D, Dmax, T, nseq, seed, dist="gamma", min_duration=1,
          input_sha256=sha(npf(x)), **params)
 
 
+def fx_streaming(name, N, D, K, lens, seed, chunk_size=20, max_delay=50, lookahead=3, n_proc=6):
+    """StreamingHMMProcessor (streaming.py:35-503), eval mode (the emission net has dropout):
+    _greedy_decode and _beam_search_decode called directly on consecutive chunks (the
+    emission log-probs, returned states / confidences and, for beam, the hypotheses after
+    each chunk), then process_chunk on a fresh stream of n_proc chunks (statuses, states)."""
+    torch.manual_seed(seed)
+    g = StreamingHMMProcessor(N, D, chunk_size=chunk_size, lookahead_frames=lookahead, max_delay_frames=max_delay,
+                              use_beam_search=False).eval()
+    b = StreamingHMMProcessor(N, D, chunk_size=chunk_size, lookahead_frames=lookahead, max_delay_frames=max_delay,
+                              use_beam_search=True, beam_width=K).eval()
+    b.load_state_dict(g.state_dict())
+    feats = [torch.randn(L, D) for L in lens]
+    out = {}
+    t0 = time.time()
+    with torch.no_grad():
+        for i, f in enumerate(feats):
+            out[f"emis{i}"] = npf(g.emission_net(f))
+            st, conf = g._greedy_decode(f)
+            out[f"greedy_states{i}"], out[f"greedy_conf{i}"] = npf(st), npf(conf)
+            st, conf = b._beam_search_decode(f)
+            out[f"beam_states{i}"], out[f"beam_conf{i}"] = npf(st), npf(conf)
+            out[f"beam_hs{i}"] = np.array([float(h[0]) for h in b.beam_hypotheses], np.float32)
+            out[f"beam_hl{i}"] = np.array([h[2] for h in b.beam_hypotheses], np.int64)
+            out[f"beam_plen{i}"] = np.array([len(h[1]) for h in b.beam_hypotheses], np.int64)
+            out[f"beam_path0_{i}"] = np.array(b.beam_hypotheses[0][1], np.int64)
+        out["log_T"] = npf(torch.log(g.get_transition_matrix() + 1e-8))
+        # process_chunk on fresh streams (greedy and beam)
+        chunks = [torch.randn(chunk_size // 2 + 3, D) for _ in range(n_proc)]
+        for tag, proc in (("pg", g), ("pb", b)):
+            proc.reset_streaming_state()
+            for i, c in enumerate(chunks):
+                r = proc.process_chunk(c)
+                out[f"{tag}_status{i}"] = np.array(r.status)
+                out[f"{tag}_states{i}"] = npf(r.decoded_states) if r.decoded_states is not None else np.zeros(0, np.int64)
+                out[f"{tag}_conf{i}"] = np.array(r.confidence, np.float64)
+        for i, c in enumerate(chunks):
+            out[f"chunk{i}"] = npf(c)
+    print(f"    streaming {name}: {time.time()-t0:.1f}s")
+    params = {"param__" + k.replace(".", "__"): npf(v) for k, v in g.state_dict().items()}
+    save(name, config=np.array([N, D, K, chunk_size, max_delay, lookahead, len(lens), n_proc]),
+         **{f"feat{i}": npf(f) for i, f in enumerate(feats)}, **out, **params)
+
+
 def _neural_capture(m, x, ctx, call_fb, call_vit):
     """Log-emissions, log-transitions, the FB outputs with log_forward / log_backward (the last
     two torch.exp arguments, neural.py:401), Viterbi and compute_likelihood of one NeuralHMM."""
@@ -376,6 +420,9 @@ def main():
         ("smk_gaussian", lambda: fx_semimarkov("smk_gaussian", 6, 5, 12, 48, 1, 2, dist="gaussian")),
         ("smk_neuraldur", lambda: fx_semimarkov("smk_neuraldur", 4, 6, 6, 20, 2, 3, dist="neural")),
         ("smk_neuralobs", lambda: fx_semimarkov("smk_neuralobs", 3, 4, 5, 15, 1, 4, obs_model="neural")),
+        ("stream_n5", lambda: fx_streaming("stream_n5", 5, 30, 4, [40, 25, 33], 0)),
+        ("stream_n12", lambda: fx_streaming("stream_n12", 12, 16, 8, [64, 70, 9], 1, chunk_size=30)),
+        ("stream_n3k16", lambda: fx_streaming("stream_n3k16", 3, 8, 16, [10, 12], 2)),
         ("smk_s8", lambda: fx_semimarkov("smk_s8", 8, 16, 16, 96, 1, 6)),
         ("smk_short", lambda: fx_semimarkov("smk_short", 3, 4, 10, 4, 2, 5)),
         ("neural_mlp_small", lambda: fx_neural("neural_mlp_small", 5, 8, 12, 64, 2, 20, 0)),

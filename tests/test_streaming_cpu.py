@@ -1,0 +1,74 @@
+"""CPU: the streaming-decoder oracle (oracle/hmm_oracle.c: stream_greedy_f32 /
+stream_beam_f32) against the reference's own StreamingHMMProcessor outputs
+(tests/golden/stream_*.npz, written by tests/golden/make_golden.py): greedy states and
+confidences, beam hypotheses (scores, last states, path lengths) after every chunk, and the
+returned best-path states — all exact, given the reference's emission log-probabilities."""
+import numpy as np
+import pytest
+import torch
+
+from conftest import golden
+from oracle import hmm_oracle as O
+from pytorch_hmm_amd.streaming import AdaptiveLatencyController
+
+NAMES = ["stream_n5", "stream_n12", "stream_n3k16"]
+
+
+def beam_chain(g):
+    """Run the oracle over the fixture's chunks; yields per chunk (hs, hl, plen, states, path0)."""
+    N, D, K = (int(v) for v in g["config"][:3])
+    nchunks = int(g["config"][6])
+    hs = np.full(min(K, N), -float(torch.log(torch.tensor(N, dtype=torch.float))), np.float32)
+    hl = np.arange(min(K, N))
+    paths = [[] for _ in range(len(hs))]
+    first = True
+    for i in range(nchunks):
+        e = g[f"emis{i}"]
+        T = e.shape[0]
+        hs, hl, par, hst = O.c_stream_beam(e, g["log_T"], K, hs, hl, first)
+        first = False
+        new = []
+        for r in range(len(hs)):
+            tail, rr = [], r
+            for t in range(T - 1, -1, -1):
+                tail.append(int(hst[t, rr]))
+                rr = int(par[t, rr])
+            new.append(paths[rr] + tail[::-1])
+        paths = new
+        yield hs, hl, np.array([len(p) for p in paths]), np.array(paths[0][-T:]), np.array(paths[0])
+
+
+@pytest.mark.parametrize("name", NAMES)
+def test_greedy_oracle_matches_reference(name):
+    g = golden(name)
+    N = int(g["config"][0])
+    log_n = float(torch.log(torch.tensor(N)))
+    prev = -1
+    for i in range(int(g["config"][6])):
+        st, sc = O.c_stream_greedy(g[f"emis{i}"], g["log_T"], prev, log_n)
+        assert np.array_equal(st, g[f"greedy_states{i}"])
+        assert np.array_equal(torch.exp(torch.from_numpy(sc)).numpy(), g[f"greedy_conf{i}"])
+        prev = int(st[-1])
+
+
+@pytest.mark.parametrize("name", NAMES)
+def test_beam_oracle_matches_reference(name):
+    g = golden(name)
+    for i, (hs, hl, plen, states, path0) in enumerate(beam_chain(g)):
+        assert np.array_equal(hs, g[f"beam_hs{i}"]), (i, hs, g[f"beam_hs{i}"])
+        assert np.array_equal(hl, g[f"beam_hl{i}"])
+        assert np.array_equal(plen, g[f"beam_plen{i}"])
+        assert np.array_equal(path0, g[f"beam_path0_{i}"])
+        assert np.array_equal(states, g[f"beam_states{i}"])
+        conf = torch.exp(torch.tensor(hs[0]) / int(plen[0]))
+        assert float(conf) == float(g[f"beam_conf{i}"][0])
+
+
+def test_adaptive_latency_controller():
+    """streaming.py:506-593: no advice before 10 samples or within the 1 s cooldown."""
+    c = AdaptiveLatencyController(target_latency_ms=50.0)
+    for _ in range(9):
+        assert c.update(200.0, 0) == {}
+    rec = c.update(200.0, 0)
+    assert rec["chunk_size"] == 144 and rec["use_beam_search"] is False and rec["beam_width"] == 3
+    assert c.update(200.0, 0) == {}   # cooldown
