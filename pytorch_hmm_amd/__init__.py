@@ -2,7 +2,8 @@
 
 Drop-in for the hot path of crlotwhite/pytorch_hmm: HMMPyTorch.forward_backward /
 viterbi_decode / compute_likelihood, HMMLayer, GaussianHMMLayer,
-MixtureGaussianHMMLayer and HSMMLayer, with the per-time-step loops replaced by
+MixtureGaussianHMMLayer and HSMMLayer, and the next rows of that path (NeuralHMM,
+SemiMarkovHMM, StreamingHMMProcessor), with the per-time-step loops replaced by
 hand-written HIP kernels (csrc/) behind the C ABI in include/hmm355.h and the
 torch.library ops in ops.py.  Tensors must be on a ROCm GPU; there is no CPU path.
 """
@@ -25,5 +26,13 @@ except ImportError:  # pragma: no cover
 try:
     from .hsmm import HSMMLayer  # noqa: F401
     __all__ += ["HSMMLayer"]
+except ImportError:  # pragma: no cover
+    pass
+try:
+    from .neural import NeuralHMM, ContextualNeuralHMM  # noqa: F401
+    from .semi_markov import DurationModel, SemiMarkovHMM, AdaptiveDurationHSMM  # noqa: F401
+    from .streaming import StreamingHMMProcessor, StreamingResult, AdaptiveLatencyController  # noqa: F401
+    __all__ += ["NeuralHMM", "ContextualNeuralHMM", "DurationModel", "SemiMarkovHMM", "AdaptiveDurationHSMM",
+                "StreamingHMMProcessor", "StreamingResult", "AdaptiveLatencyController"]
 except ImportError:  # pragma: no cover
     pass
