@@ -396,8 +396,7 @@ def main():
         hmm = ph.HMMPyTorch(ph.create_left_to_right_matrix(N, 0.7))
     g = torch.Generator(device=dev).manual_seed(1234 + rank)
     obs = torch.softmax(torch.randn(B, T, N, device=dev, generator=g), dim=-1)
-    hmm._params_for(obs)
-    lP, lp0 = hmm.log_P.to(dev), hmm.log_p0.to(dev)
+    lP, lp0, plan = hmm._device_params(dev)   # what HMMPyTorch passes (log_P fixed at init)
 
     s_fb = torch.cuda.Stream(dev)
     s_vit = s_fb if args.serial else torch.cuda.Stream(dev)
@@ -408,57 +407,77 @@ def main():
         gather_bufs = ([torch.empty(B, T, N, device=dev) for _ in range(world)],
                        [torch.empty(B, T, dtype=torch.int64, device=dev) for _ in range(world)])
 
-    def step(record):
-        main_s = torch.cuda.current_stream(dev)  # the capture stream while a graph is captured
-        s_fb.wait_stream(main_s)
-        s_vit.wait_stream(main_s)
-        with torch.cuda.stream(s_fb):
-            e0 = torch.cuda.Event(enable_timing=True) if record else None
-            if record:
-                e0.record(s_fb)
-            post, fwd, bwd, _, _ = ops.forward_backward(obs, lP, lp0, ops.OBS_PROB, 7)
-            if record:
-                e1 = torch.cuda.Event(enable_timing=True)
-                e1.record(s_fb)
-                ev["fb"].append((e0, e1))
-        with torch.cuda.stream(s_vit):
-            if record:
-                v0 = torch.cuda.Event(enable_timing=True)
-                v0.record(s_vit)
-            states, delta, _ = ops.viterbi(obs, lP, lp0, ops.OBS_PROB)
-            if record:
-                v1 = torch.cuda.Event(enable_timing=True)
-                v1.record(s_vit)
-                ev["vit"].append((v0, v1))
-        main_s.wait_stream(s_fb)
-        main_s.wait_stream(s_vit)
-        if args.gather and world > 1:
-            if rank == 0:
-                dist.gather(post, gather_bufs[0], dst=0)
-                dist.gather(states, gather_bufs[1], dst=0)
-            else:
-                dist.gather(post, None, dst=0)
-                dist.gather(states, None, dst=0)
-        return post, states
+    def fb_op(record=False):
+        e0 = torch.cuda.Event(enable_timing=True) if record else None
+        if record:
+            e0.record()
+        out = ops.forward_backward(obs, lP, lp0, ops.OBS_PROB, 7, plan)
+        if record:
+            e1 = torch.cuda.Event(enable_timing=True)
+            e1.record()
+            ev["fb"].append((e0, e1))
+        return out
 
+    def vit_op(record=False):
+        v0 = torch.cuda.Event(enable_timing=True) if record else None
+        if record:
+            v0.record()
+        out = ops.viterbi(obs, lP, lp0, ops.OBS_PROB, plan)
+        if record:
+            v1 = torch.cuda.Event(enable_timing=True)
+            v1.record()
+            ev["vit"].append((v0, v1))
+        return out
+
+    def gather(post, states):
+        if rank == 0:
+            dist.gather(post, gather_bufs[0], dst=0)
+            dist.gather(states, gather_bufs[1], dst=0)
+        else:
+            dist.gather(post, None, dst=0)
+            dist.gather(states, None, dst=0)
+
+    # A step is one forward_backward (posterior, forward, backward) and one viterbi_decode of
+    # the batch.  The two ops are independent, so each runs on its own stream; consecutive
+    # steps are stream-ordered per op and pipeline across the two streams (no per-step
+    # cross-stream join: it costs two cross-queue signal hops, ~35 us, per step).
     use_graph = not args.no_graph and not (args.gather and world > 1)
-    graph = None
+    graphs = []
     if use_graph:
-        # one step (both streams) captured as a HIP graph: the timed loop replays it, so the
-        # host launch path (op dispatch, workspace allocation, ctypes) is out of the step
-        for _ in range(2):
-            step(False)
+        # each op captured once as a HIP graph on its stream: the timed loop replays them,
+        # so the host launch path (op dispatch, workspace allocation, ctypes) is out of the step
+        main_s = torch.cuda.current_stream(dev)
+        for s_, op in ((s_fb, fb_op), (s_vit, vit_op)):
+            s_.wait_stream(main_s)
+            with torch.cuda.stream(s_):
+                for _ in range(2):
+                    op()
         torch.cuda.synchronize(dev)
-        graph = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(graph):
-            step(False)
+        for s_, op in ((s_fb, fb_op), (s_vit, vit_op)):
+            gr = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(gr, stream=s_):
+                op()
+            graphs.append((s_, gr))
         torch.cuda.synchronize(dev)
+    graph = graphs[0][1] if graphs else None
 
     def run_step():
-        if graph is not None:
-            graph.replay()
-        else:
-            step(True)
+        if graphs:
+            for s_, gr in graphs:
+                with torch.cuda.stream(s_):
+                    gr.replay()
+            return
+        with torch.cuda.stream(s_fb):
+            post = fb_op()[0]
+        with torch.cuda.stream(s_vit):
+            states = vit_op()[0]
+        if args.gather and world > 1:
+            main_s = torch.cuda.current_stream(dev)
+            main_s.wait_stream(s_fb)
+            main_s.wait_stream(s_vit)
+            gather(post, states)
+            s_fb.wait_stream(main_s)
+            s_vit.wait_stream(main_s)
 
     for _ in range(args.warmup):
         run_step()
@@ -478,12 +497,14 @@ def main():
         tt = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         elapsed = float(tt.item())
-    if graph is not None:
-        # per-op launch durations for the roofline: the same ops, eagerly, HIP events on the
-        # stream each op's kernels run on
-        for _ in range(min(args.steps, 10)):
-            step(True)
-        torch.cuda.synchronize(dev)
+    # per-op launch durations for the roofline: the same ops, eagerly, HIP events on the
+    # stream each op's kernels run on
+    for _ in range(min(args.steps, 10)):
+        with torch.cuda.stream(s_fb):
+            fb_op(True)
+        with torch.cuda.stream(s_vit):
+            vit_op(True)
+    torch.cuda.synchronize(dev)
 
     fb_ms = sum(a.elapsed_time(b) for a, b in ev["fb"]) / len(ev["fb"])
     vit_ms = sum(a.elapsed_time(b) for a, b in ev["vit"]) / len(ev["vit"])
@@ -494,10 +515,10 @@ def main():
     # roofline of the dominant op, algorithmic bytes per SURVEY.md §8(d)
     if fb_ms >= vit_ms:
         dom, dur_ms, bytes_per_launch = "forward_backward", fb_ms, 16 * N * B * T
-        kernels = "band_prep_kernel + fb_recur_kernel + fb_posterior_kernel"
+        kernels = "fb_recur_kernel + fb_posterior_kernel"
     else:
         dom, dur_ms, bytes_per_launch = "viterbi", vit_ms, (8 * N + 8) * B * T
-        kernels = "band_prep_kernel + log_obs_kernel + vit_fwd_kernel + vit_psi_kernel + vit_backtrace_kernel"
+        kernels = "log_obs_kernel + vit_fwd_kernel + vit_psi_kernel + vit_backtrace_kernel"
     achieved = bytes_per_launch / (dur_ms * 1e-3) / 1e9
     traffic, traffic_src = profiled_traffic(dom, B, T, N, args.transition)
     out = {
@@ -510,7 +531,8 @@ def main():
                    "transition": "left_to_right(0.7)" if args.transition == "left_to_right" else "ergodic",
                    "parallelism": f"batch-sharded x{world}",
                    "streams": 1 if args.serial else 2, "gather": bool(args.gather and world > 1),
-                   "hip_graph": graph is not None},
+                   "hip_graph": graph is not None, "step_pipelining": "per-op streams, no per-step join",
+                   "transition_plan": plan is not None},
         "op_ms": {"forward_backward": fb_ms, "viterbi": vit_ms},
         "roofline": {"bound": "hbm", "kernel": dom, "kernels": kernels, "achieved": achieved,
                      "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,

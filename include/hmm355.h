@@ -86,6 +86,27 @@ int hmm355_forward_backward_f32(const float* obs, int obs_mode, const float* log
                                 size_t workspace_bytes, void* stream);
 
 /* ---------------------------------------------------------------------------------
+ * Transition plan: the banded decomposition of log_P (csrc/band.h) measured once into
+ * caller-owned device memory (hmm355_plan_bytes(N) bytes), for callers whose matrix is fixed
+ * across calls (HMMPyTorch computes log_P once in __init__, hmm.py:39-42).  The *_plan_f32
+ * entry points use it instead of re-measuring the matrix on every call; plan == NULL
+ * behaves exactly as the plain entry points.  A plan is valid for the log_P it was made
+ * from; the results are identical with or without it.
+ * ------------------------------------------------------------------------------ */
+size_t hmm355_plan_bytes(int N);
+int hmm355_plan_f32(const float* log_P, int N, void* plan, void* stream);
+int hmm355_forward_backward_plan_f32(const float* obs, int obs_mode, const float* log_P,
+                                     const float* log_p0, const void* plan,
+                                     const float* log_beta_T, int B, int T, int N,
+                                     unsigned out_mask, float* posterior, float* forward,
+                                     float* backward, float* loglik, float* lik_ref,
+                                     void* workspace, size_t workspace_bytes, void* stream);
+int hmm355_viterbi_plan_f32(const float* obs, int obs_mode, const float* log_P, const float* init,
+                            const void* plan, int B, int T, int N, int64_t* states,
+                            float* log_delta, float* final_score, void* workspace,
+                            size_t workspace_bytes, void* stream);
+
+/* ---------------------------------------------------------------------------------
  * Viterbi.  Replaces HMMPyTorch.viterbi_decode (hmm.py:132-184) and
  * MixtureGaussianHMMLayer._viterbi_decode (mixture_gaussian.py:290-338).
  *   init       (N) additive t=0 vector: log_p0 (hmm.py:159), or -log(S) per state

@@ -29,6 +29,7 @@ EXPORTS = (
     "hmm355_semimarkov_workspace_bytes", "hmm355_semimarkov_quad_f32",
     "hmm355_semimarkov_viterbi_f32", "hmm355_semimarkov_forward_f32",
     "hmm355_stream_greedy_f32", "hmm355_stream_beam_f32",
+    "hmm355_plan_bytes", "hmm355_plan_f32", "hmm355_forward_backward_plan_f32", "hmm355_viterbi_plan_f32",
 )
 
 _lib = None
@@ -82,6 +83,12 @@ def lib():
     L.hmm355_semimarkov_forward_f32.argtypes = [P, P, P, P, P, I, I, I, I, P, P, P, S, P]
     L.hmm355_semimarkov_forward_f32.restype = I
     F = ctypes.c_float
+    L.hmm355_plan_bytes.argtypes, L.hmm355_plan_bytes.restype = [I], S
+    L.hmm355_plan_f32.argtypes, L.hmm355_plan_f32.restype = [P, I, P, P], I
+    L.hmm355_forward_backward_plan_f32.argtypes = [P, I, P, P, P, P, I, I, I, U, P, P, P, P, P, P, S, P]
+    L.hmm355_forward_backward_plan_f32.restype = I
+    L.hmm355_viterbi_plan_f32.argtypes = [P, I, P, P, P, I, I, I, P, P, P, P, S, P]
+    L.hmm355_viterbi_plan_f32.restype = I
     L.hmm355_stream_greedy_f32.argtypes, L.hmm355_stream_greedy_f32.restype = [P, P, P, F, I, I, I, P, P, P], I
     L.hmm355_stream_beam_f32.argtypes = [P, P, I, I, I, I, I, P, P, P, P, P, P, P, P]
     L.hmm355_stream_beam_f32.restype = I

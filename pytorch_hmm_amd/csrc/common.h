@@ -146,6 +146,16 @@ __device__ __forceinline__ void wave_argmax_dpp(float& v, int& i) {
   i = ic;
 }
 
+// all-lane wave sum / max on DPP + permlane swaps (no LDS round trips)
+__device__ __forceinline__ float wave_sum_dpp(float x) { return rows_sum(row16_sum(x)); }
+__device__ __forceinline__ float wave_max_dpp2(float x) {
+  x = fmaxf(x, dpp_f<0xB1>(x));
+  x = fmaxf(x, dpp_f<0x4E>(x));
+  x = fmaxf(x, dpp_f<0x124>(x));
+  x = fmaxf(x, dpp_f<0x128>(x));
+  return rows_max(x);
+}
+
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll
   for (int off = 32; off >= 1; off >>= 1) v += __shfl_xor(v, off);

@@ -34,10 +34,10 @@ __global__ void __launch_bounds__(RC<NP>::NT) fb_recur_kernel(RecArgs fa, RecArg
 }
 
 template <int NP>
-static hipError_t launch_fb(const RecArgs& fa, const RecArgs& fb, const PostArgs& pa, hipStream_t st) {
+static hipError_t launch_fb(const RecArgs& fa, const RecArgs& fb, const PostArgs& pa, bool prep, hipStream_t st) {
   hipError_t e = allow_lds(fb_recur_kernel<NP>, kExclusiveLds);  // own the CU (recur.h)
   if (e != hipSuccess) return e;
-  if (fa.band) {
+  if (fa.band && prep) {
     e = launch_band_prep(fa.mat, fa.N, const_cast<BandDesc*>(fa.band), st);
     if (e != hipSuccess) return e;
   }
@@ -88,11 +88,20 @@ HMM355_API size_t hmm355_fb_workspace_bytes(int B, int T, int N) {
   return fb_ws_layout(B, T, N, nullptr, nullptr);
 }
 
-HMM355_API int hmm355_forward_backward_ex_f32(const float* obs, int obs_mode, const float* log_P,
-                                              const float* log_p0, const float* log_beta_T, int B, int T, int N,
-                                              unsigned out_mask, float* posterior, float* forward, float* backward,
-                                              float* loglik, float* lik_ref, void* workspace,
-                                              size_t workspace_bytes, void* stream) {
+HMM355_API size_t hmm355_plan_bytes(int N) { return (N >= 1 && N <= 256) ? sizeof(BandDesc) : 0; }
+
+HMM355_API int hmm355_plan_f32(const float* log_P, int N, void* plan, void* stream) {
+  if (N < 1 || N > 256) return HMM355_E_STATES;
+  if (!log_P || !plan) return HMM355_E_ARG;
+  const hipError_t e = launch_band_prep(log_P, N, static_cast<BandDesc*>(plan), static_cast<hipStream_t>(stream));
+  return e == hipSuccess ? HMM355_OK : (int)e;
+}
+
+HMM355_API int hmm355_forward_backward_plan_f32(const float* obs, int obs_mode, const float* log_P,
+                                                const float* log_p0, const void* plan, const float* log_beta_T,
+                                                int B, int T, int N, unsigned out_mask, float* posterior,
+                                                float* forward, float* backward, float* loglik, float* lik_ref,
+                                                void* workspace, size_t workspace_bytes, void* stream) {
   if (B < 0 || N < 0) return HMM355_E_ARG;
   if (N < 1 || N > 256) return HMM355_E_STATES;
   if (T < 1) return HMM355_E_SHAPE;
@@ -107,7 +116,7 @@ HMM355_API int hmm355_forward_backward_ex_f32(const float* obs, int obs_mode, co
   const int NP = pad_states(N);
   FbWs w;
   fb_ws_layout(B, T, N, static_cast<char*>(workspace), &w);
-  BandDesc* band = use_band() ? w.band : nullptr;
+  BandDesc* band = use_band() ? (plan ? static_cast<BandDesc*>(const_cast<void*>(plan)) : w.band) : nullptr;
   hipStream_t st = static_cast<hipStream_t>(stream);
   const float* binit = nullptr;
   const float* bscale = nullptr;
@@ -127,11 +136,21 @@ HMM355_API int hmm355_forward_backward_ex_f32(const float* obs, int obs_mode, co
   PostArgs pa{w.U, w.V, w.LA, w.LB, posterior, forward, backward, lik_ref, B, T, N, out_mask};
   hipError_t e;
   switch (NP) {
-    case 64: e = launch_fb<64>(fa, fb, pa, st); break;
-    case 128: e = launch_fb<128>(fa, fb, pa, st); break;
-    default: e = launch_fb<256>(fa, fb, pa, st); break;
+    case 64: e = launch_fb<64>(fa, fb, pa, plan == nullptr, st); break;
+    case 128: e = launch_fb<128>(fa, fb, pa, plan == nullptr, st); break;
+    default: e = launch_fb<256>(fa, fb, pa, plan == nullptr, st); break;
   }
   return e == hipSuccess ? HMM355_OK : (int)e;
+}
+
+HMM355_API int hmm355_forward_backward_ex_f32(const float* obs, int obs_mode, const float* log_P,
+                                              const float* log_p0, const float* log_beta_T, int B, int T, int N,
+                                              unsigned out_mask, float* posterior, float* forward, float* backward,
+                                              float* loglik, float* lik_ref, void* workspace,
+                                              size_t workspace_bytes, void* stream) {
+  return hmm355_forward_backward_plan_f32(obs, obs_mode, log_P, log_p0, nullptr, log_beta_T, B, T, N, out_mask,
+                                          posterior, forward, backward, loglik, lik_ref, workspace,
+                                          workspace_bytes, stream);
 }
 
 HMM355_API int hmm355_forward_backward_f32(const float* obs, int obs_mode, const float* log_P,

@@ -38,13 +38,13 @@ __global__ void __launch_bounds__(256) fb_posterior_kernel(PostArgs a) {
     float mu = 0.f, mv = 0.f;
 #pragma unroll
     for (int k = 0; k < K; ++k) { mu = fmaxf(mu, u[k]); mv = fmaxf(mv, v[k]); }
-    mu = wave_max(mu);
-    mv = wave_max(mv);
+    mu = wave_max_dpp2(mu);
+    mv = wave_max_dpp2(mv);
     const float iu = mu > 0.f ? 1.f / mu : 0.f, iv = mv > 0.f ? 1.f / mv : 0.f;
     float p[K], s = 0.f;
 #pragma unroll
     for (int k = 0; k < K; ++k) { p[k] = (u[k] * iu) * (v[k] * iv); s += p[k]; }
-    s = wave_sum(s);
+    s = wave_sum_dpp(s);
     const float is = s > 0.f ? 1.f / s : 0.f;
     const bool last = (row % a.T) == (size_t)(a.T - 1);
     float fw[K];

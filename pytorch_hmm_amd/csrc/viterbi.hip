@@ -89,9 +89,16 @@ __device__ __forceinline__ void psi_band_rows(const VitArgs& a, uint8_t (*prow)[
   const int rows = t_hi - t_first + 1;
   // the chunk's delta rows t_first-1 .. t_hi-1, coalesced, into LDS (row stride NP)
   const float* dsrc = a.delta + ((size_t)b * T + (t_first - 1)) * N;
-  for (int idx = tid; idx < rows * N; idx += C::NT) {
-    const int r = idx / N, c = idx - r * N;
-    drows[r * NP + c] = dsrc[idx];
+  if (N == NP && (reinterpret_cast<uintptr_t>(dsrc) & 15) == 0) {
+    // full rows: 16-B loads, no index division
+    const float4* s4 = reinterpret_cast<const float4*>(dsrc);
+    float4* d4 = reinterpret_cast<float4*>(drows);
+    for (int idx = tid; idx < rows * (NP / 4); idx += C::NT) d4[idx] = s4[idx];
+  } else {
+    for (int idx = tid; idx < rows * N; idx += C::NT) {
+      const int r = idx / N, c = idx - r * N;
+      drows[r * NP + c] = dsrc[idx];
+    }
   }
   __syncthreads();
   float rf[C::NBLK];
@@ -105,7 +112,7 @@ __device__ __forceinline__ void psi_band_rows(const VitArgs& a, uint8_t (*prow)[
       const int i = 64 * blk + l;
       if (i < N) argmax_combine(bv, bi, drows[r * NP + i] + rf[blk], i);
     }
-    wave_argmax(bv, bi);
+    wave_argmax_dpp(bv, bi);
     if (l == 0) { rowM[r] = bv; rowI[r] = bi; }
   }
   // each thread keeps one output column o for all rows (NT is a multiple of NP)
@@ -224,10 +231,10 @@ __global__ void __launch_bounds__(VF<NP>::NT) vit_psi_kernel(VitArgs a) {
 }
 
 template <int NP>
-static hipError_t launch_vit(const VitArgs& va, hipStream_t sm) {
+static hipError_t launch_vit(const VitArgs& va, bool prep, hipStream_t sm) {
   hipError_t e = allow_lds(vit_fwd_kernel<NP>, kExclusiveLds);  // own the CU (recur.h)
   if (e != hipSuccess) return e;
-  if (va.band) {
+  if (va.band && prep) {
     e = launch_band_prep(va.log_P, va.N, const_cast<BandDesc*>(va.band), sm);
     if (e != hipSuccess) return e;
   }
@@ -257,9 +264,9 @@ HMM355_API size_t hmm355_viterbi_workspace_bytes(int B, int T, int N) {
          align_up((size_t)B * T * N * sizeof(float), 256);
 }
 
-HMM355_API int hmm355_viterbi_f32(const float* obs, int obs_mode, const float* log_P, const float* init, int B,
-                                  int T, int N, int64_t* states, float* log_delta, float* final_score,
-                                  void* workspace, size_t workspace_bytes, void* stream) {
+HMM355_API int hmm355_viterbi_plan_f32(const float* obs, int obs_mode, const float* log_P, const float* init,
+                                       const void* plan, int B, int T, int N, int64_t* states, float* log_delta,
+                                       float* final_score, void* workspace, size_t workspace_bytes, void* stream) {
   if (B < 0 || N < 0) return HMM355_E_ARG;
   if (N < 1 || N > 256) return HMM355_E_STATES;
   if (T < 1) return HMM355_E_SHAPE;
@@ -273,11 +280,14 @@ HMM355_API int hmm355_viterbi_f32(const float* obs, int obs_mode, const float* l
   uint8_t* psi = static_cast<uint8_t*>(workspace);
   uint8_t* G = psi + align_up((size_t)B * T * NP, 256);
   uint8_t* bandp = G + align_up((size_t)B * nc * NP, 256);
-  BandDesc* band = use_band() ? reinterpret_cast<BandDesc*>(bandp) : nullptr;
+  BandDesc* band = use_band() ? (plan ? static_cast<BandDesc*>(const_cast<void*>(plan))
+                                      : reinterpret_cast<BandDesc*>(bandp))
+                               : nullptr;
   hipStream_t sm0 = static_cast<hipStream_t>(stream);
   if (obs_mode == HMM355_OBS_PROB) {
     // log(x + 1e-8) once over the whole tensor, full chip (fp64 log, rounded once): the
-    // serial chain then stages plain copies
+    // serial chain then stages plain copies (forming the fp64 logs in the chain's helper
+    // waves instead measured 0.51 ms vs 0.32 ms per call at B=32, T=2000, N=128)
     float* lo = reinterpret_cast<float*>(bandp + align_up(sizeof(BandDesc), 256));
     const hipError_t e0 = launch_log_obs(obs, lo, (size_t)B * T * N, sm0);
     if (e0 != hipSuccess) return (int)e0;
@@ -288,11 +298,18 @@ HMM355_API int hmm355_viterbi_f32(const float* obs, int obs_mode, const float* l
   hipStream_t sm = static_cast<hipStream_t>(stream);
   hipError_t e;
   switch (NP) {
-    case 64: e = launch_vit<64>(va, sm); break;
-    case 128: e = launch_vit<128>(va, sm); break;
-    default: e = launch_vit<256>(va, sm); break;
+    case 64: e = launch_vit<64>(va, plan == nullptr, sm); break;
+    case 128: e = launch_vit<128>(va, plan == nullptr, sm); break;
+    default: e = launch_vit<256>(va, plan == nullptr, sm); break;
   }
   return e == hipSuccess ? HMM355_OK : (int)e;
+}
+
+HMM355_API int hmm355_viterbi_f32(const float* obs, int obs_mode, const float* log_P, const float* init, int B,
+                                  int T, int N, int64_t* states, float* log_delta, float* final_score,
+                                  void* workspace, size_t workspace_bytes, void* stream) {
+  return hmm355_viterbi_plan_f32(obs, obs_mode, log_P, init, nullptr, B, T, N, states, log_delta, final_score,
+                                 workspace, workspace_bytes, stream);
 }
 
 #if HMM355_STAMP

@@ -50,13 +50,24 @@ class HMMPyTorch(HMM):
 
     # -- helpers -------------------------------------------------------------------
     def _params_for(self, obs: torch.Tensor):
-        dev = obs.device
+        """(log_P, log_p0) on the observations' device.  Device copies and the transition
+        plan (ops.make_plan: the banded structure of log_P, measured once) are cached while
+        log_P / log_p0 are unchanged (same storage and version)."""
+        return self._device_params(obs.device)[:2]
+
+    def _device_params(self, dev):
         lp, l0 = self.log_P, self.log_p0
-        if lp.device != dev:
-            lp = lp.to(dev)
-        if l0.device != dev:
-            l0 = l0.to(dev)
-        return lp, l0
+        key = (str(dev), lp.data_ptr(), lp._version, l0.data_ptr(), l0._version)
+        cache = self.__dict__.setdefault("_dev_cache", {})
+        hit = cache.get(str(dev))
+        if hit is None or hit[0] != key or lp.requires_grad or l0.requires_grad:
+            lpd = lp if lp.device == dev else lp.to(dev)
+            l0d = l0 if l0.device == dev else l0.to(dev)
+            plan = ops.make_plan(lpd.detach()) if dev.type == "cuda" else None
+            hit = (key, lpd, l0d, plan)
+            if not (lp.requires_grad or l0.requires_grad):
+                cache[str(dev)] = hit
+        return hit[1], hit[2], hit[3]
 
     @staticmethod
     def _as_batch(observations):
@@ -72,10 +83,10 @@ class HMMPyTorch(HMM):
         obs, _ = self._as_batch(observations)
         B, T, K = obs.shape
         assert K == self.K, f"Observation dim {K} must match model states {self.K}"
-        log_P, log_p0 = self._params_for(obs)
+        log_P, log_p0, plan = self._device_params(obs.device)
         post, fwd, bwd, _, _ = ops.forward_backward(
             obs.detach(), log_P.detach(), log_p0.detach(), ops.OBS_PROB,
-            ops.FB_POSTERIOR | ops.FB_FORWARD | ops.FB_BACKWARD)
+            ops.FB_POSTERIOR | ops.FB_FORWARD | ops.FB_BACKWARD, plan)
         if needs_grad(obs, log_P, log_p0):
             post, fwd, bwd = forward_backward_with_grad(obs, log_P, log_p0, (post, fwd, bwd))
         return post, fwd, bwd
@@ -96,8 +107,8 @@ class HMMPyTorch(HMM):
         obs, squeeze = self._as_batch(observations)
         B, T, K = obs.shape
         assert K == self.K, f"Observation dim {K} must match model states {self.K}"
-        log_P, log_p0 = self._params_for(obs)
-        states, delta, _ = ops.viterbi(obs.detach(), log_P.detach(), log_p0.detach(), ops.OBS_PROB)
+        log_P, log_p0, plan = self._device_params(obs.device)
+        states, delta, _ = ops.viterbi(obs.detach(), log_P.detach(), log_p0.detach(), ops.OBS_PROB, plan)
         if squeeze:
             return states.squeeze(0), delta.squeeze(0)
         return states, delta

@@ -39,9 +39,22 @@ def _workspace(nbytes, device):
 
 
 # ------------------------------------------------------------------ forward-backward
+def make_plan(log_P: Tensor) -> Tensor:
+    """Measure log_P's banded structure once (hmm355_plan_f32) into a device byte tensor that
+    forward_backward / viterbi accept as `plan` (valid while log_P is unchanged)."""
+    nat.require_gpu(log_P)
+    log_P = _f32c(log_P)
+    N = log_P.shape[0]
+    L = nat.lib()
+    plan = torch.empty(L.hmm355_plan_bytes(N), dtype=torch.uint8, device=log_P.device)
+    with torch.cuda.device(log_P.device):
+        nat.check(L.hmm355_plan_f32(nat.ptr(log_P), N, nat.ptr(plan), nat.stream_of(log_P.device)))
+    return plan
+
+
 @torch.library.custom_op("hmm355::forward_backward", mutates_args=())
 def forward_backward(obs: Tensor, log_P: Tensor, log_p0: Tensor, obs_mode: int,
-                     out_mask: int) -> Tuple[Tensor, Tensor, Tensor, Tensor, Tensor]:
+                     out_mask: int, plan: Optional[Tensor] = None) -> Tuple[Tensor, Tensor, Tensor, Tensor, Tensor]:
     nat.require_gpu(obs, log_P, log_p0)
     obs, log_P, log_p0 = _f32c(obs), _f32c(log_P), _f32c(log_p0)
     B, T, N = obs.shape
@@ -57,8 +70,8 @@ def forward_backward(obs: Tensor, log_P: Tensor, log_p0: Tensor, obs_mode: int,
     nbytes = L.hmm355_fb_workspace_bytes(B, T, N)
     ws = _workspace(nbytes, dev)
     with torch.cuda.device(dev):
-        nat.check(L.hmm355_forward_backward_f32(
-            nat.ptr(obs), obs_mode, nat.ptr(log_P), nat.ptr(log_p0), B, T, N, out_mask,
+        nat.check(L.hmm355_forward_backward_plan_f32(
+            nat.ptr(obs), obs_mode, nat.ptr(log_P), nat.ptr(log_p0), nat.ptr(plan), None, B, T, N, out_mask,
             nat.ptr(post) if out_mask & FB_POSTERIOR else None,
             nat.ptr(fwd) if out_mask & FB_FORWARD else None,
             nat.ptr(bwd) if out_mask & FB_BACKWARD else None,
@@ -67,7 +80,7 @@ def forward_backward(obs: Tensor, log_P: Tensor, log_p0: Tensor, obs_mode: int,
 
 
 @forward_backward.register_fake
-def _(obs, log_P, log_p0, obs_mode, out_mask):
+def _(obs, log_P, log_p0, obs_mode, out_mask, plan=None):
     B, T, N = obs.shape
     mk = lambda bit: obs.new_empty((B, T, N) if out_mask & bit else _EMPTY)
     return mk(FB_POSTERIOR), mk(FB_FORWARD), mk(FB_BACKWARD), obs.new_empty(B), obs.new_empty(B)
@@ -75,7 +88,8 @@ def _(obs, log_P, log_p0, obs_mode, out_mask):
 
 # ---------------------------------------------------------------------------- Viterbi
 @torch.library.custom_op("hmm355::viterbi", mutates_args=())
-def viterbi(obs: Tensor, log_P: Tensor, init: Tensor, obs_mode: int) -> Tuple[Tensor, Tensor, Tensor]:
+def viterbi(obs: Tensor, log_P: Tensor, init: Tensor, obs_mode: int,
+            plan: Optional[Tensor] = None) -> Tuple[Tensor, Tensor, Tensor]:
     nat.require_gpu(obs, log_P, init)
     obs, log_P, init = _f32c(obs), _f32c(log_P), _f32c(init)
     B, T, N = obs.shape
@@ -88,14 +102,14 @@ def viterbi(obs: Tensor, log_P: Tensor, init: Tensor, obs_mode: int) -> Tuple[Te
         return states, delta, final
     ws = _workspace(L.hmm355_viterbi_workspace_bytes(B, T, N), dev)
     with torch.cuda.device(dev):
-        nat.check(L.hmm355_viterbi_f32(
-            nat.ptr(obs), obs_mode, nat.ptr(log_P), nat.ptr(init), B, T, N, nat.ptr(states),
+        nat.check(L.hmm355_viterbi_plan_f32(
+            nat.ptr(obs), obs_mode, nat.ptr(log_P), nat.ptr(init), nat.ptr(plan), B, T, N, nat.ptr(states),
             nat.ptr(delta), nat.ptr(final), nat.ptr(ws), ws.numel(), nat.stream_of(dev)))
     return states, delta, final
 
 
 @viterbi.register_fake
-def _(obs, log_P, init, obs_mode):
+def _(obs, log_P, init, obs_mode, plan=None):
     B, T, N = obs.shape
     return (obs.new_empty((B, T), dtype=torch.int64), obs.new_empty((B, T, N)), obs.new_empty(B))
 
