@@ -17,30 +17,37 @@
 //   obs_sum is torch-CPU's order for a strided slice of length d: four accumulators over
 //   whole groups of 4, the tail folded into the first, then ((a0+a1)+a2)+a3.
 //
-// hsmm_fwd_kernel: one 1024-thread workgroup per sequence (16 lanes = one DPP row per
-// state), 3 barriers per start time:
-//   A  group-complete updates of the per-(start,state) accumulators F0..F3 (LDS ring);
-//   B  the S x Dmax candidate values delta[st-1][s'][d'] and their max over d';
-//   C  M[st][s], p1 and xb (row-wide DPP combines).
-//   lp rows arrive 64 at a time into a 128-row LDS ring, prefetched a chunk ahead.
-// hsmm_backtrace_kernel: one wave per sequence walks the segments (hsmm.py:331-352).
+// hsmm_fwd_kernel: one 1024-thread workgroup per sequence, the segment END time t as the
+//   loop index (semimarkov.hip's layout): 16 lanes (one DPP row) per state; lane `sub` owns
+//   the start-time slots k = sub + 16j (mod 64) of its state.  A live segment's torch-order
+//   obs_sum state (the four group accumulators, the pending group and the tail sum) and its
+//   predecessor score M stay in the slot's registers for the segment's life, so a step reads
+//   one lp row, writes delta's per-state maximum Dm for the predecessor phase, and meets at
+//   ONE barrier.  Per end time t it stores M[t][s] (the best fl(delta + logT) over
+//   predecessors ending at t, for segments starting at t+1), the first s' attaining it, and
+//   Dm[t][s].
+// hsmm_backtrace_kernel: one wave per sequence walks the segments (hsmm.py:331-352); for each
+//   segment it recomputes, bit-identically, the candidate deltas of the winning s' to find
+//   the first d' and xb (the best total of the earlier candidates), and re-resolves the rare
+//   case where an earlier candidate rounds to the same total.
 #include "common.h"
 
 namespace hmm355 {
 
 constexpr int kHsS = 64;    // max states
-constexpr int kHsR = 64;    // start-time ring (>= Dmax + 1)
-constexpr int kHsL = 128;   // lp row ring
-constexpr int kHsSub = 16;                 // lanes per state in phases B/C (one DPP row)
+constexpr int kHsR = 64;    // start-time slots (> Dmax)
+constexpr int kHsL = 128;   // lp row ring (two 64-row chunks)
+constexpr int kHsSub = 16;                 // lanes per state (one DPP row)
 constexpr int kHsThreads = kHsS * kHsSub;  // 1024
+constexpr int kHsNJ = 4;                   // slots / predecessor states per lane
 
 struct HsArgs {
   const float* lp;      // (B,T,S)
   const float* dur;     // (S,Dm)
   const float* logT;    // (S,S)
-  float* Mg;            // (B,T,S)
-  uint16_t* P1;         // (B,T,S): s1 | d1 << 8
-  float* XB;            // (B,T,S)
+  float* Mg;            // (B,T,S): M[t][s], best predecessor total for segments starting at t+1
+  uint8_t* S1;          // (B,T,S): first s' attaining M[t][s]
+  float* Dg;            // (B,T,S): Dm[t][s] = max_d delta[t][s][d]
   int* fin;             // (B,2): final (s, d)
   float* scores;        // (B)
   int64_t* states;      // (B,T)
@@ -49,36 +56,12 @@ struct HsArgs {
 
 struct HsLds {
   float lpr[kHsL][kHsS];
-  float Mr[kHsR][kHsS];
-  float F[kHsR][kHsS][4];
-  float cand[kHsS][kHsR];
-  float dmx[kHsS];
-  float logT[kHsS][kHsS];
+  float dur[kHsS][kHsR + 1];
+  float dmx[2][kHsS];
+  int fd[kHsS];
 };
 
-__device__ __forceinline__ float quad_max(float v) {
-  v = fmaxf(v, dpp_f<0xB1>(v));
-  return fmaxf(v, dpp_f<0x4E>(v));
-}
-__device__ __forceinline__ int quad_min_i(int v) {
-  v = min(v, dpp_i<0xB1>(v));
-  return min(v, dpp_i<0x4E>(v));
-}
-
-// torch-order obs_sum from the F accumulators of start st0 (length d, elements up to row st0+d-1)
-__device__ __forceinline__ float hs_obs_sum(const HsLds& L, int st0, int d, int sp) {
-  const float* Fv = L.F[st0 % kHsR][sp];
-  const int g = d >> 2, rt = d & 3;
-  float a0 = Fv[0];
-  for (int i = 0; i < rt; ++i) a0 += L.lpr[(st0 + 4 * g + i) % kHsL][sp];
-  float r = 0.f + a0;
-  r = r + Fv[1];
-  r = r + Fv[2];
-  r = r + Fv[3];
-  return r;
-}
-
-// all-reduce over the 16 lanes of a DPP row (the SUB lanes of one state)
+// all-reduce over the 16 lanes of a DPP row (the lanes of one state)
 __device__ __forceinline__ float row_max16(float v) {
   v = fmaxf(v, dpp_f<0xB1>(v));
   v = fmaxf(v, dpp_f<0x4E>(v));
@@ -97,196 +80,158 @@ __global__ void __launch_bounds__(kHsThreads) hsmm_fwd_kernel(HsArgs a) {
   HsLds& L = *reinterpret_cast<HsLds*>(smem);
   const int b = blockIdx.x, tid = threadIdx.x;
   const int T = a.T, S = a.S, Dm = a.Dm;
+  const int s = tid >> 4, sub = tid & 15;
+  const bool live = s < S;
   const float* lp = a.lp + (size_t)b * T * S;
-  // phases B/C: 16 lanes (one DPP row) per state q; lane `sub` owns d' = sub + 1 + 16j and
-  // s' = sub + 16j
-  const int q = tid >> 4, sub = tid & 15;
-  constexpr int NJ = kHsR / kHsSub;  // 4
 
-  for (int i = tid; i < S * S; i += kHsThreads) L.logT[i / S][i % S] = a.logT[i];
-  float du[NJ];
-#pragma unroll
-  for (int j = 0; j < NJ; ++j) {
-    const int d = sub + 1 + kHsSub * j;
-    const bool ok = q < S && d <= Dm;
-    const float v = a.dur[ok ? (size_t)q * Dm + d - 1 : 0];
-    du[j] = ok ? v : 0.f;
+  for (int i = tid; i < kHsS * kHsR; i += kHsThreads) {
+    const int r = i / kHsR, d = i % kHsR;
+    L.dur[r][d] = (r < S && d < Dm) ? a.dur[(size_t)r * Dm + d] : -INFINITY;
   }
-  // phase-A item walk without integer division in the loop
-  const int a_k0 = tid / S, a_s0 = tid % S;
-  const int a_dk = kHsThreads / S, a_ds = kHsThreads % S;
+  float lt[kHsNJ];  // log T[s'][s] for the lane's predecessor states s' = sub + 16j (-inf: excluded)
+#pragma unroll
+  for (int j = 0; j < kHsNJ; ++j) {
+    const int sp = sub + kHsSub * j;
+    const bool ok = live && sp < S && sp != s;
+    const float v = a.logT[ok ? (size_t)sp * S + s : 0];
+    lt[j] = ok ? v : -INFINITY;
+  }
 
   constexpr int PER = kHsS * 64 / kHsThreads;  // lp values per thread per 64-row chunk
-  auto chunk_load = [&](int c, float (&r)[PER]) {
+  float rc[PER];
+  auto chunk_load = [&](int c) {
 #pragma unroll
     for (int k = 0; k < PER; ++k) {
       const int idx = tid + k * kHsThreads;
       const int row = c * 64 + idx / kHsS, col = idx % kHsS;
       const bool ok = row < T && col < S;
       const float v = lp[ok ? (size_t)row * S + col : 0];
-      r[k] = ok ? v : 0.f;
+      rc[k] = ok ? v : 0.f;
     }
   };
-  auto chunk_store = [&](int c, const float (&r)[PER]) {
+  auto chunk_store = [&](int c) {
 #pragma unroll
     for (int k = 0; k < PER; ++k) {
       const int idx = tid + k * kHsThreads;
-      const int row = c * 64 + idx / kHsS, col = idx % kHsS;
-      L.lpr[row % kHsL][col] = r[k];
+      L.lpr[(c * 64 + idx / kHsS) % kHsL][idx % kHsS] = rc[k];
     }
   };
-  float rc[PER];
-  chunk_load(0, rc);
-  chunk_store(0, rc);
-  if (T > 64) chunk_load(1, rc);
+  chunk_load(0);
+  chunk_store(0);
+  if (T > 64) chunk_load(1);
   __syncthreads();
 
-  // ---- A(st): element row st-1 joins every active start; complete groups fold into F.
-  // Runs for st = 1 before the loop and for st + 1 in the same phase as C(st) (they touch
-  // disjoint LDS), so a start costs two barriers: A+C | B.
-  auto phaseA = [&](int st) {
-    const int e = st - 1;
-    int k = a_k0, sp = a_s0;
-    while (k < Dm) {
-      const int st0 = e - k;  // start whose element index k is row e
-      if (st0 >= 0) {
-        float* Fv = L.F[st0 % kHsR][sp];
-        if (k == 0) { Fv[0] = 0.f; Fv[1] = 0.f; Fv[2] = 0.f; Fv[3] = 0.f; }
-        if ((k & 3) == 3) {  // group [k-3, k] complete
-          Fv[0] += L.lpr[(st0 + k - 3) % kHsL][sp];
-          Fv[1] += L.lpr[(st0 + k - 2) % kHsL][sp];
-          Fv[2] += L.lpr[(st0 + k - 1) % kHsL][sp];
-          Fv[3] += L.lpr[(st0 + k) % kHsL][sp];
-        }
-      }
-      k += a_dk;
-      sp += a_ds;
-      if (sp >= S) { sp -= S; ++k; }
-    }
-  };
-  phaseA(1);
-  __syncthreads();
-
-  for (int st = 1; st <= T; ++st) {
-    // ---- B: candidates delta[st-1][s'][d'-1] and their max over d'
-    const int dlim = Dm < st ? Dm : st;
-    if (q < S) {
-      float mx = -INFINITY;
+  // torch-CPU order of sum(lp[st:st+d, s]) (a strided slice): four accumulators over the
+  // whole groups of 4, the tail folded into the first, then ((a0+a1)+a2)+a3.  Per slot:
+  // G = completed-group sums, Q = the open group's sums (G_i + x_i), A0 = G0 + tail.
+  float G[kHsNJ][4], Q[kHsNJ][4], A0[kHsNJ], mp[kHsNJ];
 #pragma unroll
-      for (int j = 0; j < NJ; ++j) {
-        const int d = sub + 1 + kHsSub * j;
-        if (d <= Dm) {
-          float v = -INFINITY;
-          if (d <= dlim) {
-            const int st0 = st - d;
-            const float o = hs_obs_sum(L, st0, d, q);
-            if (st0 == 0) {
-              v = o + du[j];
-            } else {
-              const float m = L.Mr[st0 % kHsR][q];
-              v = (m == -INFINITY) ? -INFINITY : (m + o) + du[j];
-            }
-          }
-          L.cand[q][d - 1] = v;
-          mx = fmaxf(mx, v);
+  for (int j = 0; j < kHsNJ; ++j) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) { G[j][i] = 0.f; Q[j][i] = 0.f; }
+    A0[j] = 0.f;
+    mp[j] = -INFINITY;
+  }
+  float Mlast = -INFINITY;
+
+  for (int t = 0; t < T; ++t) {
+    const float x = live ? L.lpr[t % kHsL][s] : 0.f;
+    float v[kHsNJ];
+    int dd[kHsNJ];
+    float mx = -INFINITY;
+#pragma unroll
+    for (int j = 0; j < kHsNJ; ++j) {
+      const int age = (t - (sub + kHsSub * j)) & (kHsR - 1);
+      const int d = age + 1, st = t - age;
+      dd[j] = d;
+      const bool fresh = age == 0;
+      if (fresh) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) G[j][i] = 0.f;
+        mp[j] = Mlast;
+      }
+      const int pos = age & 3;  // this element's accumulator
+      // branch-free update of the slot's accumulators
+      const float q0 = G[j][0] + x, q1 = G[j][1] + x, q2 = G[j][2] + x, q3 = G[j][3] + x;
+      Q[j][0] = pos == 0 ? q0 : Q[j][0];
+      Q[j][1] = pos == 1 ? q1 : Q[j][1];
+      Q[j][2] = pos == 2 ? q2 : Q[j][2];
+      Q[j][3] = pos == 3 ? q3 : Q[j][3];
+      A0[j] = pos == 0 ? q0 : (pos == 3 ? Q[j][0] : A0[j] + x);
+      if (pos == 3) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) G[j][i] = Q[j][i];
+      }
+      v[j] = -INFINITY;
+      if (live && d <= Dm && st >= 0) {
+        float o = 0.f + A0[j];
+        o = o + G[j][1];
+        o = o + G[j][2];
+        o = o + G[j][3];
+        const float u = L.dur[s][d - 1];
+        if (st == 0) v[j] = o + u;                                              // hsmm.py:269-274
+        else v[j] = (mp[j] == -INFINITY) ? -INFINITY : (mp[j] + o) + u;          // hsmm.py:304-314
+      }
+      mx = fmaxf(mx, v[j]);
+    }
+    mx = row_max16(mx);
+    if (live && sub == 0) {
+      L.dmx[t & 1][s] = mx;
+      a.Dg[((size_t)b * T + t) * S + s] = mx;
+    }
+    if (t == T - 1) {
+      // best over (s asc, d asc) of delta[T-1][s][d-1], strict > (hsmm.py:319-329)
+      int ld = 0x7fff;
+#pragma unroll
+      for (int j = 0; j < kHsNJ; ++j)
+        if (v[j] == mx && dd[j] < ld) ld = dd[j];
+      ld = row_min16_i(ld);
+      if (live && sub == 0) L.fd[s] = ld;
+      __syncthreads();
+      if (tid < 64) {
+        float bv = tid < S ? L.dmx[t & 1][tid] : -INFINITY;
+        int bi = tid < S ? tid : 0x7fffffff;
+        wave_argmax(bv, bi);
+        if (tid == 0) {
+          const bool any = bv != -INFINITY;
+          a.scores[b] = bv;
+          a.fin[2 * b] = any ? bi : 0;
+          a.fin[2 * b + 1] = any ? L.fd[bi] : 1;
         }
       }
-      mx = row_max16(mx);
-      if (sub == 0) L.dmx[q] = mx;
+      break;
     }
-    __syncthreads();
-    if (st == T) break;  // final candidates are in L.cand
-    // ---- C: M[st][s], first candidate attaining it (p1) and xb
-    if (q < S) {
-      const int s = q;
+    step_barrier();
+    // M[t][s] = max_{s' != s} fl(Dm[t][s'] + logT[s'][s]) and the first s' attaining it
+    {
       float lm = -INFINITY;
       int ls = 0x7fff;
 #pragma unroll
-      for (int j = 0; j < NJ; ++j) {
+      for (int j = 0; j < kHsNJ; ++j) {
         const int sp = sub + kHsSub * j;
-        if (sp < S) {
-          const float dm = L.dmx[sp];
-          const float v = (sp == s || dm == -INFINITY) ? -INFINITY : dm + L.logT[sp][s];
-          if (v > lm) { lm = v; ls = sp; }
-        }
+        const float dm = L.dmx[t & 1][sp < S ? sp : 0];
+        const float c = (lt[j] == -INFINITY || dm == -INFINITY) ? -INFINITY : dm + lt[j];
+        if (c > lm) { lm = c; ls = sp; }
       }
       const float M = row_max16(lm);
-      int s1 = row_min16_i(lm == M && M != -INFINITY ? ls : 0x7fff);
-      float xb1 = -INFINITY, xb2 = -INFINITY;
-      int d1 = 0x7fff;
-      if (M != -INFINITY) {
-#pragma unroll
-        for (int j = 0; j < NJ; ++j) {
-          const int sp = sub + kHsSub * j;
-          if (sp < s1) {
-            const float dm = L.dmx[sp];
-            const float v = (sp == s || dm == -INFINITY) ? -INFINITY : dm + L.logT[sp][s];
-            xb1 = fmaxf(xb1, v);
-          }
-        }
-        const float lt = L.logT[s1][s];
-        int ld = 0x7fff;
-        float cv[NJ];
-#pragma unroll
-        for (int j = 0; j < NJ; ++j) {
-          const int d = sub + 1 + kHsSub * j;
-          const float c = d <= Dm ? L.cand[s1][d - 1] : -INFINITY;
-          cv[j] = c == -INFINITY ? -INFINITY : c + lt;
-          if (d <= Dm && cv[j] == M && ld == 0x7fff) ld = d;
-        }
-        d1 = row_min16_i(ld);
-#pragma unroll
-        for (int j = 0; j < NJ; ++j) {
-          const int d = sub + 1 + kHsSub * j;
-          if (d < d1 && d <= Dm) xb2 = fmaxf(xb2, cv[j]);
-        }
-      } else {
-        s1 = 0;
-        d1 = 0;  // literal: psi never written (hsmm.py:313)
-      }
-      const float xb = row_max16(fmaxf(xb1, xb2));
-      if (sub == 0) {
-        L.Mr[st % kHsR][s] = M;
-        const size_t gi = ((size_t)b * T + st) * S + s;
+      const int s1 = row_min16_i((lm == M && M != -INFINITY) ? ls : 0x7fff);
+      Mlast = M;
+      if (live && sub == 0) {
+        const size_t gi = ((size_t)b * T + t) * S + s;
         a.Mg[gi] = M;
-        a.P1[gi] = (uint16_t)(s1 | (d1 << 8));
-        a.XB[gi] = xb;
+        a.S1[gi] = (uint8_t)(M == -INFINITY ? 0 : s1);
       }
     }
-    if ((st + 1) % 64 == 0) {  // chunk c = (st+1)/64 holds row st, which A(st+1) needs
-      const int c = (st + 1) >> 6;
-      chunk_store(c, rc);
-      if ((c + 1) * 64 < T) chunk_load(c + 1, rc);
-    }
-    phaseA(st + 1);
-    __syncthreads();
-  }
-  // final: best over (s asc, d asc) of delta[T-1][s][d-1], strict > (hsmm.py:319-329):
-  // the maximum with the smallest linear index s*Dm + d-1
-  {
-    float bv = -INFINITY;
-    int bi = 0x7fffffff;
-    for (int i = tid; i < S * Dm; i += kHsThreads) {
-      const float v = L.cand[i / Dm][i % Dm];
-      argmax_combine(bv, bi, v, i);
-    }
-    wave_argmax(bv, bi);
-    __shared__ float fv[kHsThreads / 64];
-    __shared__ int fi[kHsThreads / 64];
-    if ((tid & 63) == 0) { fv[tid >> 6] = bv; fi[tid >> 6] = bi; }
-    __syncthreads();
-    if (tid == 0) {
-      float best = fv[0];
-      int besti = fi[0];
-      for (int w = 1; w < kHsThreads / 64; ++w) argmax_combine(best, besti, fv[w], fi[w]);
-      a.scores[b] = best;
-      a.fin[2 * b] = besti / Dm;
-      a.fin[2 * b + 1] = besti % Dm + 1;
+    if ((t + 2) % 64 == 0) {  // rows of chunk c = (t+2)/64 are first read at step t+2
+      const int cidx = (t + 2) >> 6;
+      chunk_store(cidx);
+      if ((cidx + 1) * 64 < T) chunk_load(cidx + 1);
+      __syncthreads();
     }
   }
 }
 
-// torch-order sum of lp[t0 .. t0+d-1][s] from global memory (lane 0 only; d <= 63)
+// torch-order sum of lp[t0 .. t0+d-1][s] from global memory (d <= 63)
 __device__ float hs_obs_sum_global(const float* lp, int S, int t0, int d, int s) {
   float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
   const int m = d & ~3;
@@ -305,13 +250,13 @@ __device__ float hs_obs_sum_global(const float* lp, int S, int t0, int d, int s)
   return r;
 }
 
-// delta value of the segment (start st0, state s, duration d), as the forward defines it
-__device__ float hs_delta(const HsArgs& a, const float* lp, int b, int st0, int s, int d) {
+// delta of the segment (start st0, state s, duration d), exactly as the forward forms it
+__device__ float hs_delta(const HsArgs& a, const float* lp, const float* Mb, int st0, int s, int d) {
   if (st0 < 0) return -INFINITY;
   const float o = hs_obs_sum_global(lp, a.S, st0, d, s);
   const float u = a.dur[(size_t)s * a.Dm + d - 1];
   if (st0 == 0) return o + u;
-  const float m = a.Mg[((size_t)b * a.T + st0) * a.S + s];
+  const float m = Mb[(size_t)(st0 - 1) * a.S + s];
   return m == -INFINITY ? -INFINITY : (m + o) + u;
 }
 
@@ -319,40 +264,56 @@ __global__ void __launch_bounds__(64) hsmm_backtrace_kernel(HsArgs a) {
   const int b = blockIdx.x, l = threadIdx.x;
   const int T = a.T, S = a.S, Dm = a.Dm;
   const float* lp = a.lp + (size_t)b * T * S;
+  const float* Mb = a.Mg + (size_t)b * T * S;
+  const float* Db = a.Dg + (size_t)b * T * S;
   int t = T - 1, cs = a.fin[2 * b], cd = a.fin[2 * b + 1];
   while (t >= 0 && cd > 0) {
     int start = t - cd + 1;
     if (start < 0) start = 0;
     for (int u = start + l; u <= t; u += 64) a.states[(size_t)b * T + u] = cs;
     if (start == 0) break;
-    const size_t gi = ((size_t)b * T + start) * S + cs;
-    const float M = a.Mg[gi];
-    const uint16_t p = a.P1[gi];
-    int ns = p & 0xff, nd = p >> 8;
+    const int tau = start - 1;  // end of the previous segment
+    const size_t gi = (size_t)tau * S + cs;
+    const float M = Mb[gi];
+    int ns = 0, nd = 0;  // literal: psi never written when no predecessor exists (hsmm.py:313)
     if (M != -INFINITY) {
-      const float xb = a.XB[gi];
+      ns = a.S1[(size_t)b * T * S + gi];
+      const float lt = a.logT[(size_t)ns * S + cs];
+      // first d' of s1 whose fl(delta + logT) equals M, and the best earlier total (xb)
+      const int dlim = Dm < tau + 1 ? Dm : tau + 1;
+      float dv = -INFINITY;
+      bool hit = false;
+      if (l < dlim) {
+        dv = hs_delta(a, lp, Mb, tau - l, ns, l + 1);
+        hit = dv != -INFINITY && dv + lt == M;
+      }
+      const unsigned long long mask = __ballot(hit);
+      nd = mask ? __ffsll((long long)mask) : 1;  // lane index + 1 = d'
+      float xb = (l + 1 < nd && dv != -INFINITY) ? dv + lt : -INFINITY;
+      for (int sp = l; sp < ns; sp += 64) {
+        const float dm = Db[(size_t)tau * S + sp];
+        if (sp != cs && dm != -INFINITY) xb = fmaxf(xb, dm + a.logT[(size_t)sp * S + cs]);
+      }
+      xb = wave_max(xb);
       const float o = hs_obs_sum_global(lp, S, start, cd, cs);
       const float u = a.dur[(size_t)cs * Dm + cd - 1];
       const float F = (M + o) + u;
       if (xb != -INFINITY && (xb + o) + u == F) {
-        // rare: an earlier candidate rounds to the same total — first one wins (hsmm.py:308)
+        // rare: an earlier candidate rounds to the same total — the first one wins (hsmm.py:308)
         const int p1 = ns * Dm + (nd - 1);
         int win = p1;
         for (int base = 0; base < p1; base += 64) {
           const int k = base + l;
-          bool hit = false;
+          bool h2 = false;
           if (k < p1) {
             const int sp = k / Dm, dp = k % Dm + 1;
-            if (sp != cs) {
-              const float dv = hs_delta(a, lp, b, start - dp, sp, dp);
-              if (dv != -INFINITY) {
-                const float x = dv + a.logT[(size_t)sp * S + cs];
-                hit = ((x + o) + u) == F;
-              }
+            if (sp != cs && dp <= tau + 1) {
+              const float cv = hs_delta(a, lp, Mb, tau - dp + 1, sp, dp);
+              if (cv != -INFINITY) h2 = ((cv + a.logT[(size_t)sp * S + cs]) + o) + u == F;
             }
           }
-          const unsigned long long mask = __ballot(hit);
-          if (mask) { win = base + __ffsll((long long)mask) - 1; break; }
+          const unsigned long long m2 = __ballot(h2);
+          if (m2) { win = base + __ffsll((long long)m2) - 1; break; }
         }
         ns = win / Dm;
         nd = win % Dm + 1;
@@ -371,7 +332,7 @@ using namespace hmm355;
 HMM355_API size_t hmm355_hsmm_workspace_bytes(int B, int T, int S, int Dmax) {
   if (B < 0 || T < 1 || S < 1 || S > kHsS || Dmax < 1 || Dmax >= kHsR) return 0;
   const size_t n = (size_t)B * T * S;
-  return align_up(n * 4, 256) + align_up(n * 2, 256) + align_up(n * 4, 256) + align_up((size_t)B * 8, 256);
+  return align_up(n * 4, 256) + align_up(n, 256) + align_up(n * 4, 256) + align_up((size_t)B * 8, 256);
 }
 
 HMM355_API int hmm355_hsmm_viterbi_f32(const float* lp, const float* dur_lp, const float* log_T, int B, int T,
@@ -387,10 +348,10 @@ HMM355_API int hmm355_hsmm_viterbi_f32(const float* lp, const float* dur_lp, con
   const size_t n = (size_t)B * T * S;
   char* ws = static_cast<char*>(workspace);
   float* Mg = reinterpret_cast<float*>(ws);
-  uint16_t* P1 = reinterpret_cast<uint16_t*>(ws + align_up(n * 4, 256));
-  float* XB = reinterpret_cast<float*>(ws + align_up(n * 4, 256) + align_up(n * 2, 256));
-  int* fin = reinterpret_cast<int*>(ws + align_up(n * 4, 256) + align_up(n * 2, 256) + align_up(n * 4, 256));
-  HsArgs ha{lp, dur_lp, log_T, Mg, P1, XB, fin, scores, states, B, T, S, Dmax};
+  uint8_t* S1 = reinterpret_cast<uint8_t*>(ws + align_up(n * 4, 256));
+  float* Dg = reinterpret_cast<float*>(ws + align_up(n * 4, 256) + align_up(n, 256));
+  int* fin = reinterpret_cast<int*>(ws + align_up(n * 4, 256) + align_up(n, 256) + align_up(n * 4, 256));
+  HsArgs ha{lp, dur_lp, log_T, Mg, S1, Dg, fin, scores, states, B, T, S, Dmax};
   hipStream_t st = static_cast<hipStream_t>(stream);
   hipError_t e = allow_lds(hsmm_fwd_kernel, sizeof(HsLds));
   if (e != hipSuccess) return (int)e;

@@ -167,6 +167,21 @@ def test_hsmm_bitexact_given_lp(name):
     assert np.array_equal(scores.cpu().numpy(), g["scores"])
 
 
+@pytest.mark.parametrize("seed,T,S,Dm", [(1, 60, 6, 9), (2, 45, 4, 20), (3, 80, 9, 7), (4, 130, 12, 33)])
+def test_hsmm_ties_vs_c_oracle(seed, T, S, Dm):
+    """Coarse values (many equal totals): the first-candidate rule and the backtrace's
+    re-resolution of earlier candidates that round to the same total."""
+    rng = np.random.default_rng(seed)
+    lp = np.round(-(rng.random((2, T, S)) * 8 + 4), 1).astype(np.float32)
+    dur = np.round(np.log(rng.random((S, Dm)) + 1e-3), 1).astype(np.float32)
+    logT = np.round(np.log(rng.random((S, S)) + 1e-3), 1).astype(np.float32)
+    cs, csc = O.c_hsmm(lp, dur, logT, literal=True)
+    o = ops()
+    states, scores = o.hsmm_viterbi(t(lp), t(dur), t(logT))
+    assert np.array_equal(states.cpu().numpy(), cs)
+    assert np.array_equal(scores.cpu().numpy(), csc)
+
+
 @pytest.mark.parametrize("B,T,S,Dm", [(2, 150, 16, 12), (1, 300, 64, 40), (3, 70, 7, 63)])
 def test_hsmm_vs_c_oracle(B, T, S, Dm):
     rng = np.random.default_rng(T + S + Dm)
