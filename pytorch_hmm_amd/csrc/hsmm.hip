@@ -19,7 +19,7 @@
 //
 // hsmm_fwd_kernel: one 1024-thread workgroup per sequence, the segment END time t as the
 //   loop index (semimarkov.hip's layout): 16 lanes (one DPP row) per state; lane `sub` owns
-//   the start-time slots k = sub + 16j (mod 64) of its state.  A live segment's torch-order
+//   the start-time slots k = 4*sub + j (mod 64) of its state.  A live segment's torch-order
 //   obs_sum state (the four group accumulators, the pending group and the tail sum) and its
 //   predecessor score M stay in the slot's registers for the segment's life, so a step reads
 //   one lp row, writes delta's per-state maximum Dm for the predecessor phase, and meets at
@@ -30,6 +30,8 @@
 //   segment it recomputes, bit-identically, the candidate deltas of the winning s' to find
 //   the first d' and xb (the best total of the earlier candidates), and re-resolves the rare
 //   case where an earlier candidate rounds to the same total.
+#include <type_traits>
+
 #include "common.h"
 
 namespace hmm355 {
@@ -60,6 +62,15 @@ struct HsLds {
   float dmx[2][kHsS];
   int fd[kHsS];
 };
+
+// compile-time loop: f(integral_constant<int, J>) for J in [B, E)
+template <int J, int E, typename F>
+__device__ __forceinline__ void static_for(F&& f) {
+  if constexpr (J < E) {
+    f(std::integral_constant<int, J>{});
+    static_for<J + 1, E>(f);
+  }
+}
 
 // all-reduce over the 16 lanes of a DPP row (the lanes of one state)
 __device__ __forceinline__ float row_max16(float v) {
@@ -134,33 +145,36 @@ __global__ void __launch_bounds__(kHsThreads) hsmm_fwd_kernel(HsArgs a) {
   }
   float Mlast = -INFINITY;
 
-  for (int t = 0; t < T; ++t) {
+  // One end time.  Lane `sub` owns slots k = 4*sub + j, so the new element's position in its
+  // segment's group of four, (t - k) & 3 = (U - j) & 3 with U = t & 3, is a compile-time
+  // constant of the unrolled copy: each slot runs only its own accumulator update.
+  auto end_step = [&](const int t, auto Uc) -> bool {
+    constexpr int U = decltype(Uc)::value;
     const float x = live ? L.lpr[t % kHsL][s] : 0.f;
     float v[kHsNJ];
     int dd[kHsNJ];
     float mx = -INFINITY;
-#pragma unroll
-    for (int j = 0; j < kHsNJ; ++j) {
-      const int age = (t - (sub + kHsSub * j)) & (kHsR - 1);
+    static_for<0, kHsNJ>([&](auto Jc) {
+      constexpr int j = decltype(Jc)::value;
+      const int age = (t - (4 * sub + j)) & (kHsR - 1);
       const int d = age + 1, st = t - age;
       dd[j] = d;
-      const bool fresh = age == 0;
-      if (fresh) {
+      constexpr int pos = (U - j) & 3;  // == age & 3
+      if constexpr (pos == 0) {
+        const bool fresh = age == 0;
 #pragma unroll
-        for (int i = 0; i < 4; ++i) G[j][i] = 0.f;
-        mp[j] = Mlast;
-      }
-      const int pos = age & 3;  // this element's accumulator
-      // branch-free update of the slot's accumulators
-      const float q0 = G[j][0] + x, q1 = G[j][1] + x, q2 = G[j][2] + x, q3 = G[j][3] + x;
-      Q[j][0] = pos == 0 ? q0 : Q[j][0];
-      Q[j][1] = pos == 1 ? q1 : Q[j][1];
-      Q[j][2] = pos == 2 ? q2 : Q[j][2];
-      Q[j][3] = pos == 3 ? q3 : Q[j][3];
-      A0[j] = pos == 0 ? q0 : (pos == 3 ? Q[j][0] : A0[j] + x);
-      if (pos == 3) {
+        for (int i = 0; i < 4; ++i) G[j][i] = fresh ? 0.f : G[j][i];
+        mp[j] = fresh ? Mlast : mp[j];
+        Q[j][0] = G[j][0] + x;
+        A0[j] = Q[j][0];
+      } else if constexpr (pos == 3) {
+        Q[j][3] = G[j][3] + x;
 #pragma unroll
         for (int i = 0; i < 4; ++i) G[j][i] = Q[j][i];
+        A0[j] = G[j][0];
+      } else {
+        Q[j][pos] = G[j][pos] + x;
+        A0[j] = A0[j] + x;
       }
       v[j] = -INFINITY;
       if (live && d <= Dm && st >= 0) {
@@ -173,7 +187,7 @@ __global__ void __launch_bounds__(kHsThreads) hsmm_fwd_kernel(HsArgs a) {
         else v[j] = (mp[j] == -INFINITY) ? -INFINITY : (mp[j] + o) + u;          // hsmm.py:304-314
       }
       mx = fmaxf(mx, v[j]);
-    }
+    });
     mx = row_max16(mx);
     if (live && sub == 0) {
       L.dmx[t & 1][s] = mx;
@@ -199,7 +213,7 @@ __global__ void __launch_bounds__(kHsThreads) hsmm_fwd_kernel(HsArgs a) {
           a.fin[2 * b + 1] = any ? L.fd[bi] : 1;
         }
       }
-      break;
+      return false;
     }
     step_barrier();
     // M[t][s] = max_{s' != s} fl(Dm[t][s'] + logT[s'][s]) and the first s' attaining it
@@ -228,6 +242,17 @@ __global__ void __launch_bounds__(kHsThreads) hsmm_fwd_kernel(HsArgs a) {
       if ((cidx + 1) * 64 < T) chunk_load(cidx + 1);
       __syncthreads();
     }
+    return true;
+  };
+  using I0 = std::integral_constant<int, 0>;
+  using I1 = std::integral_constant<int, 1>;
+  using I2 = std::integral_constant<int, 2>;
+  using I3 = std::integral_constant<int, 3>;
+  for (int t = 0; t < T; t += 4) {
+    if (!end_step(t, I0{})) break;
+    if (!end_step(t + 1, I1{})) break;
+    if (!end_step(t + 2, I2{})) break;
+    if (!end_step(t + 3, I3{})) break;
   }
 }
 
@@ -260,7 +285,29 @@ __device__ float hs_delta(const HsArgs& a, const float* lp, const float* Mb, int
   return m == -INFINITY ? -INFINITY : (m + o) + u;
 }
 
+// torch-order sum of the d elements col[d-1-e], e = 0..d-1 (a segment's column in time
+// order, staged newest-first in LDS)
+__device__ __forceinline__ float hs_obs_sum_lds(const float* col, int d) {
+  float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
+  const int m = d & ~3;
+  int i = 0;
+  for (; i < m; i += 4) {
+    a0 += col[d - 1 - i];
+    a1 += col[d - 2 - i];
+    a2 += col[d - 3 - i];
+    a3 += col[d - 4 - i];
+  }
+  for (; i < d; ++i) a0 += col[d - 1 - i];
+  float r = 0.f + a0;
+  r = r + a1;
+  r = r + a2;
+  r = r + a3;
+  return r;
+}
+
 __global__ void __launch_bounds__(64) hsmm_backtrace_kernel(HsArgs a) {
+  __shared__ float pcol[kHsR];  // lp[tau - i][s1], i < Dm: the predecessor's candidate column
+  __shared__ float ccol[kHsR];  // lp[t - i][cs], i < cd: the current segment, newest first
   const int b = blockIdx.x, l = threadIdx.x;
   const int T = a.T, S = a.S, Dm = a.Dm;
   const float* lp = a.lp + (size_t)b * T * S;
@@ -279,23 +326,33 @@ __global__ void __launch_bounds__(64) hsmm_backtrace_kernel(HsArgs a) {
     if (M != -INFINITY) {
       ns = a.S1[(size_t)b * T * S + gi];
       const float lt = a.logT[(size_t)ns * S + cs];
-      // first d' of s1 whose fl(delta + logT) equals M, and the best earlier total (xb)
       const int dlim = Dm < tau + 1 ? Dm : tau + 1;
+      // one round trip: both columns, the candidates' predecessor scores, the per-state maxima
+      const bool pin = l < dlim;
+      const float pv = lp[(size_t)(pin ? tau - l : 0) * S + ns];
+      const float cv = lp[(size_t)(l < cd ? t - l : 0) * S + cs];
+      const int pst = tau - l;  // candidate d' = l + 1 starts at tau - l
+      const float pm = (pin && pst >= 1) ? Mb[(size_t)(pst - 1) * S + ns] : 0.f;
+      const float dm = l < ns ? Db[(size_t)tau * S + l] : -INFINITY;
+      const float ltl = l < ns ? a.logT[(size_t)l * S + cs] : 0.f;
+      if (pin) pcol[l] = pv;
+      if (l < cd) ccol[l] = cv;
+      __syncthreads();
+      // first d' of s1 whose fl(delta + logT) equals M, and the best earlier total (xb)
       float dv = -INFINITY;
       bool hit = false;
-      if (l < dlim) {
-        dv = hs_delta(a, lp, Mb, tau - l, ns, l + 1);
+      if (pin) {
+        const float o = hs_obs_sum_lds(pcol, l + 1);
+        const float u = a.dur[(size_t)ns * Dm + l];
+        dv = pst == 0 ? o + u : (pm == -INFINITY ? -INFINITY : (pm + o) + u);
         hit = dv != -INFINITY && dv + lt == M;
       }
       const unsigned long long mask = __ballot(hit);
       nd = mask ? __ffsll((long long)mask) : 1;  // lane index + 1 = d'
       float xb = (l + 1 < nd && dv != -INFINITY) ? dv + lt : -INFINITY;
-      for (int sp = l; sp < ns; sp += 64) {
-        const float dm = Db[(size_t)tau * S + sp];
-        if (sp != cs && dm != -INFINITY) xb = fmaxf(xb, dm + a.logT[(size_t)sp * S + cs]);
-      }
+      if (l < ns && l != cs && dm != -INFINITY) xb = fmaxf(xb, dm + ltl);
       xb = wave_max(xb);
-      const float o = hs_obs_sum_global(lp, S, start, cd, cs);
+      const float o = hs_obs_sum_lds(ccol, cd);
       const float u = a.dur[(size_t)cs * Dm + cd - 1];
       const float F = (M + o) + u;
       if (xb != -INFINITY && (xb + o) + u == F) {
@@ -308,8 +365,8 @@ __global__ void __launch_bounds__(64) hsmm_backtrace_kernel(HsArgs a) {
           if (k < p1) {
             const int sp = k / Dm, dp = k % Dm + 1;
             if (sp != cs && dp <= tau + 1) {
-              const float cv = hs_delta(a, lp, Mb, tau - dp + 1, sp, dp);
-              if (cv != -INFINITY) h2 = ((cv + a.logT[(size_t)sp * S + cs]) + o) + u == F;
+              const float c2 = hs_delta(a, lp, Mb, tau - dp + 1, sp, dp);
+              if (c2 != -INFINITY) h2 = ((c2 + a.logT[(size_t)sp * S + cs]) + o) + u == F;
             }
           }
           const unsigned long long m2 = __ballot(h2);
@@ -318,6 +375,7 @@ __global__ void __launch_bounds__(64) hsmm_backtrace_kernel(HsArgs a) {
         ns = win / Dm;
         nd = win % Dm + 1;
       }
+      __syncthreads();  // the columns are restaged for the next segment
     }
     t = start - 1;
     cs = ns;
