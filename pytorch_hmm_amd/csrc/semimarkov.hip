@@ -173,7 +173,9 @@ __global__ void __launch_bounds__(kSmThreads) smk_fwd_kernel(SmArgs a) {
   for (int j = 0; j < kSmNJ; ++j) { acc[j] = 0.f; mp[j] = -INFINITY; }
   float Mlast = -INFINITY;  // M[t-1][s] (every lane of the row holds it)
 
-  for (int t = 0; t < T; ++t) {
+  // one end time (returns false after the last); the loop below runs it four times per
+  // iteration so the compiler can schedule across consecutive end times
+  auto end_step = [&](const int t) -> bool {
     // ---- A: every segment ending at t, for this lane's start slots
     const float qt = live ? L.qr[t % kSmL][s] : 0.f;
     float v[kSmNJ];
@@ -244,7 +246,7 @@ __global__ void __launch_bounds__(kSmThreads) smk_fwd_kernel(SmArgs a) {
           if (tid == 0) a.scores[b] = (m == -INFINITY) ? -INFINITY : m + __logf(e);
         }
       }
-      break;
+      return false;
     }
     step_barrier();
     // ---- C: best (or LSE) predecessor score for segments starting at t+1
@@ -280,22 +282,18 @@ __global__ void __launch_bounds__(kSmThreads) smk_fwd_kernel(SmArgs a) {
       if ((cidx + 1) * 64 < T) chunk_load(cidx + 1);
       __syncthreads();
     }
+    return true;
+  };
+  for (int t = 0; t < T; t += 4) {
+    if (!end_step(t)) break;
+    if (!end_step(t + 1)) break;
+    if (!end_step(t + 2)) break;
+    if (!end_step(t + 3)) break;
   }
 }
 
-// delta[tau][s][d] recomputed exactly as smk_fwd_kernel forms it (d <= tau + 1)
-__device__ float smk_delta(const SmArgs& a, const float* q, const float* Mb, int tau, int s, int d) {
-  const int st = tau - d + 1;
-  float Q = q[(size_t)st * a.S + s];
-  for (int k = st + 1; k <= tau; ++k) Q = Q + q[(size_t)k * a.S + s];
-  const float o = sm_seg_obs(a.cseg ? a.cseg[s] : 0.f, Q, a.cseg != nullptr);
-  const float u = a.dur[(size_t)s * a.Dm + d - 1];
-  if (st == 0) return (a.li[s] + o) + u;
-  const float m = Mb[(size_t)(st - 1) * a.S + s];
-  return m == -INFINITY ? -INFINITY : (m + o) + u;
-}
-
 __global__ void __launch_bounds__(64) smk_backtrace_kernel(SmArgs a) {
+  __shared__ float col[kSmR];  // q[tau - i][s1], i < Dm: the predecessor's candidate column
   const int b = blockIdx.x, l = threadIdx.x;
   const int T = a.T, S = a.S, Dm = a.Dm;
   const float* q = a.q + (size_t)b * T * S;
@@ -317,18 +315,26 @@ __global__ void __launch_bounds__(64) smk_backtrace_kernel(SmArgs a) {
       ns = a.argS[(size_t)b * T * S + gi];
       const float lt = a.logT[(size_t)ns * S + cs];
       const int dlim = Dm < tau + 1 ? Dm : tau + 1;
-      nd = 0;
-      for (int base = 1; base <= dlim && nd == 0; base += 64) {
-        const int dp = base + l;
-        bool hit = false;
-        if (dp <= dlim) {
-          const float dv = smk_delta(a, q, Mb, tau, ns, dp);
-          hit = dv != -INFINITY && (dv + lt) == M;
-        }
-        const unsigned long long mask = __ballot(hit);
-        if (mask) nd = base + __ffsll((long long)mask) - 1;
+      // one round trip: the candidate column and the candidates' predecessor scores
+      const bool pin = l < dlim;
+      const int st = tau - l;  // candidate d' = l + 1 starts at tau - l
+      const float qv = q[(size_t)(pin ? st : 0) * S + ns];
+      const float pm = (pin && st >= 1) ? Mb[(size_t)(st - 1) * S + ns] : 0.f;
+      if (pin) col[l] = qv;
+      __syncthreads();
+      bool hit = false;
+      if (pin) {
+        // delta[tau][s1][d'] exactly as smk_fwd_kernel forms it: Q left to right from st
+        float Q = col[l];
+        for (int e = l - 1; e >= 0; --e) Q = Q + col[e];
+        const float o = sm_seg_obs(a.cseg ? a.cseg[ns] : 0.f, Q, a.cseg != nullptr);
+        const float u = a.dur[(size_t)ns * Dm + l];
+        const float dv = st == 0 ? (a.li[ns] + o) + u : (pm == -INFINITY ? -INFINITY : (pm + o) + u);
+        hit = dv != -INFINITY && (dv + lt) == M;
       }
-      if (nd == 0) nd = 1;  // unreachable when M is finite
+      const unsigned long long mask = __ballot(hit);
+      nd = mask ? __ffsll((long long)mask) : 1;  // lane index + 1 = d' (always found when M is finite)
+      __syncthreads();  // the column is restaged for the next segment
     }
     t = tau;
     cs = ns;
