@@ -179,7 +179,15 @@ struct RecArgs {
   const BandDesc* band;  // banded decomposition (band.h) or null: dense chain
   const float* binit;    // backward only: (B,NP) terminal vector (max-normalised) or null = ones
   const float* bscale;   // backward only: (B) log-scale of binit
+  uint8_t* psi;          // Viterbi, fused banded chain only: (B,T,NP) argmax pointers (kVitFused)
 };
+
+// The banded Viterbi chain computes the argmax pointers psi itself (helper waves on the idle
+// SIMDs, from the delta rows still in its LDS ring), so the psi pass only composes the
+// 64-step chunk maps from them.  Enabled where the helpers have the issue slots: NP >= 128.
+constexpr int kPsiChunk = 64;
+template <int NP>
+constexpr bool kVitFused = RC<NP>::NW >= 6;
 
 template <int KIND>
 __device__ __forceinline__ int rec_tau(int q, int T) {
@@ -468,7 +476,7 @@ __device__ __forceinline__ void rec_run(const RecArgs& a, float* lds, int b) {
 // runs beside the W window reads, then W fma / add+max per state.  No s_barrier inside the
 // 16-step block: LDS accesses of one wave complete in order.  Waves 1..NW-1 are helpers:
 // during block kb they stage the emissions of block kb+1 (log / +1e-8 transform included),
-// issue the global loads of block kb+2 and flush the rows and log-scales of block kb-2, so
+// issue the global loads of block kb+3 and flush the rows and log-scales of block kb-2, so
 // the chain wave issues no global memory operation and no transcendental of the staging.
 // All waves meet at one s_barrier per 16 steps.
 template <int NP, int KIND, int WP, int TD0 = 0, int TW = 0>
@@ -481,16 +489,20 @@ __device__ __forceinline__ void rec_band(const RecArgs& a, float* lds, int b, co
   constexpr int NH = 3;
   constexpr int HV = (C::NW + NH - 1) / NH;  // virtual staging waves per helper
   constexpr bool FB = KIND != kVit;
+  // fused psi (kVitFused): helpers 1..3 also form the psi rows of the block they flush
+  constexpr bool FUSE = KIND == kVit && kVitFused<NP>;
   const int tid = threadIdx.x;
   const int w = tid >> 6, l = tid & 63;
-  if (w > NH) return;
+  if (w > NH && !(FUSE && w >= 5 && w <= 7)) return;  // 5..7: psi-only waves (SIMDs 1..3)
   const int T = a.T, N = a.N;
   const int nblocks = (T + 15) / 16;
   double base = (KIND == kFbBeta && a.bscale) ? (double)a.bscale[b] : 0.0;
 
   // prologue: the helpers stage block 0 and load block 1
-  float er0[HV][4], er1[HV][4];
-  if (w > 0) {
+  // three register sets: the loads of block kb+3 are issued during block kb, so each has two
+  // blocks (~3 us) to land before it is staged
+  float er0[HV][4], er1[HV][4], er2[HV][4];
+  if (w > 0 && w <= NH) {
 #pragma unroll
     for (int h = 0; h < HV; ++h) {
       const int vw = (w - 1) + h * NH;
@@ -499,6 +511,7 @@ __device__ __forceinline__ void rec_band(const RecArgs& a, float* lds, int b, co
         rec_load<NP, KIND>(a, b, 0, vw, l, er);
         rec_stage<NP, KIND>(a, lds, 0, vw, l, er);
         if (nblocks > 1) rec_load<NP, KIND>(a, b, 1, vw, l, er1[h]);
+        if (nblocks > 2) rec_load<NP, KIND>(a, b, 2, vw, l, er2[h]);
       }
     }
   }
@@ -613,6 +626,8 @@ __device__ __forceinline__ void rec_band(const RecArgs& a, float* lds, int b, co
 #pragma unroll
         for (int j = 0; j < NB; ++j) { src[j] = y[j]; g = fmaxf(g, y[j] + fl[j]); }
         const float M = wave_max_bcast(g);
+        // fused psi: M_q = max_i fl(delta_{q-1,i} + r_i) is also psi row q's floor maximum
+        if constexpr (FUSE) lds[C::OFF_SC + 64 * ((q - 1) & (C::RING - 1)) + l] = M;
 #pragma unroll
         for (int j = 0; j < NB; ++j) acc[j] = M;
       }
@@ -671,34 +686,141 @@ __device__ __forceinline__ void rec_band(const RecArgs& a, float* lds, int b, co
     lds_barrier();
   } else {
     // ---------------------------------------------------------------- helper waves
+    // Fused psi (vit_psi_kernel's banded rule, psi_band_rows in viterbi.hip), on the
+    // psi-only waves 5..7 (SIMDs 1..3, so neither the chain nor the staging helpers lose issue
+    // slots).  With g_i = fl(delta_{t-1,i} + r_i) and M = max g (the chain's own floor term,
+    // left in LDS), i1 = first index with g_i == M is a ballot + s_ff1, and psi_t[o] is the
+    // first index attaining max(M, window values), i1 when M attains it.  The window is the
+    // chain's: Toeplitz offsets TD0.. (TW > 0) or the column windows clo_o .. clo_o + WP.
+    // Lane l owns outputs o = NB*l + j (one 16/32-bit store per row).  Rows r == w-5 (mod 3)
+    // of the block; a wave's rows are computed without branches so their latencies overlap.
+    constexpr int PWN = TW > 0 ? TW : WP;  // window slots per output
+    [[maybe_unused]] float prf[NB];
+    [[maybe_unused]] int plo[NB];
+    [[maybe_unused]] float pcl[NB][PWN];
+    if constexpr (FUSE) {
+#pragma unroll
+      for (int j = 0; j < NB; ++j) {
+        const int o = NB * l + j;
+        prf[j] = d->rfl[o];
+        plo[j] = TW > 0 ? o + TD0 : d->clo[o];
+#pragma unroll
+        for (int kk = 0; kk < PWN; ++kk) {
+          const int i = plo[j] + kk;
+          pcl[j][kk] = (i >= 0 && i < N && o < N) ? (TW > 0 ? d->tL[o][kk] : d->cL[o][kk]) : -INFINITY;
+        }
+      }
+      // resolve the table loads here, once: left pending, the waitcnt pass would re-wait for
+      // them inside the loop with a vmcnt that also drains in-flight memory operations
+#pragma unroll
+      for (int j = 0; j < NB; ++j) {
+        keep(prf[j]);
+        keep(plo[j]);
+#pragma unroll
+        for (int kk = 0; kk < PWN; ++kk) keep(pcl[j][kk]);
+      }
+    }
+    auto psi_rows = [&](int bk) {
+      if constexpr (FUSE) {
+        if (bk < 0 || w <= NH || (kAbl & 128)) return;
+        constexpr int NPW = 3, PR = (16 + NPW - 1) / NPW;
+        const int hw = w - 5;
+#pragma unroll
+        for (int m = 0; m < PR; ++m) {
+          const int r = hw + NPW * m;
+          int t = 16 * bk + (r < 16 ? r : 15);
+          t = t < T ? t : T - 1;
+          const int rho = (t - 1) & (C::RING - 1);
+          const float* drow = lds + C::OFF_RING + rho * NP;
+          // unconditional LDS reads, pinned by keep(): a read sunk under a guard ends in an
+          // s_waitcnt vmcnt(0) join
+          float yv[NB], xw[NB][PWN];
+          if constexpr (NB == 2) {
+            const float2 v2 = *reinterpret_cast<const float2*>(drow + NB * l);
+            yv[0] = v2.x; yv[1] = v2.y;
+          } else {
+            const float4 v4 = *reinterpret_cast<const float4*>(drow + NB * l);
+            yv[0] = v4.x; yv[1] = v4.y; yv[2] = v4.z; yv[3] = v4.w;
+          }
+          float M = lds[C::OFF_SC + 64 * rho + l];
+          keep(M);
+#pragma unroll
+          for (int j = 0; j < NB; ++j) {
+            keep(yv[j]);
+#pragma unroll
+            for (int kk = 0; kk < PWN; ++kk) {
+              const int i = plo[j] + kk;
+              xw[j][kk] = drow[i < 0 ? 0 : (i < NP ? i : NP - 1)];
+              keep(xw[j][kk]);
+            }
+          }
+          int i1 = 0x7fffffff;
+#pragma unroll
+          for (int j = 0; j < NB; ++j) {
+            const float g = NB * l + j < N ? yv[j] + prf[j] : -INFINITY;
+            const unsigned long long hit = __ballot(g == M);
+            const int c = NB * (__ffsll((long long)hit) - 1) + j;
+            i1 = (hit && c < i1) ? c : i1;
+          }
+          unsigned pk = 0;
+#pragma unroll
+          for (int j = 0; j < NB; ++j) {
+            float v = M, val[PWN];
+#pragma unroll
+            for (int kk = 0; kk < PWN; ++kk) {
+              const int i = plo[j] + kk;
+              val[kk] = (i >= 0 && i < N) ? xw[j][kk] + pcl[j][kk] : -INFINITY;
+              v = fmaxf(v, val[kk]);
+            }
+            int arg = M == v ? i1 : 0x7fffffff;
+#pragma unroll
+            for (int kk = 0; kk < PWN; ++kk)
+              if (val[kk] == v && plo[j] + kk < arg) arg = plo[j] + kk;
+            arg = (NB * l + j < N && t > 0) ? arg : 0;  // psi_0 = 0 (hmm.py:156 zeros)
+            pk |= (unsigned)arg << (8 * j);
+          }
+          if (r < 16 && 16 * bk + r < T) {
+            uint8_t* gdst = a.psi + ((size_t)b * T + t) * NP + NB * l;
+            if constexpr (NB == 2) *reinterpret_cast<uint16_t*>(gdst) = (uint16_t)pk;
+            else *reinterpret_cast<uint32_t*>(gdst) = pk;
+          }
+        }
+      }
+    };
     auto block_work = [&](int kb, float(&ernext)[HV][4], float(&erfree)[HV][4]) {
 #pragma unroll
       for (int h = 0; h < HV; ++h) {
         const int vw = (w - 1) + h * NH;
-        if (vw < C::NW) {
+        if (w <= NH && vw < C::NW) {
           if (!(kAbl & 64)) {
             if (kb + 1 < nblocks) rec_stage<NP, KIND>(a, lds, kb + 1, vw, l, ernext[h]);
-            if (kb + 2 < nblocks) rec_load<NP, KIND>(a, b, kb + 2, vw, l, erfree[h]);
+            if (kb + 3 < nblocks) rec_load<NP, KIND>(a, b, kb + 3, vw, l, erfree[h]);
           }
           if (!(kAbl & 32) && kb >= 2) rec_flush<NP, KIND>(a, lds, b, kb - 2, l + 64 * vw, base);
         }
       }
+      psi_rows(kb - 2);
       lds_barrier();
     };
-    for (int kb = 0; kb < nblocks; kb += 2) {
+    for (int kb = 0; kb < nblocks; kb += 3) {
       block_work(kb, er1, er0);
-      if (kb + 1 < nblocks) block_work(kb + 1, er0, er1);
+      if (kb + 1 < nblocks) block_work(kb + 1, er2, er1);
+      if (kb + 2 < nblocks) block_work(kb + 2, er0, er2);
     }
     lds_barrier();  // the chain's last row and c_{T-1}
 #pragma unroll
     for (int h = 0; h < HV; ++h) {
       const int vw = (w - 1) + h * NH;
-      if (vw < C::NW) {
+      if (w <= NH && vw < C::NW) {
         if (nblocks >= 2) rec_flush<NP, KIND>(a, lds, b, nblocks - 2, l + 64 * vw, base);
         rec_flush<NP, KIND>(a, lds, b, nblocks - 1, l + 64 * vw, base);
         if (KIND == kFbAlpha && a.loglik && vw == C::NW - 1 && l == 0)
           a.loglik[b] = (float)(base + (double)__logf(lds[C::OFF_SC + 64 * ((T - 1) & (C::RING - 1))]));
       }
+    }
+    if constexpr (FUSE) {  // the last two blocks' psi rows
+      psi_rows(nblocks - 2);
+      psi_rows(nblocks - 1);
     }
   }
 }

@@ -146,9 +146,22 @@ __device__ __forceinline__ void psi_band_rows(const VitArgs& a, uint8_t (*prow)[
 template <int NP>
 __global__ void __launch_bounds__(VF<NP>::NT) vit_psi_kernel(VitArgs a) {
   using C = VF<NP>;
+  static_assert(kPsiChunk == kChunk, "chunk length shared with the fused banded chain");
   __shared__ __attribute__((aligned(16))) uint8_t prow[kChunk][NP];
   const int chunk = blockIdx.x, b = blockIdx.y;
   const int tid = threadIdx.x;
+  if (kVitFused<NP> && a.band && a.band->wc <= kBandMax) {
+    // the banded chain's helpers wrote the psi rows (recur.h kVitFused): compose the map only
+    if (chunk == 0) return;
+    const int t_lo = chunk * kChunk;
+    const int t_hi = (t_lo + kChunk < a.T ? t_lo + kChunk : a.T) - 1;
+    const uint8_t* psrc = a.psi + ((size_t)b * a.T + t_lo) * NP;
+    for (int idx = tid; idx < (t_hi - t_lo + 1) * NP / 16; idx += C::NT)
+      *reinterpret_cast<uint4*>(&prow[0][0] + idx * 16) = *reinterpret_cast<const uint4*>(psrc + idx * 16);
+    __syncthreads();
+    compose_chunk_map<NP>(a, prow, b, chunk, t_lo, t_hi);
+    return;
+  }
   const int w = tid >> 6, l = tid & 63, r = l >> 4, c = l & 15;
   const int o = 16 * w + c;
   const int T = a.T, N = a.N;
@@ -239,7 +252,7 @@ static hipError_t launch_vit(const VitArgs& va, bool prep, hipStream_t sm) {
     if (e != hipSuccess) return e;
   }
   RecArgs ra{va.obs, va.log_P, va.init, va.delta, nullptr, nullptr, va.B, va.T, va.N, va.obs_mode, va.N, va.band,
-             nullptr, nullptr};
+             nullptr, nullptr, va.psi};
   hipLaunchKernelGGL(vit_fwd_kernel<NP>, dim3(va.B), dim3(RC<NP>::NT), kExclusiveLds, sm, ra);
   e = hipGetLastError();
   if (e != hipSuccess) return e;

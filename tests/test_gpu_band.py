@@ -84,6 +84,25 @@ def test_banded_viterbi_ties(kind):
     assert np.array_equal(states.cpu().numpy(), cs)
 
 
+@pytest.mark.parametrize("kind", ["l2r", "band5"])
+@pytest.mark.parametrize("N", [128, 97, 256])
+def test_fused_psi_block_and_chunk_edges(kind, N):
+    """NP >= 128: the banded chain forms psi and the 64-step chunk maps in its helper waves
+    (recur.h kVitFused) instead of vit_psi_kernel.  Every T around the 16-step block and
+    64-step chunk boundaries, tie-heavy emissions; states and trellis exact."""
+    rng = np.random.default_rng(N + 11)
+    P = banded_matrix(N, kind, rng)
+    P = np.round(P * 4) / 4 + (P > 0) * 0.25
+    lP, lp0 = O.hmm_params(torch.from_numpy(P.astype(np.float32)))
+    o = ops()
+    for T in (1, 2, 15, 16, 17, 33, 47, 48, 63, 64, 65, 127, 128, 129, 191, 257):
+        lo = np.log(np.round(rng.random((2, T, N)) * 2) / 2 + 0.25).astype(np.float32)
+        cs, cd, _ = O.c_viterbi(lo, lP.numpy(), lp0.numpy())
+        states, delta, _ = o.viterbi(t(lo), t(lP), t(lp0), o.OBS_LOG)
+        assert np.array_equal(delta.cpu().numpy(), cd), f"T={T}"
+        assert np.array_equal(states.cpu().numpy(), cs), f"T={T}"
+
+
 @pytest.mark.parametrize("kind", ["l2r", "left_to_right_skip", "circular", "ergodic", "band5"])
 @pytest.mark.parametrize("B,T,N", [(2, 300, 128), (3, 77, 40), (1, 50, 256)])
 def test_banded_fb_vs_fp64(kind, B, T, N):

@@ -5,7 +5,7 @@ import ctypes, os, sys, json
 HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
 sys.path.insert(0, ROOT)
-VARIANTS = [0, 1, 2, 1 | 2 | 4 | 8 | 16]
+VARIANTS = [int(v) for v in os.environ.get("ABL_VARIANTS", "0,1,2,31").split(",")]
 LIBD = os.path.join(ROOT, "gpurun_out", "..", "tools", "ablate_libs")
 
 def libpath(v):
@@ -23,7 +23,12 @@ import pytorch_hmm_amd._native as nat
 dev = torch.device("cuda", 0)
 B, T, N = int(os.environ.get("B", 32)), int(os.environ.get("T", 2000)), int(os.environ.get("N", 128))
 obs = torch.softmax(torch.randn(B, T, N, device=dev), -1)
-P = torch.rand(N, N, device=dev); lP = torch.log(P / P.sum(1, keepdim=True) + 1e-8); lp0 = torch.full((N,), -4.85, device=dev)
+if os.environ.get("MAT") == "l2r":   # the BASELINE matrix (banded chains)
+    from pytorch_hmm_amd.utils import create_left_to_right_matrix
+    P = create_left_to_right_matrix(N, 0.7).to(dev)
+else:
+    P = torch.rand(N, N, device=dev)
+lP = torch.log(P / P.sum(1, keepdim=True) + 1e-8); lp0 = torch.full((N,), -4.85, device=dev)
 libs = {}
 for v in VARIANTS:
     L = ctypes.CDLL(libpath(v))
