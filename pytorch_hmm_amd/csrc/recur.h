@@ -588,7 +588,9 @@ __device__ __forceinline__ void rec_band(const RecArgs& a, float* lds, int b, co
       return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, t1, 0x130, 0xF, 0xF, true));
     };
 
-    auto step = [&](int q, int jj, bool last_in_block) {
+    // UA: uniform floor (alpha), a compile-time branch: a runtime one splits every unrolled
+    // step into basic blocks whose joins wait for all outstanding LDS reads
+    auto step = [&](int q, int jj, bool last_in_block, auto UA) {
       float* row = lds + C::OFF_RING + ((q - 1) & (C::RING - 1)) * NP;
       st(row + NB * l, y);  // row q-1: flushed by the helpers, window source in LDS mode
       float eo[NB];
@@ -611,7 +613,7 @@ __device__ __forceinline__ void rec_band(const RecArgs& a, float* lds, int b, co
         for (int j = 0; j < NB; ++j) { src[j] = y[j]; t += y[j]; }
         cs = wave_sum_bcast(t);
         float sw;
-        if (uafl) {
+        if constexpr (decltype(UA)::value) {
           sw = afl0 * cs;
         } else {
           float tw = 0.f;
@@ -662,17 +664,25 @@ __device__ __forceinline__ void rec_band(const RecArgs& a, float* lds, int b, co
       }
     };
 
-    for (int kb = 0; kb < nblocks; ++kb) {
-      const int q0 = kb * 16 < 1 ? 1 : kb * 16;
-      const int q1 = (kb + 1) * 16 < T ? (kb + 1) * 16 : T;
-      if (q0 < q1) ld(erow(q0 - EL), en);
-      if (q0 == kb * 16 && q1 == kb * 16 + 16) {
+    auto run_blocks = [&](auto UA) {
+      for (int kb = 0; kb < nblocks; ++kb) {
+        const int q0 = kb * 16 < 1 ? 1 : kb * 16;
+        const int q1 = (kb + 1) * 16 < T ? (kb + 1) * 16 : T;
+        if (q0 < q1) ld(erow(q0 - EL), en);
+        if (q0 == kb * 16 && q1 == kb * 16 + 16) {
 #pragma unroll
-        for (int jj = 0; jj < 16; ++jj) step(kb * 16 + jj, jj, jj == 15);
-      } else {
-        for (int q = q0; q < q1; ++q) step(q, q - kb * 16, q + 1 == q1);
+          for (int jj = 0; jj < 16; ++jj) step(kb * 16 + jj, jj, jj == 15, UA);
+        } else {
+          for (int q = q0; q < q1; ++q) step(q, q - kb * 16, q + 1 == q1, UA);
+        }
+        lds_barrier();  // B_{kb+1}: block kb+1 staged by the helpers, rows of block kb-1 written
       }
-      lds_barrier();  // B_{kb+1}: block kb+1 staged by the helpers, rows of block kb-1 written
+    };
+    if constexpr (KIND == kFbAlpha) {
+      if (uafl) run_blocks(std::true_type{});
+      else run_blocks(std::false_type{});
+    } else {
+      run_blocks(std::false_type{});
     }
     float* row = lds + C::OFF_RING + ((T - 1) & (C::RING - 1)) * NP;
     st(row + NB * l, y);
