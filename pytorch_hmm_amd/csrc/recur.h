@@ -712,7 +712,7 @@ __device__ __forceinline__ void rec_band(const RecArgs& a, float* lds, int b, co
 #pragma unroll
       for (int j = 0; j < NB; ++j) {
         const int o = NB * l + j;
-        prf[j] = d->rfl[o];
+        prf[j] = o < N ? d->rfl[o] : -INFINITY;  // -inf: padded states never attain M
         plo[j] = TW > 0 ? o + TD0 : d->clo[o];
 #pragma unroll
         for (int kk = 0; kk < PWN; ++kk) {
@@ -742,8 +742,8 @@ __device__ __forceinline__ void rec_band(const RecArgs& a, float* lds, int b, co
           t = t < T ? t : T - 1;
           const int rho = (t - 1) & (C::RING - 1);
           const float* drow = lds + C::OFF_RING + rho * NP;
-          // unconditional LDS reads, pinned by keep(): a read sunk under a guard ends in an
-          // s_waitcnt vmcnt(0) join
+          // no guards around the LDS reads (out-of-range slots carry -inf in prf / pcl): a
+          // read under a guard ends in an s_waitcnt vmcnt(0) join
           float yv[NB], xw[NB][PWN];
           if constexpr (NB == 2) {
             const float2 v2 = *reinterpret_cast<const float2*>(drow + NB * l);
@@ -752,22 +752,18 @@ __device__ __forceinline__ void rec_band(const RecArgs& a, float* lds, int b, co
             const float4 v4 = *reinterpret_cast<const float4*>(drow + NB * l);
             yv[0] = v4.x; yv[1] = v4.y; yv[2] = v4.z; yv[3] = v4.w;
           }
-          float M = lds[C::OFF_SC + 64 * rho + l];
-          keep(M);
+          const float M = lds[C::OFF_SC + 64 * rho + l];
 #pragma unroll
-          for (int j = 0; j < NB; ++j) {
-            keep(yv[j]);
+          for (int j = 0; j < NB; ++j)
 #pragma unroll
             for (int kk = 0; kk < PWN; ++kk) {
               const int i = plo[j] + kk;
               xw[j][kk] = drow[i < 0 ? 0 : (i < NP ? i : NP - 1)];
-              keep(xw[j][kk]);
             }
-          }
           int i1 = 0x7fffffff;
 #pragma unroll
           for (int j = 0; j < NB; ++j) {
-            const float g = NB * l + j < N ? yv[j] + prf[j] : -INFINITY;
+            const float g = yv[j] + prf[j];
             const unsigned long long hit = __ballot(g == M);
             const int c = NB * (__ffsll((long long)hit) - 1) + j;
             i1 = (hit && c < i1) ? c : i1;
@@ -778,8 +774,7 @@ __device__ __forceinline__ void rec_band(const RecArgs& a, float* lds, int b, co
             float v = M, val[PWN];
 #pragma unroll
             for (int kk = 0; kk < PWN; ++kk) {
-              const int i = plo[j] + kk;
-              val[kk] = (i >= 0 && i < N) ? xw[j][kk] + pcl[j][kk] : -INFINITY;
+              val[kk] = xw[j][kk] + pcl[j][kk];  // -inf outside [0, N)
               v = fmaxf(v, val[kk]);
             }
             int arg = M == v ? i1 : 0x7fffffff;
