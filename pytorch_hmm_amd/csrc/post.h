@@ -2,6 +2,7 @@
 // (tv.hip) recursions: the forward-backward posterior pass and the Viterbi chunk maps +
 // backtrace.  Both consume the row layouts the recursions leave in the workspace.
 #pragma once
+#include <type_traits>
 #include "common.h"
 #include "band.h"
 
@@ -22,19 +23,41 @@ struct PostArgs {
 
 template <int NP>
 __global__ void __launch_bounds__(256) fb_posterior_kernel(PostArgs a) {
+  // One wave per row, grid-stride, the next row's loads issued before this row's math (one
+  // row in flight behind the stores).  When N == NP every lane owns K consecutive states:
+  // one 8/16-byte load per array and one 8/16-byte store per output row.
   constexpr int K = NP / 64;
+  using VecK = typename std::conditional<K == 1, float, typename std::conditional<K == 2, float2, float4>::type>::type;
   const int l = threadIdx.x & 63;
   const int wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
   const int nwaves = (gridDim.x * blockDim.x) >> 6;
   const size_t rows = (size_t)a.B * a.T;
-  for (size_t row = wave; row < rows; row += nwaves) {
-    float u[K], v[K];
+  const bool vec = a.N == NP && (reinterpret_cast<uintptr_t>(a.posterior) | reinterpret_cast<uintptr_t>(a.forward) |
+                                 reinterpret_cast<uintptr_t>(a.backward)) % sizeof(VecK) == 0;
+  // element k of this lane: state j(k) (contiguous when vec, else strided by 64)
+  auto jof = [&](int k) { return vec ? K * l + k : l + 64 * k; };
+  auto load = [&](size_t row, float (&u)[K], float (&v)[K], float& la, float& lb) {
+    if (vec) {
+      const VecK tu = reinterpret_cast<const VecK*>(a.U + row * NP)[l];
+      const VecK tv = reinterpret_cast<const VecK*>(a.V + row * NP)[l];
+      __builtin_memcpy(u, &tu, sizeof(tu));
+      __builtin_memcpy(v, &tv, sizeof(tv));
+    } else {
 #pragma unroll
-    for (int k = 0; k < K; ++k) {
-      u[k] = a.U[row * NP + l + 64 * k];
-      v[k] = a.V[row * NP + l + 64 * k];
+      for (int k = 0; k < K; ++k) {
+        u[k] = a.U[row * NP + l + 64 * k];
+        v[k] = a.V[row * NP + l + 64 * k];
+      }
     }
-    const float la = a.LA[row], lb = a.LB[row];
+    la = a.LA[row];
+    lb = a.LB[row];
+  };
+  float u[K], v[K], la = 0.f, lb = 0.f;
+  size_t row = wave;
+  if (row < rows) load(row, u, v, la, lb);
+  for (; row < rows; row += nwaves) {
+    float un[K], vn[K], lan = 0.f, lbn = 0.f;
+    if (row + nwaves < rows) load(row + nwaves, un, vn, lan, lbn);
     float mu = 0.f, mv = 0.f;
 #pragma unroll
     for (int k = 0; k < K; ++k) { mu = fmaxf(mu, u[k]); mv = fmaxf(mv, v[k]); }
@@ -47,17 +70,29 @@ __global__ void __launch_bounds__(256) fb_posterior_kernel(PostArgs a) {
     s = wave_sum_dpp(s);
     const float is = s > 0.f ? 1.f / s : 0.f;
     const bool last = (row % a.T) == (size_t)(a.T - 1);
-    float fw[K];
-#pragma unroll
-    for (int k = 0; k < K; ++k) fw[k] = __expf(__logf(u[k]) + la);
+    float fw[K], bw[K];
 #pragma unroll
     for (int k = 0; k < K; ++k) {
-      const int j = l + 64 * k;
-      if (j < a.N) {
-        const size_t off = row * a.N + j;
-        if (a.mask & HMM355_FB_POSTERIOR) a.posterior[off] = p[k] * is;
-        if (a.mask & HMM355_FB_FORWARD) a.forward[off] = fw[k];
-        if (a.mask & HMM355_FB_BACKWARD) a.backward[off] = __expf(__logf(v[k]) + lb);
+      p[k] *= is;
+      fw[k] = __expf(__logf(u[k]) + la);
+      bw[k] = __expf(__logf(v[k]) + lb);
+    }
+    if (vec) {
+      VecK t;
+      const size_t off = row * NP;
+      if (a.mask & HMM355_FB_POSTERIOR) { __builtin_memcpy(&t, p, sizeof(t)); reinterpret_cast<VecK*>(a.posterior + off)[l] = t; }
+      if (a.mask & HMM355_FB_FORWARD) { __builtin_memcpy(&t, fw, sizeof(t)); reinterpret_cast<VecK*>(a.forward + off)[l] = t; }
+      if (a.mask & HMM355_FB_BACKWARD) { __builtin_memcpy(&t, bw, sizeof(t)); reinterpret_cast<VecK*>(a.backward + off)[l] = t; }
+    } else {
+#pragma unroll
+      for (int k = 0; k < K; ++k) {
+        const int j = l + 64 * k;
+        if (j < a.N) {
+          const size_t off = row * a.N + j;
+          if (a.mask & HMM355_FB_POSTERIOR) a.posterior[off] = p[k];
+          if (a.mask & HMM355_FB_FORWARD) a.forward[off] = fw[k];
+          if (a.mask & HMM355_FB_BACKWARD) a.backward[off] = bw[k];
+        }
       }
     }
     if (last && a.lik_ref) {
@@ -65,16 +100,20 @@ __global__ void __launch_bounds__(256) fb_posterior_kernel(PostArgs a) {
       float lv[K], m = -INFINITY;
 #pragma unroll
       for (int k = 0; k < K; ++k) {
-        lv[k] = (l + 64 * k < a.N) ? __logf(fw[k] + 1e-8f) : -INFINITY;
+        lv[k] = (jof(k) < a.N) ? __logf(fw[k] + 1e-8f) : -INFINITY;
         m = fmaxf(m, lv[k]);
       }
       m = wave_max(m);
       float e = 0.f;
 #pragma unroll
-      for (int k = 0; k < K; ++k) e += (l + 64 * k < a.N) ? __expf(lv[k] - m) : 0.f;
+      for (int k = 0; k < K; ++k) e += (jof(k) < a.N) ? __expf(lv[k] - m) : 0.f;
       e = wave_sum(e);
       if (l == 0) a.lik_ref[row / a.T] = m + __logf(e);
     }
+#pragma unroll
+    for (int k = 0; k < K; ++k) { u[k] = un[k]; v[k] = vn[k]; }
+    la = lan;
+    lb = lbn;
   }
 }
 
