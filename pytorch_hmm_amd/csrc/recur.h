@@ -201,6 +201,11 @@ __device__ __forceinline__ void rec_load(const RecArgs& a, int b, int blk, int w
   const int col = 16 * w + 4 * (l & 3);
   const bool qok = q < a.T;
   const float* src = a.obs + ((size_t)b * a.T + (qok ? rec_tau<KIND>(q, a.T) : 0)) * a.N;
+  if (a.N == NP && (reinterpret_cast<uintptr_t>(a.obs) & 15) == 0) {  // full rows: one 16-B load
+    const float4 v = *reinterpret_cast<const float4*>(src + col);
+    r[0] = v.x; r[1] = v.y; r[2] = v.z; r[3] = v.w;
+    return;
+  }
 #pragma unroll
   for (int k = 0; k < 4; ++k) {
     const bool ok = qok && col + k < a.N;
@@ -214,16 +219,23 @@ __device__ __forceinline__ void rec_stage(const RecArgs& a, float* lds, int blk,
   const int sq = l >> 2;
   const int col = 16 * w + 4 * (l & 3);
   const bool qok = blk * 16 + sq < a.T;
+  // one uniform branch on the emission mode per call, selects inside: per-element branches
+  // bloat the helpers' unrolled code (three block copies x HV virtual waves) and end in
+  // waitcnt joins
   float e[4];
+  const bool lg = a.obs_mode == HMM355_OBS_LOG;
+  if (lg) {
 #pragma unroll
-  for (int k = 0; k < 4; ++k) {
-    const bool ok = qok && col + k < a.N;
-    float v;
-    if (KIND == kVit)
-      v = ok ? (a.obs_mode == HMM355_OBS_LOG ? r[k] : log_obs_cr(r[k])) : -INFINITY;
-    else
-      v = ok ? (a.obs_mode == HMM355_OBS_LOG ? __expf(r[k]) : r[k] + 1e-8f) : 0.f;
-    e[k] = v;
+    for (int k = 0; k < 4; ++k) {
+      const bool ok = qok && col + k < a.N;
+      e[k] = KIND == kVit ? (ok ? r[k] : -INFINITY) : (ok ? __expf(r[k]) : 0.f);
+    }
+  } else {
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const bool ok = qok && col + k < a.N;
+      e[k] = KIND == kVit ? (ok ? log_obs_cr(r[k]) : -INFINITY) : (ok ? r[k] + 1e-8f : 0.f);
+    }
   }
   *reinterpret_cast<float4*>(lds + C::OFF_EMIS + ((blk % 3) * 16 + sq) * NP + col) = make_float4(e[0], e[1], e[2], e[3]);
 }
@@ -237,10 +249,10 @@ __device__ __forceinline__ void rec_flush(const RecArgs& a, const float* lds, in
     constexpr int PER_ROW = NP / 4;
     const int row = tid / PER_ROW, c4 = (tid % PER_ROW) * 4;
     const int q = q_base + row;
-    if (q < a.T) {
-      const float4 v = *reinterpret_cast<const float4*>(lds + C::OFF_RING + (q & (C::RING - 1)) * NP + c4);
-      *reinterpret_cast<float4*>(a.rows + ((size_t)b * a.T + rec_tau<KIND>(q, a.T)) * NP + c4) = v;
-    }
+    // the LDS read is unconditional (only the store is guarded): a read under the guard
+    // ends in an s_waitcnt vmcnt(0) join that drains the helper's emission prefetches
+    const float4 v = *reinterpret_cast<const float4*>(lds + C::OFF_RING + (q & (C::RING - 1)) * NP + c4);
+    if (q < a.T) *reinterpret_cast<float4*>(a.rows + ((size_t)b * a.T + rec_tau<KIND>(q, a.T)) * NP + c4) = v;
   } else {
     for (int idx = tid; idx < 16 * a.N; idx += C::NT) {
       const int row = idx / a.N, col = idx - row * a.N;
@@ -254,7 +266,8 @@ __device__ __forceinline__ void rec_flush(const RecArgs& a, const float* lds, in
     // LS_rho = LS_{rho-1} + log c_{rho-1}: 16-lane inclusive scan, running base in double
     const int j = tid & 15, lane = tid & 63;
     const int rho = q_base + j;
-    float x = (lane < 16 && rho >= 1 && rho < a.T) ? __logf(lds[C::OFF_SC + 64 * ((rho - 1) & (C::RING - 1))]) : 0.f;
+    const float c = lds[C::OFF_SC + 64 * ((rho - 1) & (C::RING - 1))];  // unconditional (as above)
+    float x = (lane < 16 && rho >= 1 && rho < a.T) ? __logf(c) : 0.f;
     x += dpp_f<0x111>(x);  // row_shr:1
     x += dpp_f<0x112>(x);  // row_shr:2
     x += dpp_f<0x114>(x);  // row_shr:4
@@ -675,7 +688,7 @@ __device__ __forceinline__ void rec_band(const RecArgs& a, float* lds, int b, co
         } else {
           for (int q = q0; q < q1; ++q) step(q, q - kb * 16, q + 1 == q1, UA);
         }
-        lds_barrier();  // B_{kb+1}: block kb+1 staged by the helpers, rows of block kb-1 written
+        if (!(kAbl & 16384)) lds_barrier();  // B_{kb+1}: block kb+1 staged by the helpers, rows of block kb-1 written
       }
     };
     if constexpr (KIND == kFbAlpha) {
@@ -732,7 +745,7 @@ __device__ __forceinline__ void rec_band(const RecArgs& a, float* lds, int b, co
     }
     auto psi_rows = [&](int bk) {
       if constexpr (FUSE) {
-        if (bk < 0 || w <= NH || (kAbl & 128)) return;
+        if (bk < 0 || (kAbl & 128)) return;
         constexpr int NPW = 3, PR = (16 + NPW - 1) / NPW;
         const int hw = w - 5;
 #pragma unroll
@@ -796,7 +809,7 @@ __device__ __forceinline__ void rec_band(const RecArgs& a, float* lds, int b, co
 #pragma unroll
       for (int h = 0; h < HV; ++h) {
         const int vw = (w - 1) + h * NH;
-        if (w <= NH && vw < C::NW) {
+        if (vw < C::NW && !(kAbl & 32768)) {
           if (!(kAbl & 64)) {
             if (kb + 1 < nblocks) rec_stage<NP, KIND>(a, lds, kb + 1, vw, l, ernext[h]);
             if (kb + 3 < nblocks) rec_load<NP, KIND>(a, b, kb + 3, vw, l, erfree[h]);
@@ -804,9 +817,20 @@ __device__ __forceinline__ void rec_band(const RecArgs& a, float* lds, int b, co
           if (!(kAbl & 32) && kb >= 2) rec_flush<NP, KIND>(a, lds, b, kb - 2, l + 64 * vw, base);
         }
       }
-      psi_rows(kb - 2);
-      lds_barrier();
+      if (!(kAbl & 16384)) lds_barrier();
     };
+    if constexpr (FUSE) {
+      if (w > NH) {  // psi-only waves: one compact loop, same barrier count as the helpers
+        for (int kb = 0; kb < nblocks; ++kb) {
+          psi_rows(kb - 2);
+          if (!(kAbl & 16384)) lds_barrier();
+        }
+        lds_barrier();  // the chain's last row
+        psi_rows(nblocks - 2);
+        psi_rows(nblocks - 1);
+        return;
+      }
+    }
     for (int kb = 0; kb < nblocks; kb += 3) {
       block_work(kb, er1, er0);
       if (kb + 1 < nblocks) block_work(kb + 1, er2, er1);
@@ -816,16 +840,12 @@ __device__ __forceinline__ void rec_band(const RecArgs& a, float* lds, int b, co
 #pragma unroll
     for (int h = 0; h < HV; ++h) {
       const int vw = (w - 1) + h * NH;
-      if (w <= NH && vw < C::NW) {
+      if (vw < C::NW) {
         if (nblocks >= 2) rec_flush<NP, KIND>(a, lds, b, nblocks - 2, l + 64 * vw, base);
         rec_flush<NP, KIND>(a, lds, b, nblocks - 1, l + 64 * vw, base);
         if (KIND == kFbAlpha && a.loglik && vw == C::NW - 1 && l == 0)
           a.loglik[b] = (float)(base + (double)__logf(lds[C::OFF_SC + 64 * ((T - 1) & (C::RING - 1))]));
       }
-    }
-    if constexpr (FUSE) {  // the last two blocks' psi rows
-      psi_rows(nblocks - 2);
-      psi_rows(nblocks - 1);
     }
   }
 }
