@@ -195,13 +195,13 @@ __device__ __forceinline__ int rec_tau(int q, int T) {
 }
 
 // ---- emission staging: lane l of wave w holds 4 consecutive states of one step
-template <int NP, int KIND>
+template <int NP, int KIND, bool FULL = false>
 __device__ __forceinline__ void rec_load(const RecArgs& a, int b, int blk, int w, int l, float (&r)[4]) {
   const int q = blk * 16 + (l >> 2);
   const int col = 16 * w + 4 * (l & 3);
   const bool qok = q < a.T;
   const float* src = a.obs + ((size_t)b * a.T + (qok ? rec_tau<KIND>(q, a.T) : 0)) * a.N;
-  if (a.N == NP && (reinterpret_cast<uintptr_t>(a.obs) & 15) == 0) {  // full rows: one 16-B load
+  if constexpr (FULL) {  // full 16-B aligned rows (the caller checked): one 16-B load
     const float4 v = *reinterpret_cast<const float4*>(src + col);
     r[0] = v.x; r[1] = v.y; r[2] = v.z; r[3] = v.w;
     return;
@@ -805,14 +805,18 @@ __device__ __forceinline__ void rec_band(const RecArgs& a, float* lds, int b, co
         }
       }
     };
-    auto block_work = [&](int kb, float(&ernext)[HV][4], float(&erfree)[HV][4]) {
+    // Straight-line block work (no branch around the staging or the loads: the tail stages
+    // a block past the end as padding and re-loads the last block), so the waitcnt pass
+    // keeps exact counts and never drains the in-flight prefetches or the flush stores.
+    auto block_work = [&](int kb, float(&ernext)[HV][4], float(&erfree)[HV][4], auto FULLC) {
+      const int kload = kb + 3 < nblocks ? kb + 3 : nblocks - 1;
 #pragma unroll
       for (int h = 0; h < HV; ++h) {
         const int vw = (w - 1) + h * NH;
         if (vw < C::NW && !(kAbl & 32768)) {
           if (!(kAbl & 64)) {
-            if (kb + 1 < nblocks) rec_stage<NP, KIND>(a, lds, kb + 1, vw, l, ernext[h]);
-            if (kb + 3 < nblocks) rec_load<NP, KIND>(a, b, kb + 3, vw, l, erfree[h]);
+            rec_stage<NP, KIND>(a, lds, kb + 1, vw, l, ernext[h]);
+            rec_load<NP, KIND, decltype(FULLC)::value>(a, b, kload, vw, l, erfree[h]);
           }
           if (!(kAbl & 32) && kb >= 2) rec_flush<NP, KIND>(a, lds, b, kb - 2, l + 64 * vw, base);
         }
@@ -831,11 +835,15 @@ __device__ __forceinline__ void rec_band(const RecArgs& a, float* lds, int b, co
         return;
       }
     }
-    for (int kb = 0; kb < nblocks; kb += 3) {
-      block_work(kb, er1, er0);
-      if (kb + 1 < nblocks) block_work(kb + 1, er2, er1);
-      if (kb + 2 < nblocks) block_work(kb + 2, er0, er2);
-    }
+    auto helper_loop = [&](auto FULLC) {
+      for (int kb = 0; kb < nblocks; kb += 3) {
+        block_work(kb, er1, er0, FULLC);
+        if (kb + 1 < nblocks) block_work(kb + 1, er2, er1, FULLC);
+        if (kb + 2 < nblocks) block_work(kb + 2, er0, er2, FULLC);
+      }
+    };
+    if (a.N == NP && (reinterpret_cast<uintptr_t>(a.obs) & 15) == 0) helper_loop(std::true_type{});
+    else helper_loop(std::false_type{});
     lds_barrier();  // the chain's last row and c_{T-1}
 #pragma unroll
     for (int h = 0; h < HV; ++h) {
