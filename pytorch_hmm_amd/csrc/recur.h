@@ -345,8 +345,10 @@ __device__ __forceinline__ void rec_run(const RecArgs& a, float* lds, int b) {
 
   auto run_block = [&](int kb, float(&ernext)[4], float(&erfree)[4]) {
     if (!(kAbl & 4)) {
-      if (kb + 1 < nblocks) rec_stage<NP, KIND>(a, lds, kb + 1, w, l, ernext);
-      if (kb + 2 < nblocks) rec_load<NP, KIND>(a, b, kb + 2, w, l, erfree);
+      // straight-line staging and loads (the tail stages a padding block and re-loads the
+      // last one), as in the banded helpers: exact waitcnt counts
+      rec_stage<NP, KIND>(a, lds, kb + 1, w, l, ernext);
+      rec_load<NP, KIND>(a, b, kb + 2 < nblocks ? kb + 2 : nblocks - 1, w, l, erfree);
       if (kb >= 2) rec_flush<NP, KIND>(a, lds, b, kb - 2, tid, base);
     }
     const int q0 = kb * 16 < 1 ? 1 : kb * 16;
