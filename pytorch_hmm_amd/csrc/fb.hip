@@ -45,7 +45,7 @@ static hipError_t launch_fb(const RecArgs& fa, const RecArgs& fb, const PostArgs
   e = hipGetLastError();
   if (e != hipSuccess) return e;
   const size_t rows = (size_t)pa.B * pa.T;
-  const size_t waves = rows < 8192 ? rows : 8192;
+  const size_t waves = rows < (size_t)kPostWaves ? rows : (size_t)kPostWaves;
   const unsigned blocks = (unsigned)((waves + 3) / 4);
   hipLaunchKernelGGL(fb_posterior_kernel<NP>, dim3(blocks), dim3(256), 0, st, pa);
   return hipGetLastError();
