@@ -20,6 +20,8 @@
 //   kernel run at the max-only cost.  While the chunk's psi rows are in LDS the kernel also
 //   composes them into the chunk map G_c[j] = state at the end of chunk c-1 given state j
 //   at the end of chunk c (pointer jumping: 64 dependent LDS lookups per lane).
+//   On a banded matrix with NP >= 128 (recur.h kVitFused) the chain kernel's psi waves have
+//   already written the psi rows, and this kernel only composes the chunk maps.
 //
 // Kernel 3, vit_backtrace<NP> (one wave per (sequence, chunk)): argmax of delta_{T-1}
 //   (first index, hmm.py:174), the chain of chunk maps from the last chunk down to this one
