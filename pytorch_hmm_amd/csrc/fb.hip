@@ -27,10 +27,11 @@ template <int NP>
 __global__ void __launch_bounds__(RC<NP>::NT) fb_recur_kernel(RecArgs fa, RecArgs fb) {
   extern __shared__ __attribute__((aligned(16))) float lds[];
   const int b = blockIdx.x >> 1;
-  if (blockIdx.x & 1)
-    rec_dispatch<NP, kFbBeta>(fb, lds, b);
-  else
-    rec_dispatch<NP, kFbAlpha>(fa, lds, b);
+  if (blockIdx.x & 1) {
+    if (!(kAbl & (1 << 20))) rec_dispatch<NP, kFbBeta>(fb, lds, b);  // diagnostic: alpha only
+  } else {
+    if (!(kAbl & (1 << 21))) rec_dispatch<NP, kFbAlpha>(fa, lds, b);  // diagnostic: beta only
+  }
 }
 
 template <int NP>
