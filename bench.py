@@ -44,16 +44,34 @@ def parse():
     p.add_argument("--cpu-seconds", type=float, default=12.0, help="bounded CPU-baseline budget (0 = skip)")
     p.add_argument("--no-graph", action="store_true",
                    help="launch every step eagerly instead of replaying one captured HIP graph")
-    p.add_argument("--transition", default="left_to_right", choices=["left_to_right", "ergodic"],
-                   help="transition matrix of the workload (BASELINE: left_to_right 0.7)")
+    p.add_argument("--transition", default="left_to_right", choices=["left_to_right", "ergodic", "random"],
+                   help="transition matrix of the workload (BASELINE: left_to_right 0.7; SURVEY §8(d) also "
+                        "names create_transition_matrix(N,'ergodic'); 'random' = a dense learned-style "
+                        "matrix softmax(randn), which takes the dense chains)")
     p.add_argument("--workload", default="ns", choices=["ns", "c1", "c2", "c3", "c5", "neural", "smk", "stream"],
                    help="ns: the BASELINE metric (default).  c1/c2/c3/c5: BASELINE configs 1, 2, 3, 5 "
                         "(HMMLayer, GaussianHMMLayer, MixtureGaussianHMMLayer, HSMMLayer) through the layers")
     return p.parse_args()
 
 
+def spawn_ranks(args):
+    """`bench.py --gpus N` outside a launcher: start N ranks through torch.distributed.run as
+    child processes (this parent never touches the GPU) and exit with their status."""
+    import socket
+    import subprocess
+    with socket.socket() as s_:
+        s_.bind(("127.0.0.1", 0))
+        port = s_.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + sys.argv[1:]
+    return subprocess.run(cmd).returncode
+
+
 def setup_dist(args):
     world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world != args.gpus:
+        sys.exit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world} (launch N ranks with "
+                 "torch.distributed.run, or run `bench.py --gpus N` without a launcher to spawn them)")
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1:
@@ -86,16 +104,17 @@ def profiled_traffic(op, B, T, N, transition):
     return None, None
 
 
-def cpu_baseline(B, T, N, budget):
-    """Time the oracle (reference op sequence on torch-CPU) on the NS workload, repeated
-    until `budget` seconds of CPU work are spent (at least one FB+Viterbi pair)."""
+def cpu_baseline(B, T, N, budget, P):
+    """Time the oracle (reference op sequence on torch-CPU) on the NS workload (transition
+    matrix P), repeated until `budget` seconds of CPU work are spent (at least one FB+Viterbi
+    pair)."""
     from oracle import hmm_oracle as O
     threads = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
     threads = max(1, min(threads, os.cpu_count() or 1))
     torch.set_num_threads(threads)
     g = torch.Generator().manual_seed(1234)
     obs = torch.softmax(torch.randn(B, T, N, generator=g), dim=-1)
-    lP, lp0 = O.hmm_params(O.left_to_right_matrix(N, 0.7))
+    lP, lp0 = O.hmm_params(P.detach().cpu())
     frames, elapsed, reps = 0, 0.0, 0
     with torch.no_grad():
         while reps == 0 or (elapsed < budget and reps < 64):
@@ -379,6 +398,8 @@ def layer_cpu_baseline(wl, layer, budget):
 
 def main():
     args = parse()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(spawn_ranks(args))
     rank, world, local = setup_dist(args)
     if args.workload != "ns":
         layer_workload(args, rank, world, torch.device("cuda", local))
@@ -392,11 +413,15 @@ def main():
     B, T, N = args.batch, args.T, args.N
     if args.transition == "ergodic":
         hmm = ph.HMMPyTorch(ph.create_transition_matrix(N, "ergodic"))
+    elif args.transition == "random":
+        gp = torch.Generator().manual_seed(4321)
+        hmm = ph.HMMPyTorch(torch.softmax(torch.randn(N, N, generator=gp), dim=-1))
     else:
         hmm = ph.HMMPyTorch(ph.create_left_to_right_matrix(N, 0.7))
     g = torch.Generator(device=dev).manual_seed(1234 + rank)
     obs = torch.softmax(torch.randn(B, T, N, device=dev, generator=g), dim=-1)
     lP, lp0, plan = hmm._device_params(dev)   # what HMMPyTorch passes (log_P fixed at init)
+    chains = ops.plan_info(plan)               # the chains that actually run (band.h)
 
     s_fb = torch.cuda.Stream(dev)
     s_vit = s_fb if args.serial else torch.cuda.Stream(dev)
@@ -512,6 +537,8 @@ def main():
     value = frames_total / elapsed
     ms_per_step = elapsed / args.steps * 1e3
 
+    tdesc = {"left_to_right": "left_to_right(0.7)", "ergodic": "ergodic",
+             "random": "random dense softmax(randn(N,N))"}[args.transition]
     # roofline of the dominant op, algorithmic bytes per SURVEY.md §8(d)
     if fb_ms >= vit_ms:
         dom, dur_ms, bytes_per_launch = "forward_backward", fb_ms, 16 * N * B * T
@@ -525,10 +552,10 @@ def main():
         "metric": "frames/sec forward-backward+Viterbi, B=32 T=2000 N=128, 1/2/4/8 GPU",
         "value": value, "unit": "frames/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
         "ms_per_step": ms_per_step, "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
-        "dtype": "f32", "data": "synthetic: softmax(randn(B,T,N)) emissions, left-to-right(0.7) transitions",
+        "dtype": "f32", "data": f"synthetic: softmax(randn(B,T,N)) emissions, {tdesc} transitions",
         "config": {"workload": "HMMPyTorch forward_backward + viterbi_decode", "batch_per_gpu": B,
                    "global_batch": B * world, "seq_len": T, "num_states": N,
-                   "transition": "left_to_right(0.7)" if args.transition == "left_to_right" else "ergodic",
+                   "transition": tdesc, "chain": chains, "world_size_seen": world,
                    "parallelism": f"batch-sharded x{world}",
                    "streams": 1 if args.serial else 2, "gather": bool(args.gather and world > 1),
                    "hip_graph": graph is not None, "step_pipelining": "per-op streams, no per-step join",
@@ -540,7 +567,7 @@ def main():
                      "bytes_per_launch": bytes_per_launch, "avg_launch_ms": dur_ms},
     }
     if rank == 0 and world == 1 and args.cpu_seconds > 0:
-        out["cpu_baseline"] = cpu_baseline(B, T, N, args.cpu_seconds)
+        out["cpu_baseline"] = cpu_baseline(B, T, N, args.cpu_seconds, hmm.P)
         out["cpu_baseline"]["speedup_gpu_over_cpu"] = value / out["cpu_baseline"]["value"]
     if rank == 0:
         print(json.dumps(out), flush=True)

@@ -73,7 +73,10 @@ size_t hmm355_fb_workspace_bytes(int B, int T, int N);
  *              hmm.py:89-101 for compute_likelihood / HMMLayer.compute_loss, hmm_layer.py:144-173).
  * Workspace layout (256-B aligned pieces, in order): U (B,T,NP) scaled alpha rows | V
  * (B,T,NP) scaled beta rows | LA (B,T) | LB (B,T) | ... ; alpha_t = U_t exp(LA_t),
- * beta_t = V_t exp(LB_t), NP = N padded to 64/128/256. */
+ * beta_t = V_t exp(LB_t), NP = N padded to 64/128/256.  With obs_mode == HMM355_OBS_LOG
+ * the chains use the shifted emissions e_t = exp(obs_t - M_t), M_t = max_j obs_t[j] (a row
+ * without a finite maximum: M_t = 0), and LA / LB carry the shifts, so log-emissions far
+ * below -87 do not underflow; U and V are the rows of that shifted recursion. */
 int hmm355_forward_backward_ex_f32(const float* obs, int obs_mode, const float* log_P,
                                    const float* log_p0, const float* log_beta_T, int B, int T, int N,
                                    unsigned out_mask, float* posterior, float* forward,
@@ -134,10 +137,13 @@ int hmm355_viterbi_f32(const float* obs, int obs_mode, const float* log_P, const
  *   out (B,T,S) = LSE_c[ -0.5*(sum_d (x-mu)^2/exp(lv) + sum_d lv + D*log(2pi)) + log_w ].
  * `mix_lse` selects the reference's mixture LSE (clamped sum, :141-155); with C == 1 pass 0
  * to get the plain component log-density.  Supported: 1 <= D <= 128, 1 <= C <= 256,
- * 1 <= S*C <= 65536.  workspace >= hmm355_gmm_workspace_bytes(D,S,C) (per-component
- * precomputed scales; written by the call).
+ * 1 <= S*C <= 65536, B*T < 2^31.  workspace >= hmm355_gmm_workspace_bytes(B,T,D,S,C)
+ * (per-component scales and an fp64 copy of the frames; written by the call).  The
+ * quadratic form is accumulated in fp64 and each score rounded to fp32 once, so the scores
+ * are as close to the exact value as the reference's fp32 ones (its Viterbi paths decode
+ * identically at BASELINE config 3).
  * ------------------------------------------------------------------------------ */
-size_t hmm355_gmm_workspace_bytes(int D, int S, int C);
+size_t hmm355_gmm_workspace_bytes(int B, int T, int D, int S, int C);
 int hmm355_gmm_diag_logprob_f32(const float* x, const float* means, const float* log_vars,
                                 const float* log_w, int B, int T, int D, int S, int C,
                                 int mix_lse, float* out, void* workspace,

@@ -13,26 +13,13 @@ from . import ops
 
 __all__ = ["HMM", "HMMPyTorch", "create_left_to_right_matrix", "create_transition_matrix", "ops"]
 
-try:  # layers are optional at import time only while they are being brought up
-    from .hmm_layer import HMMLayer, GaussianHMMLayer  # noqa: F401
-    __all__ += ["HMMLayer", "GaussianHMMLayer"]
-except ImportError:  # pragma: no cover
-    pass
-try:
-    from .mixture_gaussian import MixtureGaussianHMMLayer  # noqa: F401
-    __all__ += ["MixtureGaussianHMMLayer"]
-except ImportError:  # pragma: no cover
-    pass
-try:
-    from .hsmm import HSMMLayer  # noqa: F401
-    __all__ += ["HSMMLayer"]
-except ImportError:  # pragma: no cover
-    pass
-try:
-    from .neural import NeuralHMM, ContextualNeuralHMM  # noqa: F401
-    from .semi_markov import DurationModel, SemiMarkovHMM, AdaptiveDurationHSMM  # noqa: F401
-    from .streaming import StreamingHMMProcessor, StreamingResult, AdaptiveLatencyController  # noqa: F401
-    __all__ += ["NeuralHMM", "ContextualNeuralHMM", "DurationModel", "SemiMarkovHMM", "AdaptiveDurationHSMM",
-                "StreamingHMMProcessor", "StreamingResult", "AdaptiveLatencyController"]
-except ImportError:  # pragma: no cover
-    pass
+from .hmm_layer import HMMLayer, GaussianHMMLayer
+from .mixture_gaussian import MixtureGaussianHMMLayer
+from .hsmm import HSMMLayer
+from .neural import NeuralHMM, ContextualNeuralHMM
+from .semi_markov import DurationModel, SemiMarkovHMM, AdaptiveDurationHSMM
+from .streaming import StreamingHMMProcessor, StreamingResult, AdaptiveLatencyController
+
+__all__ += ["HMMLayer", "GaussianHMMLayer", "MixtureGaussianHMMLayer", "HSMMLayer", "NeuralHMM",
+            "ContextualNeuralHMM", "DurationModel", "SemiMarkovHMM", "AdaptiveDurationHSMM",
+            "StreamingHMMProcessor", "StreamingResult", "AdaptiveLatencyController"]

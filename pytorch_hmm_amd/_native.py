@@ -60,7 +60,7 @@ def lib():
     L.hmm355_viterbi_workspace_bytes.argtypes, L.hmm355_viterbi_workspace_bytes.restype = [I, I, I], S
     L.hmm355_viterbi_f32.argtypes = [P, I, P, P, I, I, I, P, P, P, P, S, P]
     L.hmm355_viterbi_f32.restype = I
-    L.hmm355_gmm_workspace_bytes.argtypes, L.hmm355_gmm_workspace_bytes.restype = [I, I, I], S
+    L.hmm355_gmm_workspace_bytes.argtypes, L.hmm355_gmm_workspace_bytes.restype = [I, I, I, I, I], S
     L.hmm355_gmm_diag_logprob_f32.argtypes = [P, P, P, P, I, I, I, I, I, I, P, P, S, P]
     L.hmm355_gmm_diag_logprob_f32.restype = I
     L.hmm355_hsmm_workspace_bytes.argtypes, L.hmm355_hsmm_workspace_bytes.restype = [I, I, I, I], S

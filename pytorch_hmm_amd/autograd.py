@@ -100,7 +100,11 @@ class SequenceLogLik(torch.autograd.Function):
             e = obs + 1e-8
         else:
             grad_obs = grad_lo
-            e = torch.exp(obs)
+            # the kernels' shifted emissions e_t = exp(lo_t - M_t) (hmm355.h, OBS_LOG): the
+            # shift cancels in X_t (x) Y_t, and unshifted exp(lo) would underflow
+            m = obs.amax(-1, keepdim=True)
+            m = torch.where(torch.isfinite(m), m, torch.zeros_like(m))
+            e = torch.exp(obs - m)
         grad_l0 = (G[:, None] * post[:, 0]).sum(0)
         grad_lP = None
         if T > 1 and ctx.needs_input_grad[1]:
@@ -282,9 +286,9 @@ class ViterbiScore(torch.autograd.Function):
     routes it along the decoded path only — d/d lp[b,t,s_t] = g_b, d/d log_T[s_{t-1},s_t] += g_b."""
 
     @staticmethod
-    def forward(ctx, lp, log_T, init):
+    def forward(ctx, lp, log_T, init, plan=None):
         from . import ops
-        states, _, final = ops.viterbi(lp.detach(), log_T.detach(), init.detach(), ops.OBS_LOG)
+        states, _, final = ops.viterbi(lp.detach(), log_T.detach(), init.detach(), ops.OBS_LOG, plan)
         ctx.save_for_backward(states)
         ctx.shapes = (lp.shape, log_T.shape)
         ctx.mark_non_differentiable(states)
@@ -301,4 +305,4 @@ class ViterbiScore(torch.autograd.Function):
             idx = (states[:, :-1] * S + states[:, 1:]).reshape(-1)
             grad_T.index_add_(0, idx, g.view(B, 1).expand(B, T - 1).reshape(-1))
         grad_init = torch.zeros(S, device=g.device).index_add_(0, states[:, 0], g)
-        return grad_lp, grad_T.view(S, S), grad_init
+        return grad_lp, grad_T.view(S, S), grad_init, None

@@ -23,6 +23,7 @@
 // (no host round trip) and the recursion kernels branch on it; any matrix whose window
 // exceeds kBandMax takes the dense path unchanged.
 #pragma once
+#include <stddef.h>
 #include <stdlib.h>
 
 #include "common.h"
@@ -53,6 +54,9 @@ struct BandDesc {
   float tD[kBandN][4];         // exp(L[o + tcd0 + k][o]) - afl[.]  (0 outside)
   float tR[kBandN][4];         // exp(L[i][i + trd0 + k]) - afl[i]  (0 outside)
 };
+// the host reads a plan's chain choice at these offsets (pytorch_hmm_amd/ops.py plan_info)
+static_assert(offsetof(BandDesc, wc) == 0 && offsetof(BandDesc, wrp) == 12, "BandDesc header");
+static_assert(offsetof(BandDesc, tcd0) == 4 * 7172 && offsetof(BandDesc, uafl) == 4 * 7176, "BandDesc Toeplitz fields");
 
 // max over the 64 lanes, every lane receives it (DPP rows, then permlane swaps)
 __device__ __forceinline__ float wave_max_dpp(float x) {

@@ -34,6 +34,23 @@ __global__ void __launch_bounds__(RC<NP>::NT) fb_recur_kernel(RecArgs fa, RecArg
   }
 }
 
+// OBS_LOG: the row maxima M_t = max_j lo_t[j] (one wave per (b,t) row, grid-stride); the
+// chains stage e_t = exp(lo_t - M_t) and add M_t to the log-scales (recur.h rec_stage /
+// rec_flush), so log-emissions far below -87 (Gaussian log-densities at D = 80) do not
+// underflow.  A row without a finite maximum gets M = 0 (its emissions stay exp(lo)).
+__global__ void __launch_bounds__(256) row_max_kernel(const float* __restrict__ lo, int N, size_t rows,
+                                                      float* __restrict__ m) {
+  const int l = threadIdx.x & 63;
+  const size_t nw = ((size_t)gridDim.x * blockDim.x) >> 6;
+  for (size_t row = ((size_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6; row < rows; row += nw) {
+    const float* src = lo + row * N;
+    float v = -INFINITY;
+    for (int j = l; j < N; j += 64) v = fmaxf(v, src[j]);
+    v = wave_max_dpp2(v);
+    if (l == 0) m[row] = (v > -INFINITY && v < INFINITY) ? v : 0.f;
+  }
+}
+
 template <int NP>
 static hipError_t launch_fb(const RecArgs& fa, const RecArgs& fb, const PostArgs& pa, bool prep, hipStream_t st) {
   hipError_t e = allow_lds(fb_recur_kernel<NP>, kExclusiveLds);  // own the CU (recur.h)
@@ -54,8 +71,9 @@ static hipError_t launch_fb(const RecArgs& fa, const RecArgs& fb, const PostArgs
 
 // Workspace layout (documented in include/hmm355.h for adjoint callers):
 //   U (B,T,NP) | V (B,T,NP) | LA (B,T) | LB (B,T) | BandDesc | beta init (B,NP) | its scale (B)
+//   | row maxima M (B,T) (OBS_LOG)
 struct FbWs {
-  float *U, *V, *LA, *LB, *binit, *bscale;
+  float *U, *V, *LA, *LB, *binit, *bscale, *rmax;
   BandDesc* band;
 };
 static size_t fb_ws_layout(int B, int T, int N, char* base, FbWs* w) {
@@ -68,6 +86,7 @@ static size_t fb_ws_layout(int B, int T, int N, char* base, FbWs* w) {
   const size_t oD = take(sizeof(BandDesc));
   const size_t oI = take((size_t)B * NP * sizeof(float));
   const size_t oS = take((size_t)B * sizeof(float));
+  const size_t oM = take(rows * sizeof(float));
   if (w && base) {
     w->U = reinterpret_cast<float*>(base + oU);
     w->V = w->U + rows * NP;
@@ -76,6 +95,7 @@ static size_t fb_ws_layout(int B, int T, int N, char* base, FbWs* w) {
     w->band = reinterpret_cast<BandDesc*>(base + oD);
     w->binit = reinterpret_cast<float*>(base + oI);
     w->bscale = reinterpret_cast<float*>(base + oS);
+    w->rmax = reinterpret_cast<float*>(base + oM);
   }
   return off;
 }
@@ -132,8 +152,18 @@ HMM355_API int hmm355_forward_backward_plan_f32(const float* obs, int obs_mode, 
     binit = w.binit;
     bscale = w.bscale;
   }
-  RecArgs fa{obs, log_P, log_p0, w.U, w.LA, loglik, B, T, N, obs_mode, NP, band, nullptr, nullptr};
-  RecArgs fb{obs, log_P, log_p0, w.V, w.LB, nullptr, B, T, N, obs_mode, NP, band, binit, bscale};
+  const float* rmax = nullptr;
+  if (obs_mode == HMM355_OBS_LOG) {
+    const size_t rows = (size_t)B * T;
+    size_t blocks = (rows + 3) / 4;
+    blocks = blocks < 4096 ? blocks : 4096;
+    hipLaunchKernelGGL(row_max_kernel, dim3((unsigned)blocks), dim3(256), 0, st, obs, N, rows, w.rmax);
+    const hipError_t e1 = hipGetLastError();
+    if (e1 != hipSuccess) return (int)e1;
+    rmax = w.rmax;
+  }
+  RecArgs fa{obs, log_P, log_p0, w.U, w.LA, loglik, B, T, N, obs_mode, NP, band, nullptr, nullptr, nullptr, rmax};
+  RecArgs fb{obs, log_P, log_p0, w.V, w.LB, nullptr, B, T, N, obs_mode, NP, band, binit, bscale, nullptr, rmax};
   PostArgs pa{w.U, w.V, w.LA, w.LB, posterior, forward, backward, lik_ref, B, T, N, out_mask};
   hipError_t e;
   switch (NP) {

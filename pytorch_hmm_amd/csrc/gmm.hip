@@ -9,133 +9,171 @@
 //     comp = -0.5 * (sum_d ((x_d - mu_pd) * w_pd)^2 + K_p) + log_w_p,   w = exp(-lv/2)
 //     K_p  = sum_d lv_pd + D*log(2*pi)
 //     lp[s] = log(clamp(sum_c exp(comp - m), 1e-8)) + m,   m = max_c comp (inf -> 0)
-// gmm_prep (one thread per (p,d)) turns (means, log_vars, log_w) into the scales.
-// gmm_score: a workgroup owns FT frames x floor(256/C) states.  Each lane owns one
-// component: its 2*16*DCH scale/offset values live in VGPRs for the whole tile; the frame
-// row is wave-uniform and read by scalar loads, so the inner loop is two v_fma_f32 per
-// (frame, component, d) with one SGPR operand and no LDS or vector-memory traffic —
-// VALU-FMA-bound (~1.2e5 FMA per frame at S=128, C=4, D=80) as §8(d) of the survey notes.
-// Component values go through a 16-frame LDS tile for the LSE over c and leave as rows.
+//
+// Precision.  The Viterbi path the reference decodes from these scores is decided by
+// differences far below one fp32 ulp of a 2000-frame path score, so the scores must sit as
+// close to the exact value as the reference's own fp32 ones do: an fp32 sum over D = 80
+// terms here (2 fused FMAs per term) flipped 2 states of one sequence at config 3 against
+// the reference (tests/test_gpu_fullsize.py), while the exact value rounded once does not.
+// The quadratic form is therefore accumulated in fp64 — v_fma_f64 issues at the same rate
+// as v_fma_f32 on gfx950 (78.6 TF fp64 vector = non-packed fp32), so the accuracy costs no
+// throughput — and the score is rounded to fp32 once at the end.
+//
+// Layout.  gmm_prep (one thread per (p,d)) writes the scales w and offsets -mu*w in fp64,
+// d-major ([d][P]: one coalesced 8-byte load per lane).  gmm_xt converts the frames to fp64
+// in tiles [frame tile][d chunk][64 frames][8 dims], so a frame's 8-dim chunk is one
+// s_load_dwordx16 and every FMA takes its x operand from SGPRs.  gmm_score: a workgroup owns
+// 64 frames x floor(256/C) states, a lane one component.  Per 8-dim chunk the lane holds 16
+// fp64 parameters in VGPRs and updates the 64 frames' accumulators (two v_fma_f64 per (frame,
+// component, d), no LDS or vector-memory traffic in the inner loop).  The components' LSE
+// over c runs through a 16-frame LDS tile; rows leave as fp32.
 #include "common.h"
 
 namespace hmm355 {
 
 constexpr int kGmmThreads = 256;
-constexpr int kGmmFrames = 32;  // frames per workgroup
+constexpr int kGmmFrames = 64;  // frames per workgroup (accumulators per lane)
+constexpr int kGmmDc = 8;       // dims per chunk (one s_load_dwordx16 of fp64 per frame)
 constexpr int kGmmSub = 16;     // frames per LDS LSE tile
 
 __global__ void gmm_prep_kernel(const float* __restrict__ means, const float* __restrict__ log_vars,
-                                const float* __restrict__ log_w, float* __restrict__ prm, float* __restrict__ cst,
-                                int P, int D, int DP) {
+                                const float* __restrict__ log_w, double* __restrict__ pw,
+                                double* __restrict__ pmw, double* __restrict__ cst, int P, int D, int DP) {
   const int p = blockIdx.x;
   if (p >= P) return;
   for (int d = threadIdx.x; d < DP; d += blockDim.x) {
-    float w = 0.f, mw = 0.f;
+    double w = 0.0, mw = 0.0;
     if (d < D) {
-      const float lv = log_vars[(size_t)p * D + d];
-      w = expf(-0.5f * lv);
-      mw = -means[(size_t)p * D + d] * w;
+      w = exp(-0.5 * (double)log_vars[(size_t)p * D + d]);
+      mw = -(double)means[(size_t)p * D + d] * w;
     }
-    prm[((size_t)p * 2 + 0) * DP + d] = w;
-    prm[((size_t)p * 2 + 1) * DP + d] = mw;
+    pw[(size_t)d * P + p] = w;
+    pmw[(size_t)d * P + p] = mw;
   }
   if (threadIdx.x == 0) {
-    float s = 0.f;
-    for (int d = 0; d < D; ++d) s += log_vars[(size_t)p * D + d];
-    cst[2 * p + 0] = s + (float)((double)D * 1.8378770664093453);  // D*log(2*pi)
-    cst[2 * p + 1] = log_w ? log_w[p] : 0.f;
+    double s = 0.0;
+    for (int d = 0; d < D; ++d) s += (double)log_vars[(size_t)p * D + d];
+    cst[2 * p + 0] = s + (double)D * 1.8378770664093453;  // D*log(2*pi)
+    cst[2 * p + 1] = log_w ? (double)log_w[p] : 0.0;
   }
 }
 
-template <int DCH, bool FULL>
-__global__ void __launch_bounds__(kGmmThreads) gmm_score_kernel(const float* __restrict__ x,
-                                                               const float* __restrict__ prm,
-                                                               const float* __restrict__ cst,
-                                                               float* __restrict__ out, int nframes, int D,
+// x (nframes, D) fp32 -> xt [tile][chunk][64 frames][8 dims] fp64 (zeros past the ends)
+__global__ void __launch_bounds__(256) gmm_xt_kernel(const float* __restrict__ x, double* __restrict__ xt,
+                                                     int nframes, int D, int NDC, size_t total) {
+  const size_t stride = (size_t)gridDim.x * blockDim.x;
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += stride) {
+    const int k = (int)(i % kGmmDc);
+    const size_t r = i / kGmmDc;
+    const int f = (int)(r % kGmmFrames);
+    const size_t r2 = r / kGmmFrames;
+    const int dc = (int)(r2 % NDC);
+    const size_t tile = r2 / NDC;
+    const size_t frame = tile * kGmmFrames + f;
+    const int d = dc * kGmmDc + k;
+    xt[i] = (frame < (size_t)nframes && d < D) ? (double)x[frame * D + d] : 0.0;
+  }
+}
+
+__global__ void __launch_bounds__(kGmmThreads) gmm_score_kernel(const double* __restrict__ xt,
+                                                               const double* __restrict__ pw,
+                                                               const double* __restrict__ pmw,
+                                                               const double* __restrict__ cst,
+                                                               float* __restrict__ out, int nframes, int NDC,
                                                                int S, int C, int mix_lse) {
-  constexpr int DP = 16 * DCH;
-  __shared__ float tile[kGmmSub][kGmmThreads];
+  __shared__ double tile[kGmmSub][kGmmThreads];
   const int tid = threadIdx.x;
   const int spb = kGmmThreads / C;  // states per workgroup
   const int s0 = blockIdx.y * spb;
   const int sl = tid / C, c = tid - sl * C;
   const int s = s0 + sl;
   const bool active = sl < spb && s < S;
+  const int P = S * C;
   const int p = active ? s * C + c : 0;
+  const size_t ft = blockIdx.x;
 
-  float w[DP], mw[DP];
+  double q[kGmmFrames];
 #pragma unroll
-  for (int d = 0; d < DP; ++d) {
-    w[d] = prm[((size_t)p * 2 + 0) * DP + d];
-    mw[d] = prm[((size_t)p * 2 + 1) * DP + d];
-  }
-  const float kp = cst[2 * p], lw = cst[2 * p + 1];
-  const int f_begin = blockIdx.x * kGmmFrames;
-
-  for (int f0 = 0; f0 < kGmmFrames; f0 += kGmmSub) {
-    for (int fi = 0; fi < kGmmSub; ++fi) {
-      int frame = f_begin + f0 + fi;
-      frame = frame < nframes ? frame : nframes - 1;  // uniform clamp (rows past the end are not written)
-      const float* xr = x + (size_t)__builtin_amdgcn_readfirstlane(frame) * D;
-      float q0 = 0.f, q1 = 0.f;
+  for (int f = 0; f < kGmmFrames; ++f) q[f] = 0.0;
+  const double* xtile = xt + ft * (size_t)NDC * kGmmFrames * kGmmDc;
+  for (int dc = 0; dc < NDC; ++dc) {
+    double w[kGmmDc], mw[kGmmDc];
 #pragma unroll
-      for (int d = 0; d < DP; d += 2) {
-        // FULL (D == 16*DCH): plain indices -> wide s_load_dwordx16; else clamp (w = 0 there)
-        const float x0 = xr[FULL ? d : (d < D ? d : D - 1)];
-        const float x1 = xr[FULL ? d + 1 : (d + 1 < D ? d + 1 : D - 1)];
-        const float z0 = fmaf(x0, w[d], mw[d]);
-        const float z1 = fmaf(x1, w[d + 1], mw[d + 1]);
-        q0 = fmaf(z0, z0, q0);
-        q1 = fmaf(z1, z1, q1);
-      }
-      tile[fi][tid] = -0.5f * ((q0 + q1) + kp) + lw;
+    for (int k = 0; k < kGmmDc; ++k) {
+      w[k] = pw[(size_t)(dc * kGmmDc + k) * P + p];
+      mw[k] = pmw[(size_t)(dc * kGmmDc + k) * P + p];
     }
+    // wave-uniform address: the frames' chunks arrive by scalar loads (SGPR operands)
+    const double* xc = xtile + (size_t)dc * kGmmFrames * kGmmDc;
+#pragma unroll
+    for (int f = 0; f < kGmmFrames; ++f) {
+#pragma unroll
+      for (int k = 0; k < kGmmDc; ++k) {
+        const double z = fma(xc[f * kGmmDc + k], w[k], mw[k]);
+        q[f] = fma(z, z, q[f]);
+      }
+    }
+  }
+  const double kp = cst[2 * p], lw = cst[2 * p + 1];
+  const size_t f_begin = ft * kGmmFrames;
+#pragma unroll
+  for (int f0 = 0; f0 < kGmmFrames; f0 += kGmmSub) {
+#pragma unroll
+    for (int fi = 0; fi < kGmmSub; ++fi) tile[fi][tid] = -0.5 * (q[f0 + fi] + kp) + lw;
     __syncthreads();
     for (int pair = tid; pair < kGmmSub * spb; pair += kGmmThreads) {
       const int fi = pair / spb, sj = pair - fi * spb;
-      const int frame = f_begin + f0 + fi;
+      const size_t frame = f_begin + f0 + fi;
       const int ss = s0 + sj;
-      if (frame < nframes && ss < S) {
-        float r;
+      if (frame < (size_t)nframes && ss < S) {
+        double r;
         if (!mix_lse) {
           r = tile[fi][sj * C];
         } else {
-          float m = -INFINITY;
-          for (int cc = 0; cc < C; ++cc) m = fmaxf(m, tile[fi][sj * C + cc]);
-          if (isinf(m)) m = 0.f;  // mixture_gaussian.py:144
-          float e = 0.f;
-          for (int cc = 0; cc < C; ++cc) e += expf(tile[fi][sj * C + cc] - m);
-          r = logf(fmaxf(e, 1e-8f)) + m;  // :149-153
+          double m = -INFINITY;
+          for (int cc = 0; cc < C; ++cc) m = fmax(m, tile[fi][sj * C + cc]);
+          if (isinf(m)) m = 0.0;  // mixture_gaussian.py:144
+          float e = 0.f;          // terms <= 1: fp32 sum and log add ~1e-7 absolute to |lp| ~ 1e2
+          for (int cc = 0; cc < C; ++cc) e += expf((float)(tile[fi][sj * C + cc] - m));
+          r = (double)logf(fmaxf(e, 1e-8f)) + m;  // :149-153
         }
-        out[(size_t)frame * S + ss] = r;
+        out[frame * S + ss] = (float)r;
       }
     }
     __syncthreads();
   }
 }
 
-template <int DCH>
-static hipError_t launch_gmm(const float* x, const float* prm, const float* cst, float* out, int nframes, int D,
-                             int S, int C, int mix_lse, hipStream_t st) {
-  const int spb = kGmmThreads / C;
-  dim3 grid((nframes + kGmmFrames - 1) / kGmmFrames, (S + spb - 1) / spb);
-  if (D == 16 * DCH)
-    hipLaunchKernelGGL((gmm_score_kernel<DCH, true>), grid, dim3(kGmmThreads), 0, st, x, prm, cst, out, nframes, D,
-                       S, C, mix_lse);
-  else
-    hipLaunchKernelGGL((gmm_score_kernel<DCH, false>), grid, dim3(kGmmThreads), 0, st, x, prm, cst, out, nframes, D,
-                       S, C, mix_lse);
-  return hipGetLastError();
+struct GmmWs {
+  double *pw, *pmw, *cst, *xt;
+};
+static size_t gmm_ws_layout(int B, int T, int D, int S, int C, char* base, GmmWs* w) {
+  const size_t P = (size_t)S * C;
+  const size_t NDC = (D + kGmmDc - 1) / kGmmDc, DP = NDC * kGmmDc;
+  const size_t nframes = (size_t)B * T;
+  const size_t ntiles = (nframes + kGmmFrames - 1) / kGmmFrames;
+  size_t off = 0;
+  auto take = [&](size_t bytes) { const size_t o = off; off += align_up(bytes, 256); return o; };
+  const size_t ow = take(P * DP * sizeof(double));
+  const size_t om = take(P * DP * sizeof(double));
+  const size_t oc = take(P * 2 * sizeof(double));
+  const size_t ox = take(ntiles * NDC * kGmmFrames * kGmmDc * sizeof(double));
+  if (w && base) {
+    w->pw = reinterpret_cast<double*>(base + ow);
+    w->pmw = reinterpret_cast<double*>(base + om);
+    w->cst = reinterpret_cast<double*>(base + oc);
+    w->xt = reinterpret_cast<double*>(base + ox);
+  }
+  return off;
 }
 
 }  // namespace hmm355
 
 using namespace hmm355;
 
-HMM355_API size_t hmm355_gmm_workspace_bytes(int D, int S, int C) {
-  if (D < 1 || D > 128 || S < 1 || C < 1 || C > 256) return 0;
-  const size_t P = (size_t)S * C, DP = (size_t)((D + 15) / 16) * 16;
-  return align_up(P * 2 * DP * sizeof(float), 256) + align_up(P * 2 * sizeof(float), 256);
+HMM355_API size_t hmm355_gmm_workspace_bytes(int B, int T, int D, int S, int C) {
+  if (B < 0 || T < 0 || D < 1 || D > 128 || S < 1 || C < 1 || C > 256) return 0;
+  return gmm_ws_layout(B, T, D, S, C, nullptr, nullptr);
 }
 
 HMM355_API int hmm355_gmm_diag_logprob_f32(const float* x, const float* means, const float* log_vars,
@@ -144,27 +182,31 @@ HMM355_API int hmm355_gmm_diag_logprob_f32(const float* x, const float* means, c
   if (B < 0 || T < 0 || D < 1 || S < 1 || C < 1) return HMM355_E_ARG;
   if (D > 128 || C > 256 || (size_t)S * C > 65536) return HMM355_E_SHAPE;
   if ((size_t)B * T == 0) return HMM355_OK;
+  if ((size_t)B * T > ((size_t)1 << 31) - kGmmFrames) return HMM355_E_SHAPE;
   if (!x || !means || !log_vars || !out || !workspace) return HMM355_E_ARG;
   if (!mix_lse && C != 1) return HMM355_E_ARG;
-  if (workspace_bytes < hmm355_gmm_workspace_bytes(D, S, C)) return HMM355_E_WORKSPACE;
-  const int DCH = (D + 15) / 16, DP = DCH * 16;
+  if (workspace_bytes < hmm355_gmm_workspace_bytes(B, T, D, S, C)) return HMM355_E_WORKSPACE;
+  GmmWs w;
+  gmm_ws_layout(B, T, D, S, C, static_cast<char*>(workspace), &w);
+  const int NDC = (D + kGmmDc - 1) / kGmmDc, DP = NDC * kGmmDc;
   const int P = S * C;
-  float* prm = static_cast<float*>(workspace);
-  float* cst = reinterpret_cast<float*>(static_cast<char*>(workspace) + align_up((size_t)P * 2 * DP * sizeof(float), 256));
+  const int nframes = B * T;
+  const size_t ntiles = ((size_t)nframes + kGmmFrames - 1) / kGmmFrames;
   hipStream_t st = static_cast<hipStream_t>(stream);
-  hipLaunchKernelGGL(gmm_prep_kernel, dim3(P), dim3(64), 0, st, means, log_vars, log_w, prm, cst, P, D, DP);
+  hipLaunchKernelGGL(gmm_prep_kernel, dim3(P), dim3(64), 0, st, means, log_vars, log_w, w.pw, w.pmw, w.cst, P, D,
+                     DP);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return (int)e;
-  const int nframes = B * T;
-  switch (DCH) {
-    case 1: e = launch_gmm<1>(x, prm, cst, out, nframes, D, S, C, mix_lse, st); break;
-    case 2: e = launch_gmm<2>(x, prm, cst, out, nframes, D, S, C, mix_lse, st); break;
-    case 3: e = launch_gmm<3>(x, prm, cst, out, nframes, D, S, C, mix_lse, st); break;
-    case 4: e = launch_gmm<4>(x, prm, cst, out, nframes, D, S, C, mix_lse, st); break;
-    case 5: e = launch_gmm<5>(x, prm, cst, out, nframes, D, S, C, mix_lse, st); break;
-    case 6: e = launch_gmm<6>(x, prm, cst, out, nframes, D, S, C, mix_lse, st); break;
-    case 7: e = launch_gmm<7>(x, prm, cst, out, nframes, D, S, C, mix_lse, st); break;
-    default: e = launch_gmm<8>(x, prm, cst, out, nframes, D, S, C, mix_lse, st); break;
-  }
+  const size_t total = ntiles * NDC * kGmmFrames * kGmmDc;
+  size_t blocks = (total + 255) / 256;
+  blocks = blocks < 8192 ? blocks : 8192;
+  hipLaunchKernelGGL(gmm_xt_kernel, dim3((unsigned)blocks), dim3(256), 0, st, x, w.xt, nframes, D, NDC, total);
+  e = hipGetLastError();
+  if (e != hipSuccess) return (int)e;
+  const int spb = kGmmThreads / C;
+  dim3 grid((unsigned)ntiles, (S + spb - 1) / spb);
+  hipLaunchKernelGGL(gmm_score_kernel, grid, dim3(kGmmThreads), 0, st, w.xt, w.pw, w.pmw, w.cst, out, nframes, NDC,
+                     S, C, mix_lse);
+  e = hipGetLastError();
   return e == hipSuccess ? HMM355_OK : (int)e;
 }

@@ -49,7 +49,9 @@ struct RC {
   static constexpr int OFF_RING = OFF_EMIS + 3 * 16 * NP;  // [RING][NP]
   static constexpr int OFF_SC = OFF_RING + RING * NP;      // [RING][64] normalisers c_rho (entry 0;
                                                            // the banded chain writes all 64 lanes)
-  static constexpr int LDS_FLOATS = OFF_SC + RING * 64;
+  static constexpr int OFF_M = OFF_SC + RING * 64;        // [128] OBS_LOG FB: staged row maxima (0 else)
+  static constexpr int MRING = 128;                        // rows kb-3 .. kb+1 live at once
+  static constexpr int LDS_FLOATS = OFF_M + MRING;
   static_assert(LDS_FLOATS * 4 <= kExclusiveLds, "LDS layout too large");
 };
 
@@ -180,6 +182,7 @@ struct RecArgs {
   const float* binit;    // backward only: (B,NP) terminal vector (max-normalised) or null = ones
   const float* bscale;   // backward only: (B) log-scale of binit
   uint8_t* psi;          // Viterbi, fused banded chain only: (B,T,NP) argmax pointers (kVitFused)
+  const float* rmax;     // FB with OBS_LOG: (B,T) row maxima M_t (e_t = exp(lo_t - M_t)), else null
 };
 
 // The banded Viterbi chain computes the argmax pointers psi itself (helper waves on the idle
@@ -195,12 +198,21 @@ __device__ __forceinline__ int rec_tau(int q, int T) {
 }
 
 // ---- emission staging: lane l of wave w holds 4 consecutive states of one step
+// r[0..3]: the emissions; r[4]: the step's row maximum M_t (FB with OBS_LOG; the load reads an
+// address of the same row otherwise, so the staging stays branch-free, and is not used)
 template <int NP, int KIND, bool FULL = false>
-__device__ __forceinline__ void rec_load(const RecArgs& a, int b, int blk, int w, int l, float (&r)[4]) {
+__device__ __forceinline__ void rec_load(const RecArgs& a, int b, int blk, int w, int l, float (&r)[5]) {
   const int q = blk * 16 + (l >> 2);
   const int col = 16 * w + 4 * (l & 3);
   const bool qok = q < a.T;
-  const float* src = a.obs + ((size_t)b * a.T + (qok ? rec_tau<KIND>(q, a.T) : 0)) * a.N;
+  const size_t bt = (size_t)b * a.T + (qok ? rec_tau<KIND>(q, a.T) : 0);
+  const float* src = a.obs + bt * a.N;
+  if constexpr (KIND != kVit) {
+    const float* mp = a.rmax ? a.rmax + bt : src;  // a pointer select, not a branch
+    r[4] = *mp;
+  } else {
+    r[4] = 0.f;
+  }
   if constexpr (FULL) {  // full 16-B aligned rows (the caller checked): one 16-B load
     const float4 v = *reinterpret_cast<const float4*>(src + col);
     r[0] = v.x; r[1] = v.y; r[2] = v.z; r[3] = v.w;
@@ -214,7 +226,7 @@ __device__ __forceinline__ void rec_load(const RecArgs& a, int b, int blk, int w
 }
 
 template <int NP, int KIND>
-__device__ __forceinline__ void rec_stage(const RecArgs& a, float* lds, int blk, int w, int l, const float (&r)[4]) {
+__device__ __forceinline__ void rec_stage(const RecArgs& a, float* lds, int blk, int w, int l, const float (&r)[5]) {
   using C = RC<NP>;
   const int sq = l >> 2;
   const int col = 16 * w + 4 * (l & 3);
@@ -225,10 +237,14 @@ __device__ __forceinline__ void rec_stage(const RecArgs& a, float* lds, int blk,
   float e[4];
   const bool lg = a.obs_mode == HMM355_OBS_LOG;
   if (lg) {
+    // FB: e = exp(lo - M_t) with the row maximum M_t (log-emissions of -100 .. -400 would
+    // underflow exp); M_t is carried into the log-scales by rec_flush
+    const float m = KIND == kVit ? 0.f : (a.rmax ? r[4] : 0.f);
+    if (KIND != kVit && w == 0 && (l & 3) == 0) lds[C::OFF_M + ((blk * 16 + sq) & (C::MRING - 1))] = m;
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
       const bool ok = qok && col + k < a.N;
-      e[k] = KIND == kVit ? (ok ? r[k] : -INFINITY) : (ok ? __expf(r[k]) : 0.f);
+      e[k] = KIND == kVit ? (ok ? r[k] : -INFINITY) : (ok ? __expf(r[k] - m) : 0.f);
     }
   } else {
 #pragma unroll
@@ -268,6 +284,13 @@ __device__ __forceinline__ void rec_flush(const RecArgs& a, const float* lds, in
     const int rho = q_base + j;
     const float c = lds[C::OFF_SC + 64 * ((rho - 1) & (C::RING - 1))];  // unconditional (as above)
     float x = (lane < 16 && rho >= 1 && rho < a.T) ? __logf(c) : 0.f;
+    if (a.obs_mode == HMM355_OBS_LOG) {
+      // shifted emissions: alpha row rho used M_{tau(rho)}, beta row rho used M_{tau(rho)+1}
+      // (the row staged as rho - 1); beta row 0 (the terminal vector) none
+      const int src = KIND == kFbBeta ? rho - 1 : rho;
+      const float m = lds[C::OFF_M + (src & (C::MRING - 1))];
+      x += (lane < 16 && src >= 0 && rho < a.T) ? m : 0.f;
+    }
     x += dpp_f<0x111>(x);  // row_shr:1
     x += dpp_f<0x112>(x);  // row_shr:2
     x += dpp_f<0x114>(x);  // row_shr:4
@@ -300,7 +323,7 @@ __device__ __forceinline__ void rec_run(const RecArgs& a, float* lds, int b) {
     }
 
   const int nblocks = (T + 15) / 16;
-  float er0[4], er1[4];
+  float er0[5], er1[5];
   rec_load<NP, KIND>(a, b, 0, w, l, er0);
   rec_stage<NP, KIND>(a, lds, 0, w, l, er0);
   if (nblocks > 1) rec_load<NP, KIND>(a, b, 1, w, l, er1);
@@ -343,7 +366,7 @@ __device__ __forceinline__ void rec_run(const RecArgs& a, float* lds, int b) {
     }
   };
 
-  auto run_block = [&](int kb, float(&ernext)[4], float(&erfree)[4]) {
+  auto run_block = [&](int kb, float(&ernext)[5], float(&erfree)[5]) {
     if (!(kAbl & 4)) {
       // straight-line staging and loads (the tail stages a padding block and re-loads the
       // last one), as in the banded helpers: exact waitcnt counts
@@ -516,13 +539,13 @@ __device__ __forceinline__ void rec_band(const RecArgs& a, float* lds, int b, co
   // prologue: the helpers stage block 0 and load block 1
   // three register sets: the loads of block kb+3 are issued during block kb, so each has two
   // blocks (~3 us) to land before it is staged
-  float er0[HV][4], er1[HV][4], er2[HV][4];
+  float er0[HV][5], er1[HV][5], er2[HV][5];
   if (w > 0 && w <= NH) {
 #pragma unroll
     for (int h = 0; h < HV; ++h) {
       const int vw = (w - 1) + h * NH;
       if (vw < C::NW) {
-        float er[4];
+        float er[5];
         rec_load<NP, KIND>(a, b, 0, vw, l, er);
         rec_stage<NP, KIND>(a, lds, 0, vw, l, er);
         if (nblocks > 1) rec_load<NP, KIND>(a, b, 1, vw, l, er1[h]);
@@ -810,7 +833,7 @@ __device__ __forceinline__ void rec_band(const RecArgs& a, float* lds, int b, co
     // Straight-line block work (no branch around the staging or the loads: the tail stages
     // a block past the end as padding and re-loads the last block), so the waitcnt pass
     // keeps exact counts and never drains the in-flight prefetches or the flush stores.
-    auto block_work = [&](int kb, float(&ernext)[HV][4], float(&erfree)[HV][4], auto FULLC) {
+    auto block_work = [&](int kb, float(&ernext)[HV][5], float(&erfree)[HV][5], auto FULLC) {
       const int kload = kb + 3 < nblocks ? kb + 3 : nblocks - 1;
 #pragma unroll
       for (int h = 0; h < HV; ++h) {

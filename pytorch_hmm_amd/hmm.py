@@ -49,25 +49,24 @@ class HMMPyTorch(HMM):
     """Forward-backward, Viterbi and likelihood on MI355X (reference hmm.py:58-254)."""
 
     # -- helpers -------------------------------------------------------------------
-    def _params_for(self, obs: torch.Tensor):
-        """(log_P, log_p0) on the observations' device.  Device copies and the transition
-        plan (ops.make_plan: the banded structure of log_P, measured once) are cached while
-        log_P / log_p0 are unchanged (same storage and version)."""
-        return self._device_params(obs.device)[:2]
-
     def _device_params(self, dev):
+        """(log_P, log_p0, plan) on device `dev`.  Device copies and the transition plan
+        (ops.make_plan: the banded structure of log_P, measured once) are cached while log_P /
+        log_p0 are unchanged."""
         lp, l0 = self.log_P, self.log_p0
-        key = (str(dev), lp.data_ptr(), lp._version, l0.data_ptr(), l0._version)
+        # The entry holds the source tensors themselves: a hit needs the SAME objects at the
+        # same version (a freed host buffer's address can be reused by a new tensor).
         cache = self.__dict__.setdefault("_dev_cache", {})
         hit = cache.get(str(dev))
-        if hit is None or hit[0] != key or lp.requires_grad or l0.requires_grad:
+        if (hit is None or hit[0] is not lp or hit[1] is not l0 or hit[2] != (lp._version, l0._version)
+                or lp.requires_grad or l0.requires_grad):
             lpd = lp if lp.device == dev else lp.to(dev)
             l0d = l0 if l0.device == dev else l0.to(dev)
             plan = ops.make_plan(lpd.detach()) if dev.type == "cuda" else None
-            hit = (key, lpd, l0d, plan)
+            hit = (lp, l0, (lp._version, l0._version), lpd, l0d, plan)
             if not (lp.requires_grad or l0.requires_grad):
                 cache[str(dev)] = hit
-        return hit[1], hit[2], hit[3]
+        return hit[3], hit[4], hit[5]
 
     @staticmethod
     def _as_batch(observations):
@@ -95,9 +94,9 @@ class HMMPyTorch(HMM):
         """Posterior only (what HMMLayer needs); skips the forward/backward outputs."""
         obs, _ = self._as_batch(observations)
         assert obs.shape[-1] == self.K, f"Observation dim {obs.shape[-1]} must match model states {self.K}"
-        log_P, log_p0 = self._params_for(obs)
+        log_P, log_p0, plan = self._device_params(obs.device)
         post = ops.forward_backward(obs.detach(), log_P.detach(), log_p0.detach(), ops.OBS_PROB,
-                                    ops.FB_POSTERIOR)[0]
+                                    ops.FB_POSTERIOR, plan)[0]
         if needs_grad(obs, log_P, log_p0):
             (post,) = forward_backward_with_grad(obs, log_P, log_p0, (post,))
         return post
@@ -119,11 +118,11 @@ class HMMPyTorch(HMM):
         obs, squeeze = self._as_batch(observations)
         B, T, K = obs.shape
         assert K == self.K, f"Observation dim {K} must match model states {self.K}"
-        log_P, log_p0 = self._params_for(obs)
+        log_P, log_p0, plan = self._device_params(obs.device)
         if needs_grad(obs, log_P, log_p0):
             ll = SequenceLogLik.apply(obs, log_P, log_p0, ops.OBS_PROB, "ref")
         else:
-            ll = ops.forward_backward(obs, log_P, log_p0, ops.OBS_PROB, 0)[4]
+            ll = ops.forward_backward(obs, log_P, log_p0, ops.OBS_PROB, 0, plan)[4]
         return ll.squeeze(0) if squeeze else ll
 
     def log_likelihood(self, observations: torch.Tensor) -> torch.Tensor:
@@ -131,11 +130,11 @@ class HMMPyTorch(HMM):
         (what compute_likelihood would return without exp() underflow)."""
         obs, squeeze = self._as_batch(observations)
         assert obs.shape[-1] == self.K, f"Observation dim {obs.shape[-1]} must match model states {self.K}"
-        log_P, log_p0 = self._params_for(obs)
+        log_P, log_p0, plan = self._device_params(obs.device)
         if needs_grad(obs, log_P, log_p0):
             ll = SequenceLogLik.apply(obs, log_P, log_p0, ops.OBS_PROB, "exact")
         else:
-            ll = ops.forward_backward(obs, log_P, log_p0, ops.OBS_PROB, 0)[3]
+            ll = ops.forward_backward(obs, log_P, log_p0, ops.OBS_PROB, 0, plan)[3]
         return ll.squeeze(0) if squeeze else ll
 
     def sample(self, seq_length: int, batch_size: int = 1) -> Tuple[torch.Tensor, torch.Tensor]:

@@ -52,18 +52,38 @@ class HMMLayer(nn.Module):
     def _get_initial_probabilities(self) -> torch.Tensor:
         return F.softmax(self.log_initial_logits, dim=0)
 
+    def _param_key(self):
+        """Identity + version of the tensors P and p0 derive from (and whether autograd is
+        recording through them)."""
+        src = self.log_transition_logits if self.log_transition_logits is not None else self.transition_matrix
+        init = self.log_initial_logits
+        grad = torch.is_grad_enabled() and (src.requires_grad or init.requires_grad)
+        return (src, src._version, src.device, init, init._version, grad)
+
     def _get_hmm(self) -> HMMPyTorch:
+        if self._hmm is not None:
+            # later calls assign log(P + 1e-8) (hmm_layer.py:83-86).  With the parameters
+            # unchanged since the previous later call and no autograd, the assigned tensors
+            # would be bit-identical: keep them, so HMMPyTorch's device copies and transition
+            # plan stay cached (no per-call softmax/log/plan launches).
+            key = self._param_key()
+            old = self.__dict__.get("_hmm_key")
+            if (old is not None and not key[5] and old[0] is key[0] and old[3] is key[3]
+                    and old[1:3] == key[1:3] and old[4:] == key[4:]):
+                return self._hmm
         P = self._get_transition_matrix()
         p0 = self._get_initial_probabilities()
         device = P.device
         if self._hmm is None:
             self._hmm = HMMPyTorch(P, p0, device=str(device))
+            self.__dict__["_hmm_key"] = None   # call 2 must re-derive (first-call quirk)
         else:
             self._hmm.P = P
             self._hmm.log_P = torch.log(P + 1e-8)
             self._hmm.p0 = p0
             self._hmm.log_p0 = torch.log(p0 + 1e-8)
             self._hmm.device = str(device)
+            self.__dict__["_hmm_key"] = self._param_key()
         return self._hmm
 
     # -- forward (hmm_layer.py:91-142) -------------------------------------------------

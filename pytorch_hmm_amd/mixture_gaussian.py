@@ -105,16 +105,30 @@ class MixtureGaussianHMMLayer(nn.Module):
             log_w = self._safe_log(F.softmax(self.mixture_weights_logits, dim=-1))
             return ops.gmm_diag_logprob(observations, self.means, self._component_log_vars(), log_w, 1)
 
+    def _transition_plan(self, log_transitions: torch.Tensor):
+        """The banded-structure plan of log T (ops.make_plan), cached while the transition
+        parameter is unchanged (same tensor, same version, same device): a fixed or learned
+        matrix is measured once, not on every forward."""
+        src = self.transition_logits if self.learnable_transitions else self.transition_matrix
+        c = self.__dict__.get("_plan_cache")
+        if (c is not None and c[0] is src and c[1] == src._version and c[2] == log_transitions.device
+                and c[3] == tuple(log_transitions.shape)):
+            return c[4]
+        plan = ops.make_plan(log_transitions.detach())
+        self.__dict__["_plan_cache"] = (src, src._version, log_transitions.device, tuple(log_transitions.shape), plan)
+        return plan
+
     def _viterbi_decode(self, obs_log_probs: torch.Tensor,
                         log_transitions: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor]:
         """(states (B,T), max_j delta_{T-1}[j] (B,)) with delta_0 = lp_0 - log S
         (mixture_gaussian.py:290-338)."""
         S = obs_log_probs.shape[-1]
         init = -(torch.zeros(S, device=obs_log_probs.device) + math.log(S))
+        plan = self._transition_plan(log_transitions)
         if needs_grad(obs_log_probs, log_transitions):
             # the score's gradient follows the decoded path (the reference's max-plus autograd)
-            return ViterbiScore.apply(obs_log_probs, log_transitions, init)
-        states, _, final = ops.viterbi(obs_log_probs, log_transitions, init, ops.OBS_LOG)
+            return ViterbiScore.apply(obs_log_probs, log_transitions, init, plan)
+        states, _, final = ops.viterbi(obs_log_probs, log_transitions, init, ops.OBS_LOG, plan)
         return states, final
 
     def forward(self, observations: torch.Tensor,

@@ -52,6 +52,25 @@ def make_plan(log_P: Tensor) -> Tensor:
     return plan
 
 
+def plan_info(plan: Optional[Tensor]) -> dict:
+    """Which chains a plan selects (band.h BandDesc: wc/wr window widths, Toeplitz windows);
+    with no plan or HMM355_DENSE=1 the dense chains run.  Reads a few ints back to the host."""
+    import os
+    if plan is None or os.environ.get("HMM355_DENSE", "") == "1":
+        return {"forward": "dense", "backward": "dense", "viterbi": "dense"}
+    h = plan[: 4 * 7177].cpu().view(torch.int32).tolist()
+    wc, wr = h[0], h[1]
+    tcd0, tcw, trd0, trw = h[7172:7176]
+    band_max = 8   # band.h kBandMax
+
+    def name(w, tw, td0):
+        if w > band_max:
+            return "dense"
+        return f"banded(W={w}, toeplitz {td0}..{td0 + tw - 1})" if tw > 0 else f"banded(W={w})"
+    col = name(wc, tcw, tcd0)
+    return {"forward": col, "viterbi": col, "backward": name(wr, trw, trd0)}
+
+
 @torch.library.custom_op("hmm355::forward_backward", mutates_args=())
 def forward_backward(obs: Tensor, log_P: Tensor, log_p0: Tensor, obs_mode: int,
                      out_mask: int, plan: Optional[Tensor] = None) -> Tuple[Tensor, Tensor, Tensor, Tensor, Tensor]:
@@ -127,7 +146,7 @@ def gmm_diag_logprob(x: Tensor, means: Tensor, log_vars: Tensor, log_w: Tensor, 
     if B * T == 0:
         return out
     L = nat.lib()
-    ws = _workspace(L.hmm355_gmm_workspace_bytes(D, S, C), x.device)
+    ws = _workspace(L.hmm355_gmm_workspace_bytes(B, T, D, S, C), x.device)
     with torch.cuda.device(x.device):
         nat.check(L.hmm355_gmm_diag_logprob_f32(
             nat.ptr(x), nat.ptr(means), nat.ptr(log_vars), nat.ptr(log_w), B, T, D, S, C, mix_lse,

@@ -209,3 +209,34 @@ def test_gaussian_layer_compute_loss_backward():
     assert torch.isfinite(loss)
     for name, p in layer.named_parameters():
         assert p.grad is not None and torch.isfinite(p.grad).all(), name
+
+
+@pytest.mark.parametrize("mat", ["l2r", "rand"])
+def test_loglik_gradients_obs_log_low_emissions(mat):
+    """OBS_LOG with log-emissions around -200 (the shifted-emission chains): gradients of the
+    exact log-likelihood vs fp64 autograd through the reference's log-space loop."""
+    rng = np.random.default_rng(17)
+    B, T, N = 2, 40, 32
+    P = O.left_to_right_matrix(N, 0.7) if mat == "l2r" else torch.from_numpy(rng.random((N, N), dtype=np.float32))
+    lP, lp0 = O.hmm_params(P)
+    lo = torch.from_numpy((-(rng.random((B, T, N)) * 240 + 80)).astype(np.float32))
+    lo64 = lo.double().requires_grad_(True)
+    lP64 = lP.double().requires_grad_(True)
+    l064 = lp0.double().requires_grad_(True)
+    la = l064 + lo64[:, 0]
+    for tt in range(1, T):
+        la = torch.logsumexp(la[:, :, None] + lP64[None], dim=1) + lo64[:, tt]
+    w = torch.linspace(0.5, 1.5, B, dtype=torch.float64)
+    (torch.logsumexp(la, -1) * w).sum().backward()
+
+    from pytorch_hmm_amd.autograd import SequenceLogLik
+    from pytorch_hmm_amd import ops
+    o = lo.to(DEV).requires_grad_(True)
+    P_ = lP.to(DEV).requires_grad_(True)
+    p0 = lp0.to(DEV).requires_grad_(True)
+    ll = SequenceLogLik.apply(o, P_, p0, ops.OBS_LOG, "exact")
+    (ll * w.float().to(DEV)).sum().backward()
+    np.testing.assert_allclose(ll.detach().cpu().numpy(), torch.logsumexp(la, -1).detach().numpy(), rtol=2e-6)
+    close(o.grad.cpu(), lo64.grad)
+    close(P_.grad.cpu(), lP64.grad)
+    close(p0.grad.cpu(), l064.grad)

@@ -193,3 +193,47 @@ def test_hsmm_vs_c_oracle(B, T, S, Dm):
     states, scores = o.hsmm_viterbi(t(lp), t(dur), t(logT))
     assert np.array_equal(states.cpu().numpy(), cs)
     assert np.array_equal(scores.cpu().numpy(), csc)
+
+
+# ---------------------------------------------- forward-backward on log-emissions (OBS_LOG)
+@pytest.mark.parametrize("mat", ["l2r", "ergodic", "rand"])
+@pytest.mark.parametrize("B,T,N", [(2, 300, 128), (3, 77, 40), (1, 50, 256), (2, 129, 64)])
+def test_forward_backward_obs_log_low_emissions(mat, B, T, N):
+    """Log-emissions in [-400, -80] (Gaussian log-densities at D = 80, the producers
+    mixture_gaussian.py:354 / hsmm.py:225): exp(lo) alone underflows, the chains stage
+    exp(lo - max_j lo) and carry the shift in the log-scales.  Banded (l2r, ergodic) and dense
+    (rand) chains, against the fp64 oracle: posterior atol 2e-5, loglik rtol 2e-6."""
+    rng = np.random.default_rng(B * T + N)
+    if mat == "l2r":
+        P = O.left_to_right_matrix(N, 0.7)
+    elif mat == "ergodic":
+        P = O.transition_matrix(N, "ergodic")
+    else:
+        P = torch.from_numpy(rng.random((N, N), dtype=np.float32))
+    lP, lp0 = O.hmm_params(P)
+    lo = (-(rng.random((B, T, N)) * 320 + 80)).astype(np.float32)
+    lo[0, T // 2, :] -= 5000.0    # a whole row far below the rest: only the shift keeps it
+    la, lb, post64, ll64 = O.c_fb64(lo, lP.numpy(), lp0.numpy())
+    o = ops()
+    post, fwd, bwd, loglik, lik_ref = o.forward_backward(t(lo), t(lP), t(lp0), o.OBS_LOG,
+                                                         o.FB_POSTERIOR | o.FB_FORWARD | o.FB_BACKWARD)
+    assert np.all(np.isfinite(post.cpu().numpy())) and np.all(np.isfinite(loglik.cpu().numpy()))
+    np.testing.assert_allclose(post.cpu().numpy(), post64, atol=2e-5, rtol=0)
+    np.testing.assert_allclose(loglik.cpu().numpy(), ll64, rtol=2e-6)
+    # exp(log alpha) / exp(log beta) underflow to 0 wherever the true values do
+    assert np.all(fwd.cpu().numpy()[np.exp(la) == 0] == 0)
+
+
+def test_forward_backward_obs_log_matches_obs_prob():
+    """Ordinary probabilities: OBS_LOG on log(x + 1e-8) and OBS_PROB on x give the same
+    posteriors (the shift is exact bookkeeping)."""
+    rng = np.random.default_rng(9)
+    B, T, N = 2, 200, 128
+    obs = rng.random((B, T, N), dtype=np.float32)
+    lP, lp0 = O.hmm_params(O.left_to_right_matrix(N, 0.7))
+    lo = np.log((obs + np.float32(1e-8)).astype(np.float64)).astype(np.float32)
+    o = ops()
+    p1, _, _, l1, _ = o.forward_backward(t(obs), t(lP), t(lp0), o.OBS_PROB, o.FB_POSTERIOR)
+    p2, _, _, l2, _ = o.forward_backward(t(lo), t(lP), t(lp0), o.OBS_LOG, o.FB_POSTERIOR)
+    np.testing.assert_allclose(p1.cpu().numpy(), p2.cpu().numpy(), atol=1e-5)
+    np.testing.assert_allclose(l1.cpu().numpy(), l2.cpu().numpy(), rtol=2e-6)

@@ -66,7 +66,7 @@ def test_workspace_sizes(L):
     assert fb >= 2 * B * T * 128 * 4 + 2 * B * T * 4  # scaled alpha/beta rows + log-scales
     vit = L.hmm355_viterbi_workspace_bytes(B, T, N)
     assert vit >= B * T * 128                          # uint8 backpointers
-    assert L.hmm355_gmm_workspace_bytes(80, 128, 4) > 0
+    assert L.hmm355_gmm_workspace_bytes(32, 2000, 80, 128, 4) > 0
     assert L.hmm355_hsmm_workspace_bytes(16, 2000, 64, 40) > 0
 
 
