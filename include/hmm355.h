@@ -89,6 +89,23 @@ int hmm355_forward_backward_f32(const float* obs, int obs_mode, const float* log
                                 size_t workspace_bytes, void* stream);
 
 /* ---------------------------------------------------------------------------------
+ * Adjoint of forward-backward's outputs (posterior / forward / backward).  Replaces the
+ * reference's autograd through its log-space loops (hmm.py:89-130) when a loss of the
+ * posteriors is back-propagated (HMMLayer training mode, hmm_layer.py:119-121; the
+ * supervised cross-entropy of compute_loss, :159-165).  Two linear chains per sequence:
+ *   W_{T-1} = Sw_{T-1};  W_{t-1}[i] = Sw_{t-1}[i] + Fw_{t-1} * sum_j A[i][j] E_t[j] W_t[j]
+ *   Z_0 = Sz_0;          Z_{t+1}[j] = Sz_{t+1}[j] + P_{t+1}[j],
+ *                        P_{t+1}[j] = Fz_{t+1} * E_{t+1}[j] * sum_i Z_t[i] A[i][j]
+ * with A = exp(log_P).  E, src_w (Sw), src_z (Sz) are (B,T,N); scale_w (Fw), scale_z (Fz)
+ * are (B,T) (Fw[T-1] and Fz[0] are not read).  Outputs W (B,T,N) and P (B,T,N), P_0 = 0.
+ * pytorch_hmm_amd/autograd.py (ForwardBackwardFn) forms the sources from the output
+ * gradients and the stored scaled rows, and the parameter gradients from W and Z.
+ * ------------------------------------------------------------------------------ */
+int hmm355_fb_adjoint_f32(const float* E, const float* log_P, const float* src_w,
+                          const float* scale_w, const float* src_z, const float* scale_z,
+                          int B, int T, int N, float* W, float* P, void* stream);
+
+/* ---------------------------------------------------------------------------------
  * Transition plan: the banded decomposition of log_P (csrc/band.h) measured once into
  * caller-owned device memory (hmm355_plan_bytes(N) bytes), for callers whose matrix is fixed
  * across calls (HMMPyTorch computes log_P once in __init__, hmm.py:39-42).  The *_plan_f32

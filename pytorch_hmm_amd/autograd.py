@@ -19,8 +19,9 @@ last contraction is a plain batched GEMM (torch.einsum -> hipBLASLt).
 Losses: 'ref'   = the reference's compute_likelihood value LSE_j log(exp(log alpha_{T-1,j}) + 1e-8)
                   (its gradient underflows to 0 exactly where the reference's does);
         'exact' = log sum_j alpha_{T-1,j}  (HMMPyTorch.log_likelihood).
-Posteriors from forward_backward are returned as values; back-propagating THROUGH them
-(e.g. the supervised cross-entropy of compute_loss) is not implemented and raises.
+Back-propagating THROUGH the posteriors / forward / backward outputs (HMMLayer training,
+the supervised cross-entropy of compute_loss) is ForwardBackwardFn: the adjoint of both
+recursions with per-step sources, on hmm355_fb_adjoint_f32 (csrc/adjoint.hip).
 """
 import math
 
@@ -37,20 +38,24 @@ def _pad(N):
     return 64 if N <= 64 else (128 if N <= 128 else 256)
 
 
-def _run_fb(obs, log_P, log_p0, obs_mode, log_beta_T=None, posterior=False):
-    """One hmm355_forward_backward_ex_f32 call; returns (posterior|None, loglik, lik_ref, U, V, LA, LB)."""
+def _run_fb(obs, log_P, log_p0, obs_mode, log_beta_T=None, posterior=False, out_mask=None, plan=None):
+    """One hmm355_forward_backward_plan_f32 call; returns (posterior|None, loglik, lik_ref, U, V,
+    LA, LB), or with `out_mask` ((posterior, forward, backward) per the mask, loglik, lik_ref, U,
+    V, LA, LB)."""
     B, T, N = obs.shape
     NP = _pad(N)
     dev = obs.device
     L = nat.lib()
     ws = torch.empty(L.hmm355_fb_workspace_bytes(B, T, N), dtype=torch.uint8, device=dev)
-    post = torch.empty(B, T, N, device=dev) if posterior else None
+    mask = out_mask if out_mask is not None else (nat.FB_POSTERIOR if posterior else 0)
+    mk = lambda bit: torch.empty(B, T, N, device=dev) if mask & bit else None
+    post, fwd, bwd = mk(nat.FB_POSTERIOR), mk(nat.FB_FORWARD), mk(nat.FB_BACKWARD)
     loglik = torch.empty(B, device=dev)
     lik_ref = torch.empty(B, device=dev)
     with torch.cuda.device(dev):
-        nat.check(L.hmm355_forward_backward_ex_f32(
-            nat.ptr(obs), obs_mode, nat.ptr(log_P), nat.ptr(log_p0), nat.ptr(log_beta_T), B, T, N,
-            nat.FB_POSTERIOR if posterior else 0, nat.ptr(post), None, None, nat.ptr(loglik), nat.ptr(lik_ref),
+        nat.check(L.hmm355_forward_backward_plan_f32(
+            nat.ptr(obs), obs_mode, nat.ptr(log_P), nat.ptr(log_p0), nat.ptr(plan), nat.ptr(log_beta_T), B, T, N,
+            mask, nat.ptr(post), nat.ptr(fwd), nat.ptr(bwd), nat.ptr(loglik), nat.ptr(lik_ref),
             nat.ptr(ws), ws.numel(), nat.stream_of(dev)))
     rows = B * T
     # workspace layout: U | V (B,T,NP) then LA | LB (B,T), pieces 256-B aligned (hmm355.h)
@@ -60,7 +65,19 @@ def _run_fb(obs, log_P, log_p0, obs_mode, log_beta_T=None, posterior=False):
     off = ((2 * rows * NP * 4 + 255) // 256) * 256 // 4
     LA = fl[off: off + rows].view(B, T)
     LB = fl[off + rows: off + 2 * rows].view(B, T)
+    if out_mask is not None:
+        return (post, fwd, bwd), loglik, lik_ref, U, V, LA, LB
     return post, loglik, lik_ref, U, V, LA, LB
+
+
+def _staged_emissions(obs, obs_mode):
+    """The emissions the chains multiply by: obs + 1e-8 (OBS_PROB, hmm.py:86) or exp(obs - M_t)
+    with M_t the row maximum (OBS_LOG; 0 for a row without a finite maximum, hmm355.h)."""
+    if obs_mode == nat.OBS_PROB:
+        return obs + 1e-8
+    m = obs.amax(-1, keepdim=True)
+    m = torch.where(torch.isfinite(m), m, torch.zeros_like(m))
+    return torch.exp(obs - m)
 
 
 class SequenceLogLik(torch.autograd.Function):
@@ -199,9 +216,101 @@ class TvSequenceLogLik(torch.autograd.Function):
         return grad_lo, grad_A, grad_l0, None
 
 
-class _NoPosteriorGrad(torch.autograd.Function):
-    """Carries forward-backward outputs (computed by the kernels) into a graph whose inputs
-    require grad: the values are exact, back-propagating through them raises."""
+class ForwardBackwardFn(torch.autograd.Function):
+    """HMMPyTorch.forward_backward outputs (posterior, forward, backward) per `out_mask`,
+    differentiable in obs, log_P and log_p0 — the reference back-propagates through its
+    log-space loops (hmm.py:89-130; HMMLayer training mode hmm_layer.py:119-121, supervised
+    compute_loss :159-165).  Forward: the gfx950 chains, keeping their scaled rows
+    (alpha_t = U_t exp(LA_t), beta_t = V_t exp(LB_t)).  Backward: the analytic adjoint.
+
+    With a = log alpha, b = log beta, gamma = exp(a + b - LSE(a + b)) and output gradients
+    Gp, Gf, Gb, the direct adjoints are
+        h_t = gamma_t (Gp_t - <gamma_t, Gp_t>) + Gf_t exp(a_t)     (of a_t)
+        k_t = gamma_t (Gp_t - <gamma_t, Gp_t>) + Gb_t exp(b_t)     (of b_t).
+    The total adjoint of a_t is alpha_t * W_t e^{-LA_t}, W the forward recursion's adjoint in
+    alpha's scaling, and that of b_t is beta_t * Z_t e^{-LB_t}:
+        W_{t-1} = h_{t-1} / u_{t-1} + (1/c_{t-1}) A (E_t W_t),          c_t = sum u_t
+        Z_{t+1} = k_{t+1} / v_{t+1} + (1/c'_t) E_{t+1} (A^T Z_t),       c'_t = sum v_{t+1} E_{t+1}
+    (hmm355_fb_adjoint_f32), where h/u = v (Gp - <.,.>) / sum(u v) + Gf exp(LA) and
+    k/v = u (Gp - <.,.>) / sum(u v) + Gb exp(LB) are O(1) (no division by a vanishing u or v).
+    Then, with P = Z - k/v the propagated part of Z,
+        dL/d log_obs_t = u_t W_t + v_t P_t
+        dL/d log_p0    = sum_b u_0 W_0
+        dL/d log_P     = exp(log_P) * sum_{b,t} [ (u_{t-1}/c_{t-1}) (x) (E_t W_t)
+                                                 + Z_t (x) (E_{t+1} v_{t+1} / c'_t) ]
+    (two GEMMs over the frames, hipBLASLt through torch)."""
+
+    @staticmethod
+    def forward(ctx, obs, log_P, log_p0, obs_mode, out_mask, plan=None):
+        nat.require_gpu(obs, log_P, log_p0)
+        obs_c, lP, l0 = (t.detach().to(torch.float32).contiguous() for t in (obs, log_P, log_p0))
+        outs, _, _, U, V, _, _ = _run_fb(obs_c, lP, l0, obs_mode, out_mask=out_mask | nat.FB_POSTERIOR, plan=plan)
+        post, fwd, bwd = outs
+        ctx.save_for_backward(obs_c, lP, l0, U, V, post, fwd, bwd)
+        ctx.obs_mode, ctx.out_mask = obs_mode, out_mask
+        ctx.set_materialize_grads(False)   # outputs the loss does not use arrive as None
+        res = tuple(o for bit, o in ((nat.FB_POSTERIOR, post), (nat.FB_FORWARD, fwd), (nat.FB_BACKWARD, bwd))
+                    if out_mask & bit)
+        return res
+
+    @staticmethod
+    def backward(ctx, *grads):
+        obs, lP, l0, U, V, post, fwd, bwd = ctx.saved_tensors
+        B, T, N = obs.shape
+        returned = [k for bit, k in ((nat.FB_POSTERIOR, "p"), (nat.FB_FORWARD, "f"), (nat.FB_BACKWARD, "b"))
+                    if ctx.out_mask & bit]
+        got = dict(zip(returned, grads))
+        gp, gf, gb = got.get("p"), got.get("f"), got.get("b")
+        E = _staged_emissions(obs, ctx.obs_mode)
+        U64, V64 = U.double(), V.double()
+        Suv = (U64 * V64).sum(-1, keepdim=True)
+        srcW = torch.zeros(B, T, N, dtype=torch.float64, device=obs.device)
+        srcZ = torch.zeros_like(srcW)
+        if gp is not None:
+            g64 = gp.double()
+            q = (g64 - (post.double() * g64).sum(-1, keepdim=True)) / torch.where(Suv > 0, Suv, torch.ones_like(Suv))
+            q = torch.where(Suv > 0, q, torch.zeros_like(q))
+            srcW += V64 * q
+            srcZ += U64 * q
+        if gf is not None:
+            srcW += torch.where(U64 > 0, gf.double() * fwd.double() / torch.where(U64 > 0, U64, torch.ones_like(U64)),
+                                torch.zeros_like(U64))
+        if gb is not None:
+            srcZ += torch.where(V64 > 0, gb.double() * bwd.double() / torch.where(V64 > 0, V64, torch.ones_like(V64)),
+                                torch.zeros_like(V64))
+        srcW, srcZ = srcW.float().contiguous(), srcZ.float().contiguous()
+        Fw = (1.0 / U64.sum(-1)).float().contiguous()                       # 1/c_t
+        Fz = torch.zeros(B, T, device=obs.device)
+        if T > 1:
+            Fz[:, 1:] = (1.0 / (V64[:, 1:] * E[:, 1:].double()).sum(-1)).float()   # 1/c'_{t-1}
+        E = E.contiguous()
+        W = torch.empty(B, T, N, device=obs.device)
+        P = torch.empty(B, T, N, device=obs.device)
+        L = nat.lib()
+        with torch.cuda.device(obs.device):
+            nat.check(L.hmm355_fb_adjoint_f32(nat.ptr(E), nat.ptr(lP), nat.ptr(srcW), nat.ptr(Fw), nat.ptr(srcZ),
+                                              nat.ptr(Fz), B, T, N, nat.ptr(W), nat.ptr(P),
+                                              nat.stream_of(obs.device)))
+        grad_lo = U * W + V * P
+        grad_obs = grad_lo / (obs + 1e-8) if ctx.obs_mode == nat.OBS_PROB else grad_lo
+        grad_l0 = (U[:, 0] * W[:, 0]).sum(0)
+        grad_lP = None
+        if ctx.needs_input_grad[1]:
+            M = torch.zeros(N, N, device=obs.device)
+            if T > 1:
+                X1 = U[:, :-1] * Fw[:, :-1, None]
+                Y1 = E[:, 1:] * W[:, 1:]
+                Z = srcZ + P
+                Y2 = E[:, 1:] * V[:, 1:] * Fz[:, 1:, None]
+                M = torch.einsum("bti,btj->ij", X1, Y1) + torch.einsum("bti,btj->ij", Z[:, :-1], Y2)
+            grad_lP = torch.exp(lP) * M
+        return grad_obs, grad_lP, grad_l0, None, None, None
+
+
+class _TvNoPosteriorGrad(torch.autograd.Function):
+    """NeuralHMM forward-backward outputs in a graph whose inputs require grad: the values are
+    exact; back-propagating through the posteriors of the per-step-matrix recursion is not
+    implemented (its likelihood is differentiable: TvSequenceLogLik)."""
 
     @staticmethod
     def forward(ctx, obs, log_P, log_p0, *outs):
@@ -210,12 +319,17 @@ class _NoPosteriorGrad(torch.autograd.Function):
     @staticmethod
     def backward(ctx, *grads):
         raise NotImplementedError(
-            "gradients through forward-backward posteriors are not implemented on the MI355X path; "
-            "differentiate compute_likelihood / compute_loss (unsupervised) instead")
+            "gradients through NeuralHMM forward-backward posteriors are not implemented on the MI355X path; "
+            "differentiate compute_likelihood instead")
 
 
-def forward_backward_with_grad(obs, log_P, log_p0, outs):
-    return _NoPosteriorGrad.apply(obs, log_P, log_p0, *outs)
+def tv_forward_backward_with_grad(obs, log_A, log_p0, outs):
+    return _TvNoPosteriorGrad.apply(obs, log_A, log_p0, *outs)
+
+
+def forward_backward_with_grad(obs, log_P, log_p0, obs_mode, out_mask, plan=None):
+    """Differentiable forward-backward outputs (tuple per out_mask: posterior, forward, backward)."""
+    return ForwardBackwardFn.apply(obs, log_P, log_p0, obs_mode, out_mask, plan)
 
 
 class GmmLogProb(torch.autograd.Function):

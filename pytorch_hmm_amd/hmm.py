@@ -83,11 +83,12 @@ class HMMPyTorch(HMM):
         B, T, K = obs.shape
         assert K == self.K, f"Observation dim {K} must match model states {self.K}"
         log_P, log_p0, plan = self._device_params(obs.device)
-        post, fwd, bwd, _, _ = ops.forward_backward(
-            obs.detach(), log_P.detach(), log_p0.detach(), ops.OBS_PROB,
-            ops.FB_POSTERIOR | ops.FB_FORWARD | ops.FB_BACKWARD, plan)
+        mask = ops.FB_POSTERIOR | ops.FB_FORWARD | ops.FB_BACKWARD
         if needs_grad(obs, log_P, log_p0):
-            post, fwd, bwd = forward_backward_with_grad(obs, log_P, log_p0, (post, fwd, bwd))
+            # differentiable through all three outputs (autograd.ForwardBackwardFn)
+            return forward_backward_with_grad(obs, log_P, log_p0, ops.OBS_PROB, mask, plan)
+        post, fwd, bwd, _, _ = ops.forward_backward(obs.detach(), log_P.detach(), log_p0.detach(), ops.OBS_PROB,
+                                                    mask, plan)
         return post, fwd, bwd
 
     def posteriors(self, observations: torch.Tensor) -> torch.Tensor:
@@ -95,11 +96,10 @@ class HMMPyTorch(HMM):
         obs, _ = self._as_batch(observations)
         assert obs.shape[-1] == self.K, f"Observation dim {obs.shape[-1]} must match model states {self.K}"
         log_P, log_p0, plan = self._device_params(obs.device)
-        post = ops.forward_backward(obs.detach(), log_P.detach(), log_p0.detach(), ops.OBS_PROB,
-                                    ops.FB_POSTERIOR, plan)[0]
         if needs_grad(obs, log_P, log_p0):
-            (post,) = forward_backward_with_grad(obs, log_P, log_p0, (post,))
-        return post
+            return forward_backward_with_grad(obs, log_P, log_p0, ops.OBS_PROB, ops.FB_POSTERIOR, plan)[0]
+        return ops.forward_backward(obs.detach(), log_P.detach(), log_p0.detach(), ops.OBS_PROB,
+                                    ops.FB_POSTERIOR, plan)[0]
 
     def viterbi_decode(self, observations: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor]:
         """(states (B,T) int64, log_delta (B,T,K)); 2-D input squeezed (hmm.py:132-184)."""

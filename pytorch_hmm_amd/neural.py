@@ -19,7 +19,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from . import ops
-from .autograd import needs_grad, TvSequenceLogLik, forward_backward_with_grad
+from .autograd import needs_grad, TvSequenceLogLik, tv_forward_backward_with_grad
 
 
 class NeuralTransitionModel(nn.Module):
@@ -190,7 +190,7 @@ class NeuralHMM(nn.Module):
         mask = ops.FB_POSTERIOR | ops.FB_FORWARD | ops.FB_BACKWARD
         post, fwd, bwd, _, _ = ops.tv_forward_backward(log_obs.detach(), log_A.detach(), log_init.detach(), mask)
         if needs_grad(log_obs, log_A, log_init):
-            post, fwd, bwd = forward_backward_with_grad(log_obs, log_A, log_init, (post, fwd, bwd))
+            post, fwd, bwd = tv_forward_backward_with_grad(log_obs, log_A, log_init, (post, fwd, bwd))
         return post, fwd, bwd
 
     def viterbi_decode(self, observations: torch.Tensor,

@@ -114,14 +114,115 @@ def test_hmmlayer_training_step_changes_transitions():
     assert not torch.allclose(before, layer.get_transition_matrix())
 
 
-def test_posterior_values_flow_but_backprop_raises():
+# ------------------------------------------------- gradients THROUGH the FB outputs
+def fb_ref64(x, lP, lp0, log_mode):
+    """hmm.py:86-130 in float64 autograd (the reference's log-space loops)."""
+    lo = x if log_mode else torch.log(x + 1e-8)
+    B, T, K = lo.shape
+    la = [lp0 + lo[:, 0]]
+    for t in range(1, T):
+        la.append(torch.logsumexp(la[-1][:, :, None] + lP[None], dim=1) + lo[:, t])
+    lb = [torch.zeros(B, K, dtype=lo.dtype)]
+    for t in range(T - 2, -1, -1):
+        lb.insert(0, torch.logsumexp(lP[None] + lo[:, t + 1, None, :] + lb[0][:, None, :], dim=2))
+    la, lb = torch.stack(la, 1), torch.stack(lb, 1)
+    lp = la + lb
+    lp = lp - torch.logsumexp(lp, dim=-1, keepdim=True)
+    return torch.exp(lp), torch.exp(la), torch.exp(lb)
+
+
+def _matrix(kind, N):
+    if kind == "l2r":
+        return O.left_to_right_matrix(N, 0.7)
+    if kind == "ergodic":
+        return O.transition_matrix(N, "ergodic")
+    g = torch.Generator().manual_seed(N)
+    return torch.softmax(torch.randn(N, N, generator=g), -1)
+
+
+@pytest.mark.parametrize("N", [5, 70, 128])
+@pytest.mark.parametrize("kind", ["l2r", "ergodic", "random"])
+@pytest.mark.parametrize("log_mode", [False, True])
+@pytest.mark.parametrize("outs", ["post", "all"])
+def test_output_vjp_matches_fp64_autograd(N, kind, log_mode, outs):
+    """d(sum Gp*posterior + Gf*forward + Gb*backward) / d(obs, log_P, log_p0) through
+    ForwardBackwardFn (hmm355_fb_adjoint_f32) vs float64 autograd through the loops."""
+    from pytorch_hmm_amd import ops
+    from pytorch_hmm_amd.autograd import ForwardBackwardFn
+    g = torch.Generator().manual_seed(7 * N + (3 if log_mode else 0))
+    B, T = 2, 40
+    if log_mode:   # Gaussian-like log-emissions far below -87 (the OBS_LOG row-max shift)
+        x = -150.0 + 20.0 * torch.randn(B, T, N, generator=g)
+    else:
+        x = torch.softmax(torch.randn(B, T, N, generator=g), -1)
+    lP, lp0 = O.hmm_params(_matrix(kind, N))
+    Gp = torch.randn(B, T, N, generator=g)
+    Gf = torch.randn(B, T, N, generator=g) if outs == "all" else None
+    Gb = torch.randn(B, T, N, generator=g) if outs == "all" else None
+    ref = [t.double().requires_grad_(True) for t in (x, lP, lp0)]
+    p, f, b = fb_ref64(ref[0], ref[1], ref[2], log_mode)
+    loss = (p * Gp.double()).sum()
+    if outs == "all":
+        loss = loss + (f * Gf.double()).sum() + (b * Gb.double()).sum()
+    loss.backward()
+    ours = [t.to(DEV).requires_grad_(True) for t in (x, lP, lp0)]
+    mask = ops.FB_POSTERIOR | (ops.FB_FORWARD | ops.FB_BACKWARD if outs == "all" else 0)
+    res = ForwardBackwardFn.apply(ours[0], ours[1], ours[2], ops.OBS_LOG if log_mode else ops.OBS_PROB, mask)
+    l2 = (res[0] * Gp.to(DEV)).sum()
+    if outs == "all":
+        l2 = l2 + (res[1] * Gf.to(DEV)).sum() + (res[2] * Gb.to(DEV)).sum()
+    l2.backward()
+    # per tensor: 1e-4 of its largest entry, plus 1e-5 of the emission-gradient scale (with
+    # log-emissions 20 nats apart the log_p0 gradient is a ~1e-4 residue of O(1) adjoints;
+    # the reference's own fp32 autograd misses it by ~1e-3 there)
+    gscale = float(ref[0].grad.abs().max())
+    for a, r in zip(ours, ref):
+        err = float((a.grad.cpu().double() - r.grad).abs().max())
+        assert err <= 1e-4 * float(r.grad.abs().max()) + 1e-5 * gscale, (err, float(r.grad.abs().max()), gscale)
+
+
+def test_hmmlayer_supervised_loss_gradients():
+    """HMMLayer training mode + compute_loss(target_alignment) (hmm_layer.py:119-121,159-165):
+    the cross-entropy on the posteriors back-propagates to the logits and the input as the
+    reference's autograd does.  compute_loss calls _get_hmm() and then forward() calls it
+    again, so the posteriors use the later-call tables log(softmax + 1e-8) (hmm_layer.py:83-86)."""
+    torch.manual_seed(3)
+    K, B, T = 6, 3, 30
+    layer = ph.HMMLayer(K).to(DEV)
+    layer.train()
+    x = torch.randn(B, T, K)
+    tgt = torch.randint(0, K, (B, T))
+    xd = x.to(DEV).requires_grad_(True)
+    loss = layer.compute_loss(xd, target_alignment=tgt.to(DEV))
+    loss.backward()
+    lt = layer.log_transition_logits.detach().cpu().double().requires_grad_(True)
+    li = layer.log_initial_logits.detach().cpu().double().requires_grad_(True)
+    xr = x.double().requires_grad_(True)
+    P = torch.softmax(lt, dim=1)
+    p0 = torch.softmax(li, dim=0)
+    post = fb_ref64(torch.sigmoid(xr), torch.log(P + 1e-8), torch.log(p0 + 1e-8), False)[0]
+    lref = torch.nn.functional.cross_entropy(post.reshape(-1, K), tgt.reshape(-1))
+    lref.backward()
+    assert abs(float(loss) - float(lref)) < 1e-5
+    close(xd.grad.cpu(), xr.grad)
+    close(layer.log_transition_logits.grad.cpu(), lt.grad)
+    close(layer.log_initial_logits.grad.cpu(), li.grad)
+
+
+def test_hmmlayer_posterior_training_step():
+    """A training step on a loss of the train-mode posteriors changes the transitions."""
+    torch.manual_seed(0)
     layer = ph.HMMLayer(4).to(DEV)
     layer.train()
+    opt = torch.optim.SGD(layer.parameters(), lr=0.5)
     x = torch.randn(2, 8, 4, device=DEV, requires_grad=True)
+    before = layer.get_transition_matrix().detach().clone()
     post = layer(x)
     assert post.requires_grad and torch.allclose(post.sum(-1), torch.ones(2, 8, device=DEV), atol=1e-5)
-    with pytest.raises(NotImplementedError):
-        post.sum().backward()
+    (post[..., 0] ** 2).sum().backward()
+    assert torch.isfinite(x.grad).all() and x.grad.abs().sum() > 0
+    opt.step()
+    assert not torch.allclose(before, layer.get_transition_matrix())
 
 
 # ------------------------------------------------------------------ emission / Viterbi score
