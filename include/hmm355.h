@@ -45,6 +45,12 @@ extern "C" {
 #define HMM355_FB_POSTERIOR 1u   /* posterior (B,T,N)              hmm.py:120-126 */
 #define HMM355_FB_FORWARD 2u     /* forward = exp(log alpha)        hmm.py:127     */
 #define HMM355_FB_BACKWARD 4u    /* backward = exp(log beta)        hmm.py:128     */
+/* Hint (forward_backward with a plan, no log_beta_T): the plan is banded in both directions
+ * (hmm355_plan_banded() returned 1).  Both chains of a sequence then run in one workgroup and
+ * form posterior / forward / backward inside it (csrc/fbpair.h): the scaled rows are not
+ * written back in full, so the workspace does NOT hold U / V / LA / LB afterwards.  A wrong
+ * hint still gives correct results (slower).  N <= 128; ignored otherwise. */
+#define HMM355_FB_PAIR 0x100u
 
 const char* hmm355_strerror(int code);
 int hmm355_version(void);
@@ -115,6 +121,10 @@ int hmm355_fb_adjoint_f32(const float* E, const float* log_P, const float* src_w
  * ------------------------------------------------------------------------------ */
 size_t hmm355_plan_bytes(int N);
 int hmm355_plan_f32(const float* log_P, int N, void* plan, void* stream);
+/* 1 if the plan selects banded chains for both the forward and the backward recursion (the
+ * condition for HMM355_FB_PAIR), 0 if not, < 0 on error.  Synchronous: waits for `stream`
+ * and copies a few bytes of the plan to the host (call once per plan, not per step). */
+int hmm355_plan_banded(const void* plan, void* stream);
 int hmm355_forward_backward_plan_f32(const float* obs, int obs_mode, const float* log_P,
                                      const float* log_p0, const void* plan,
                                      const float* log_beta_T, int B, int T, int N,

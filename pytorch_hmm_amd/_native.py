@@ -14,6 +14,7 @@ LIB_PATH = os.environ.get("HMM355_LIB", os.path.join(_HERE, "lib", "libhmm355.so
 OBS_PROB = 0
 OBS_LOG = 1
 FB_POSTERIOR = 1
+FB_PAIR = 0x100
 FB_FORWARD = 2
 FB_BACKWARD = 4
 
@@ -29,7 +30,7 @@ EXPORTS = (
     "hmm355_semimarkov_workspace_bytes", "hmm355_semimarkov_quad_f32",
     "hmm355_semimarkov_viterbi_f32", "hmm355_semimarkov_forward_f32",
     "hmm355_stream_greedy_f32", "hmm355_stream_beam_f32",
-    "hmm355_plan_bytes", "hmm355_plan_f32", "hmm355_forward_backward_plan_f32", "hmm355_viterbi_plan_f32",
+    "hmm355_plan_bytes", "hmm355_plan_f32", "hmm355_plan_banded", "hmm355_forward_backward_plan_f32", "hmm355_viterbi_plan_f32",
     "hmm355_fb_adjoint_f32",
 )
 
@@ -86,6 +87,7 @@ def lib():
     F = ctypes.c_float
     L.hmm355_plan_bytes.argtypes, L.hmm355_plan_bytes.restype = [I], S
     L.hmm355_plan_f32.argtypes, L.hmm355_plan_f32.restype = [P, I, P, P], I
+    L.hmm355_plan_banded.argtypes, L.hmm355_plan_banded.restype = [P, P], I
     L.hmm355_forward_backward_plan_f32.argtypes = [P, I, P, P, P, P, I, I, I, U, P, P, P, P, P, P, S, P]
     L.hmm355_forward_backward_plan_f32.restype = I
     L.hmm355_viterbi_plan_f32.argtypes = [P, I, P, P, P, I, I, I, P, P, P, P, S, P]

@@ -14,12 +14,17 @@
 //   FMA per (i,j) cell instead of add + exp + max + add.  The backward pass is the same with
 //   A^T and the emission applied before the product (hmm.py:113-115).
 //
+// With a banded plan and HMM355_FB_PAIR (N <= 128) both chains and the outputs run in ONE
+// workgroup per sequence instead (fbpair.h, fb_pair_kernel): kernels 1 and 2 below are the
+// dense-matrix path and the path that keeps the scaled rows for the adjoint (autograd.py).
+//
 // Kernel 2, fb_posterior<NP>: one wave per (b,t) row, grid-stride, HBM-bound:
 //   posterior = (u*v)/sum(u*v) (scale-invariant), forward = exp(log u + LA),
 //   backward = exp(log v + LB), and the reference's compute_likelihood value
 //   logsumexp_j(log(forward_{T-1}[j] + 1e-8)) (hmm.py:206) for t = T-1.
 #include "recur.h"
 #include "post.h"
+#include "fbpair.h"
 
 namespace hmm355 {
 
@@ -118,6 +123,15 @@ HMM355_API int hmm355_plan_f32(const float* log_P, int N, void* plan, void* stre
   return e == hipSuccess ? HMM355_OK : (int)e;
 }
 
+HMM355_API int hmm355_plan_banded(const void* plan, void* stream) {
+  if (!plan) return HMM355_E_ARG;
+  int wcr[2];
+  hipError_t e = hipStreamSynchronize(static_cast<hipStream_t>(stream));
+  if (e == hipSuccess) e = hipMemcpy(wcr, plan, sizeof(wcr), hipMemcpyDeviceToHost);  // BandDesc wc, wr
+  if (e != hipSuccess) return (int)e;
+  return (wcr[0] <= kBandMax && wcr[1] <= kBandMax) ? 1 : 0;
+}
+
 HMM355_API int hmm355_forward_backward_plan_f32(const float* obs, int obs_mode, const float* log_P,
                                                 const float* log_p0, const void* plan, const float* log_beta_T,
                                                 int B, int T, int N, unsigned out_mask, float* posterior,
@@ -164,6 +178,24 @@ HMM355_API int hmm355_forward_backward_plan_f32(const float* obs, int obs_mode, 
   }
   RecArgs fa{obs, log_P, log_p0, w.U, w.LA, loglik, B, T, N, obs_mode, NP, band, nullptr, nullptr, nullptr, rmax};
   RecArgs fb{obs, log_P, log_p0, w.V, w.LB, nullptr, B, T, N, obs_mode, NP, band, binit, bscale, nullptr, rmax};
+  hipStream_t st0 = static_cast<hipStream_t>(stream);
+  if ((out_mask & HMM355_FB_PAIR) && plan && band && NP <= 128 && !log_beta_T &&
+      (size_t)T * NP * sizeof(float) < ((size_t)1 << 31)) {
+    // both chains of a sequence in one workgroup, outputs formed inside it (fbpair.h)
+    PairArgs pa{fa, fb, posterior, forward, backward, lik_ref, out_mask};
+    hipError_t e;
+    if (NP == 64) {
+      e = allow_lds(fb_pair_kernel<64>, PairL<64>::LDS_FLOATS * sizeof(float));
+      if (e == hipSuccess)
+        hipLaunchKernelGGL(fb_pair_kernel<64>, dim3(B), dim3(PairL<64>::NT), PairL<64>::LDS_FLOATS * sizeof(float), st0, pa);
+    } else {
+      e = allow_lds(fb_pair_kernel<128>, PairL<128>::LDS_FLOATS * sizeof(float));
+      if (e == hipSuccess)
+        hipLaunchKernelGGL(fb_pair_kernel<128>, dim3(B), dim3(PairL<128>::NT), PairL<128>::LDS_FLOATS * sizeof(float), st0, pa);
+    }
+    if (e == hipSuccess) e = hipGetLastError();
+    return e == hipSuccess ? HMM355_OK : (int)e;
+  }
   PostArgs pa{w.U, w.V, w.LA, w.LB, posterior, forward, backward, lik_ref, B, T, N, out_mask};
   hipError_t e;
   switch (NP) {

@@ -28,6 +28,7 @@
 #pragma once
 #include "band.h"
 #include "common.h"
+#include "logcr.h"
 
 namespace hmm355 {
 
@@ -51,7 +52,8 @@ struct RC {
                                                            // the banded chain writes all 64 lanes)
   static constexpr int OFF_M = OFF_SC + RING * 64;        // [128] OBS_LOG FB: staged row maxima (0 else)
   static constexpr int MRING = 128;                        // rows kb-3 .. kb+1 live at once
-  static constexpr int LDS_FLOATS = OFF_M + MRING;
+  static constexpr int OFF_LOGT = OFF_M + MRING;           // [256] doubles: Viterbi log table (logcr.h)
+  static constexpr int LDS_FLOATS = OFF_LOGT + 512;
   static_assert(LDS_FLOATS * 4 <= kExclusiveLds, "LDS layout too large");
 };
 
@@ -197,6 +199,16 @@ __device__ __forceinline__ int rec_tau(int q, int T) {
   return KIND == kFbBeta ? T - 1 - q : q;
 }
 
+// the log table of logcr.h; each wave that stages Viterbi emissions copies it into LDS itself
+// (identical values from every copier, so no barrier: a wave's own LDS writes precede its reads)
+__device__ const double g_logcr_tab[256] = {HMM355_LOGCR_TABLE};
+template <int NP>
+__device__ __forceinline__ void rec_logt_fill(float* lds, int l) {
+  double* t = reinterpret_cast<double*>(lds + RC<NP>::OFF_LOGT);
+#pragma unroll
+  for (int k = 0; k < 4; ++k) t[l + 64 * k] = g_logcr_tab[l + 64 * k];
+}
+
 // ---- emission staging: lane l of wave w holds 4 consecutive states of one step
 // r[0..3]: the emissions; r[4]: the step's row maximum M_t (FB with OBS_LOG; the load reads an
 // address of the same row otherwise, so the staging stays branch-free, and is not used)
@@ -247,10 +259,14 @@ __device__ __forceinline__ void rec_stage(const RecArgs& a, float* lds, int blk,
       e[k] = KIND == kVit ? (ok ? r[k] : -INFINITY) : (ok ? __expf(r[k] - m) : 0.f);
     }
   } else {
+    // Viterbi: log(x + 1e-8) correctly rounded (logcr.h; the fp32 sum as hmm.py:152 forms it)
+    const double* lt = reinterpret_cast<const double*>(lds + C::OFF_LOGT);
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
       const bool ok = qok && col + k < a.N;
-      e[k] = KIND == kVit ? (ok ? log_obs_cr(r[k]) : -INFINITY) : (ok ? r[k] + 1e-8f : 0.f);
+      // (diagnostic ablation bit 1 << 22: no log, timing only)
+      const float lv = (kAbl & (1 << 22)) ? r[k] + 1e-8f : logcr_fast(r[k] + 1e-8f, lt);
+      e[k] = KIND == kVit ? (ok ? lv : -INFINITY) : (ok ? r[k] + 1e-8f : 0.f);
     }
   }
   *reinterpret_cast<float4*>(lds + C::OFF_EMIS + ((blk % 3) * 16 + sq) * NP + col) = make_float4(e[0], e[1], e[2], e[3]);
@@ -324,6 +340,7 @@ __device__ __forceinline__ void rec_run(const RecArgs& a, float* lds, int b) {
 
   const int nblocks = (T + 15) / 16;
   float er0[5], er1[5];
+  if (KIND == kVit) rec_logt_fill<NP>(lds, l);
   rec_load<NP, KIND>(a, b, 0, w, l, er0);
   rec_stage<NP, KIND>(a, lds, 0, w, l, er0);
   if (nblocks > 1) rec_load<NP, KIND>(a, b, 1, w, l, er1);
@@ -507,6 +524,197 @@ __device__ __forceinline__ void rec_run(const RecArgs& a, float* lds, int b) {
   }
 }
 
+// The banded chain wave (wave 0 of rec_band; waves 0 and 1 of the forward-backward pair
+// kernel, fbpair.h): the whole recursion of one sequence in one wave, one lds_barrier per
+// 16-step block and one after the last row, matching the helpers' barriers.  `lds` is the
+// chain's own RC<NP> layout.
+template <int NP, int KIND, int WP, int TD0 = 0, int TW = 0>
+__device__ __forceinline__ void band_chain(const RecArgs& a, float* lds, int b, const BandDesc* __restrict__ d) {
+  using C = RC<NP>;
+  constexpr int NB = C::NBLK;
+  constexpr bool FB = KIND != kVit;
+  constexpr bool FUSE = KIND == kVit && kVitFused<NP>;
+  const int l = threadIdx.x & 63;
+  const int T = a.T, N = a.N;
+  const int nblocks = (T + 15) / 16;
+  // ------------------------------------------------------------------ chain wave
+  // Lane l holds the consecutive states s = NB*l + j (j < NB): a window offset of +-1 is
+  // then another register of the same lane or ONE DPP lane shift (zero-filled at the wave
+  // edge, where the window weight is the neutral element), folded by the compiler into the
+  // add / fma that consumes it.  A wave issues one instruction per ~4 cycles, so the step is
+  // written for instruction count: 16-step blocks fully unrolled (no scalar address math),
+  // the emission read one step ahead, the block's normalisers collected by v_writelane and
+  // stored once per block.
+  constexpr int WW = TW > 0 ? TW : WP;  // window slots per state
+  int lo[NB];
+  float wv[NB][WW], fl[NB];
+#pragma unroll
+  for (int j = 0; j < NB; ++j) {
+    const int s = NB * l + j;
+    lo[j] = KIND == kFbBeta ? d->rlo[s] : d->clo[s];
+#pragma unroll
+    for (int k = 0; k < WW; ++k) {
+      if (TW > 0)
+        wv[j][k] = KIND == kVit ? d->tL[s][k] : (KIND == kFbAlpha ? d->tD[s][k] : d->tR[s][k]);
+      else
+        wv[j][k] = KIND == kVit ? d->cL[s][k] : (KIND == kFbAlpha ? d->cD[s][k] : d->rD[s][k]);
+    }
+    fl[j] = KIND == kVit ? d->rfl[s] : d->afl[s];
+  }
+  const bool uafl = d->uafl != 0;  // one floor for every row: weighted sum = afl0 * plain sum
+  const float afl0 = d->afl[0];
+  auto erow = [&](int rho) { return lds + C::OFF_EMIS + (((rho >> 4) % 3) * 16 + (rho & 15)) * NP + NB * l; };
+  auto ld = [&](const float* p, float(&v)[NB]) {
+    if constexpr (NB == 1) v[0] = p[0];
+    else if constexpr (NB == 2) { const float2 t = *reinterpret_cast<const float2*>(p); v[0] = t.x; v[1] = t.y; }
+    else { const float4 t = *reinterpret_cast<const float4*>(p); v[0] = t.x; v[1] = t.y; v[2] = t.z; v[3] = t.w; }
+  };
+  auto st = [&](float* p, const float(&v)[NB]) {
+    if constexpr (NB == 1) p[0] = v[0];
+    else if constexpr (NB == 2) *reinterpret_cast<float2*>(p) = make_float2(v[0], v[1]);
+    else *reinterpret_cast<float4*>(p) = make_float4(v[0], v[1], v[2], v[3]);
+  };
+  float y[NB];
+  {
+    float e0[NB];
+    ld(erow(0), e0);
+#pragma unroll
+    for (int j = 0; j < NB; ++j) {
+      const int s = NB * l + j;
+      const int ss = s < N ? s : 0;
+      if (KIND == kFbAlpha) y[j] = s < N ? __expf(a.init[ss]) * e0[j] : 0.f;
+      else if (KIND == kFbBeta) y[j] = s < N ? (a.binit ? a.binit[(size_t)b * NP + s] : 1.f) : 0.f;
+      else y[j] = s < N ? a.init[ss] + e0[j] : -INFINITY;
+    }
+  }
+  float* ybuf = lds + C::OFF_PART;  // beta's LDS window source [2][NP] (LDS-window mode)
+  constexpr int EL = KIND == kFbBeta ? 1 : 0;
+  float en[NB];  // the next step's emission (alpha / Viterbi e_q, beta e_{q-1})
+
+  // the value of state s + dd (s = NB*l + j) from register vector v
+  auto at = [&](const float(&v)[NB], int j, int dd) -> float {
+    const int t = j + dd + 4 * NB;
+    const int qq = t / NB - 4, jj = t % NB;
+    const int x = __builtin_bit_cast(int, v[jj]);
+    if (qq == 0) return v[jj];
+    if (qq == -1) return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, x, 0x138, 0xF, 0xF, true));
+    if (qq == 1) return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, x, 0x130, 0xF, 0xF, true));
+    if (qq == -2) {
+      const int t1 = __builtin_amdgcn_update_dpp(0, x, 0x138, 0xF, 0xF, true);
+      return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, t1, 0x138, 0xF, 0xF, true));
+    }
+    const int t1 = __builtin_amdgcn_update_dpp(0, x, 0x130, 0xF, 0xF, true);
+    return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, t1, 0x130, 0xF, 0xF, true));
+  };
+
+  // UA: uniform floor (alpha), a compile-time branch: a runtime one splits every unrolled
+  // step into basic blocks whose joins wait for all outstanding LDS reads
+  auto step = [&](int q, int jj, bool last_in_block, auto UA) {
+    float* row = lds + C::OFF_RING + ((q - 1) & (C::RING - 1)) * NP;
+    st(row + NB * l, y);  // row q-1: flushed by the helpers, window source in LDS mode
+    float eo[NB];
+#pragma unroll
+    for (int j = 0; j < NB; ++j) eo[j] = en[j];
+    if (!last_in_block) ld(erow(q + 1 - EL), en);
+    float acc[NB], src[NB];
+    float cs = 0.f, scale = 1.f;
+    if (KIND == kFbBeta) {  // the product input is y = v * e_{q-1} (hmm.py:113-115)
+      float t = 0.f;
+#pragma unroll
+      for (int j = 0; j < NB; ++j) { src[j] = y[j] * eo[j]; t += src[j]; }
+      if (TW == 0) st(ybuf + ((q - 1) & 1) * NP + NB * l, src);
+      cs = wave_sum_bcast(t);
+#pragma unroll
+      for (int j = 0; j < NB; ++j) acc[j] = fl[j] * cs;
+    } else if (KIND == kFbAlpha) {
+      float t = 0.f;
+#pragma unroll
+      for (int j = 0; j < NB; ++j) { src[j] = y[j]; t += y[j]; }
+      cs = wave_sum_bcast(t);
+      float sw;
+      if constexpr (decltype(UA)::value) {
+        sw = afl0 * cs;
+      } else {
+        float tw = 0.f;
+#pragma unroll
+        for (int j = 0; j < NB; ++j) tw = fmaf(y[j], fl[j], tw);
+        sw = wave_sum_bcast(tw);
+      }
+#pragma unroll
+      for (int j = 0; j < NB; ++j) acc[j] = sw;
+    } else {
+      float g = -INFINITY;
+#pragma unroll
+      for (int j = 0; j < NB; ++j) { src[j] = y[j]; g = fmaxf(g, y[j] + fl[j]); }
+      const float M = wave_max_bcast(g);
+      // fused psi: M_q = max_i fl(delta_{q-1,i} + r_i) is also psi row q's floor maximum
+      if constexpr (FUSE) lds[C::OFF_SC + 64 * ((q - 1) & (C::RING - 1)) + l] = M;
+#pragma unroll
+      for (int j = 0; j < NB; ++j) acc[j] = M;
+    }
+    if (FB) {
+      scale = __builtin_amdgcn_rcpf(cs);
+      lds[C::OFF_SC + 64 * ((q - 1) & (C::RING - 1)) + l] = cs;  // c_{q-1}: one conflict-free store
+    }
+    if constexpr (TW > 0) {
+#pragma unroll
+      for (int k = 0; k < TW; ++k)
+#pragma unroll
+        for (int j = 0; j < NB; ++j) {
+          const float v = at(src, j, TD0 + k);
+          acc[j] = FB ? fmaf(v, wv[j][k], acc[j]) : fmaxf(acc[j], v + wv[j][k]);
+        }
+    } else {
+      const float* wsrc = KIND == kFbBeta ? ybuf + ((q - 1) & 1) * NP : row;
+#pragma unroll
+      for (int j = 0; j < NB; ++j)
+#pragma unroll
+        for (int k = 0; k < WW; ++k) {
+          const float v = wsrc[lo[j] + k];
+          acc[j] = FB ? fmaf(v, wv[j][k], acc[j]) : fmaxf(acc[j], v + wv[j][k]);
+        }
+    }
+#pragma unroll
+    for (int j = 0; j < NB; ++j) {
+      // padded states: the staged emission is 0 (FB) / -inf (Viterbi) and the floors 0
+      if (KIND == kFbAlpha) y[j] = acc[j] * (scale * eo[j]);
+      else if (KIND == kFbBeta) y[j] = acc[j] * scale;
+      else y[j] = acc[j] + eo[j];
+    }
+  };
+
+  auto run_blocks = [&](auto UA) {
+    for (int kb = 0; kb < nblocks; ++kb) {
+      const int q0 = kb * 16 < 1 ? 1 : kb * 16;
+      const int q1 = (kb + 1) * 16 < T ? (kb + 1) * 16 : T;
+      if (q0 < q1) ld(erow(q0 - EL), en);
+      if (q0 == kb * 16 && q1 == kb * 16 + 16) {
+#pragma unroll
+        for (int jj = 0; jj < 16; ++jj) step(kb * 16 + jj, jj, jj == 15, UA);
+      } else {
+        for (int q = q0; q < q1; ++q) step(q, q - kb * 16, q + 1 == q1, UA);
+      }
+      if (!(kAbl & 16384)) lds_barrier();  // B_{kb+1}: block kb+1 staged by the helpers, rows of block kb-1 written
+    }
+  };
+  if constexpr (KIND == kFbAlpha) {
+    if (uafl) run_blocks(std::true_type{});
+    else run_blocks(std::false_type{});
+  } else {
+    run_blocks(std::false_type{});
+  }
+  float* row = lds + C::OFF_RING + ((T - 1) & (C::RING - 1)) * NP;
+  st(row + NB * l, y);
+  if (KIND == kFbAlpha && a.loglik) {
+    float t = 0.f;
+#pragma unroll
+    for (int j = 0; j < NB; ++j) t += y[j];
+    const float cs = wave_sum_bcast(t);
+    if (l == 0) lds[C::OFF_SC + 64 * ((T - 1) & (C::RING - 1))] = cs;
+  }
+  lds_barrier();
+}
+
 // ---------------------------------------------------------------------------------------
 // Banded chain (band.h).  Wave 0 runs the whole recursion; lane l owns states
 // s = 64*blk + l.  Per step: the previous row goes to the LDS ring (it is both the window
@@ -521,11 +729,16 @@ template <int NP, int KIND, int WP, int TD0 = 0, int TW = 0>
 __device__ __forceinline__ void rec_band(const RecArgs& a, float* lds, int b, const BandDesc* __restrict__ d) {
   using C = RC<NP>;
   constexpr int NB = C::NBLK;
-  // Waves 1..3 are the helpers; waves 4.. exit at once, so the chain wave is alone on its
-  // SIMD (a workgroup's waves are spread over the 4 SIMDs) and no helper instruction
-  // competes with it for issue.  Ended waves do not take part in s_barrier.
-  constexpr int NH = 3;
+  // Waves 1..3 are the helpers (forward-backward); waves 4.. exit at once, so the chain wave
+  // is alone on its SIMD (a workgroup's waves are spread over the 4 SIMDs).  Ended waves do
+  // not take part in s_barrier.
+  // The Viterbi staging also takes the emission log (logcr.h), so it runs on a fourth helper,
+  // wave 4, beside the chain on SIMD 0: measured alone, 3 helpers 259 us, 4 helpers 238 us,
+  // the separate log pass 248 us (B=32, T=2000, N=128); 3 of the 8 virtual waves on wave 4
+  // and 5 on waves 1..3 was slower (262 us).
+  constexpr int NH = (KIND == kVit && C::NW >= 8) ? 4 : 3;  // (NP = 64: a 4-wave workgroup)
   constexpr int HV = (C::NW + NH - 1) / NH;  // virtual staging waves per helper
+  auto vw_of = [&](int w, int h) -> int { return (w - 1) + h * NH; };  // virtual staging wave h of helper w
   constexpr bool FB = KIND != kVit;
   // fused psi (kVitFused): helpers 1..3 also form the psi rows of the block they flush
   constexpr bool FUSE = KIND == kVit && kVitFused<NP>;
@@ -541,9 +754,10 @@ __device__ __forceinline__ void rec_band(const RecArgs& a, float* lds, int b, co
   // blocks (~3 us) to land before it is staged
   float er0[HV][5], er1[HV][5], er2[HV][5];
   if (w > 0 && w <= NH) {
+    if (KIND == kVit) rec_logt_fill<NP>(lds, l);
 #pragma unroll
     for (int h = 0; h < HV; ++h) {
-      const int vw = (w - 1) + h * NH;
+      const int vw = vw_of(w, h);
       if (vw < C::NW) {
         float er[5];
         rec_load<NP, KIND>(a, b, 0, vw, l, er);
@@ -556,182 +770,7 @@ __device__ __forceinline__ void rec_band(const RecArgs& a, float* lds, int b, co
   lds_barrier();
 
   if (w == 0) {
-    // ------------------------------------------------------------------ chain wave
-    // Lane l holds the consecutive states s = NB*l + j (j < NB): a window offset of +-1 is
-    // then another register of the same lane or ONE DPP lane shift (zero-filled at the wave
-    // edge, where the window weight is the neutral element), folded by the compiler into the
-    // add / fma that consumes it.  A wave issues one instruction per ~4 cycles, so the step is
-    // written for instruction count: 16-step blocks fully unrolled (no scalar address math),
-    // the emission read one step ahead, the block's normalisers collected by v_writelane and
-    // stored once per block.
-    constexpr int WW = TW > 0 ? TW : WP;  // window slots per state
-    int lo[NB];
-    float wv[NB][WW], fl[NB];
-#pragma unroll
-    for (int j = 0; j < NB; ++j) {
-      const int s = NB * l + j;
-      lo[j] = KIND == kFbBeta ? d->rlo[s] : d->clo[s];
-#pragma unroll
-      for (int k = 0; k < WW; ++k) {
-        if (TW > 0)
-          wv[j][k] = KIND == kVit ? d->tL[s][k] : (KIND == kFbAlpha ? d->tD[s][k] : d->tR[s][k]);
-        else
-          wv[j][k] = KIND == kVit ? d->cL[s][k] : (KIND == kFbAlpha ? d->cD[s][k] : d->rD[s][k]);
-      }
-      fl[j] = KIND == kVit ? d->rfl[s] : d->afl[s];
-    }
-    const bool uafl = d->uafl != 0;  // one floor for every row: weighted sum = afl0 * plain sum
-    const float afl0 = d->afl[0];
-    auto erow = [&](int rho) { return lds + C::OFF_EMIS + (((rho >> 4) % 3) * 16 + (rho & 15)) * NP + NB * l; };
-    auto ld = [&](const float* p, float(&v)[NB]) {
-      if constexpr (NB == 1) v[0] = p[0];
-      else if constexpr (NB == 2) { const float2 t = *reinterpret_cast<const float2*>(p); v[0] = t.x; v[1] = t.y; }
-      else { const float4 t = *reinterpret_cast<const float4*>(p); v[0] = t.x; v[1] = t.y; v[2] = t.z; v[3] = t.w; }
-    };
-    auto st = [&](float* p, const float(&v)[NB]) {
-      if constexpr (NB == 1) p[0] = v[0];
-      else if constexpr (NB == 2) *reinterpret_cast<float2*>(p) = make_float2(v[0], v[1]);
-      else *reinterpret_cast<float4*>(p) = make_float4(v[0], v[1], v[2], v[3]);
-    };
-    float y[NB];
-    {
-      float e0[NB];
-      ld(erow(0), e0);
-#pragma unroll
-      for (int j = 0; j < NB; ++j) {
-        const int s = NB * l + j;
-        const int ss = s < N ? s : 0;
-        if (KIND == kFbAlpha) y[j] = s < N ? __expf(a.init[ss]) * e0[j] : 0.f;
-        else if (KIND == kFbBeta) y[j] = s < N ? (a.binit ? a.binit[(size_t)b * NP + s] : 1.f) : 0.f;
-        else y[j] = s < N ? a.init[ss] + e0[j] : -INFINITY;
-      }
-    }
-    float* ybuf = lds + C::OFF_PART;  // beta's LDS window source [2][NP] (LDS-window mode)
-    constexpr int EL = KIND == kFbBeta ? 1 : 0;
-    float en[NB];  // the next step's emission (alpha / Viterbi e_q, beta e_{q-1})
-
-    // the value of state s + dd (s = NB*l + j) from register vector v
-    auto at = [&](const float(&v)[NB], int j, int dd) -> float {
-      const int t = j + dd + 4 * NB;
-      const int qq = t / NB - 4, jj = t % NB;
-      const int x = __builtin_bit_cast(int, v[jj]);
-      if (qq == 0) return v[jj];
-      if (qq == -1) return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, x, 0x138, 0xF, 0xF, true));
-      if (qq == 1) return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, x, 0x130, 0xF, 0xF, true));
-      if (qq == -2) {
-        const int t1 = __builtin_amdgcn_update_dpp(0, x, 0x138, 0xF, 0xF, true);
-        return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, t1, 0x138, 0xF, 0xF, true));
-      }
-      const int t1 = __builtin_amdgcn_update_dpp(0, x, 0x130, 0xF, 0xF, true);
-      return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, t1, 0x130, 0xF, 0xF, true));
-    };
-
-    // UA: uniform floor (alpha), a compile-time branch: a runtime one splits every unrolled
-    // step into basic blocks whose joins wait for all outstanding LDS reads
-    auto step = [&](int q, int jj, bool last_in_block, auto UA) {
-      float* row = lds + C::OFF_RING + ((q - 1) & (C::RING - 1)) * NP;
-      st(row + NB * l, y);  // row q-1: flushed by the helpers, window source in LDS mode
-      float eo[NB];
-#pragma unroll
-      for (int j = 0; j < NB; ++j) eo[j] = en[j];
-      if (!last_in_block) ld(erow(q + 1 - EL), en);
-      float acc[NB], src[NB];
-      float cs = 0.f, scale = 1.f;
-      if (KIND == kFbBeta) {  // the product input is y = v * e_{q-1} (hmm.py:113-115)
-        float t = 0.f;
-#pragma unroll
-        for (int j = 0; j < NB; ++j) { src[j] = y[j] * eo[j]; t += src[j]; }
-        if (TW == 0) st(ybuf + ((q - 1) & 1) * NP + NB * l, src);
-        cs = wave_sum_bcast(t);
-#pragma unroll
-        for (int j = 0; j < NB; ++j) acc[j] = fl[j] * cs;
-      } else if (KIND == kFbAlpha) {
-        float t = 0.f;
-#pragma unroll
-        for (int j = 0; j < NB; ++j) { src[j] = y[j]; t += y[j]; }
-        cs = wave_sum_bcast(t);
-        float sw;
-        if constexpr (decltype(UA)::value) {
-          sw = afl0 * cs;
-        } else {
-          float tw = 0.f;
-#pragma unroll
-          for (int j = 0; j < NB; ++j) tw = fmaf(y[j], fl[j], tw);
-          sw = wave_sum_bcast(tw);
-        }
-#pragma unroll
-        for (int j = 0; j < NB; ++j) acc[j] = sw;
-      } else {
-        float g = -INFINITY;
-#pragma unroll
-        for (int j = 0; j < NB; ++j) { src[j] = y[j]; g = fmaxf(g, y[j] + fl[j]); }
-        const float M = wave_max_bcast(g);
-        // fused psi: M_q = max_i fl(delta_{q-1,i} + r_i) is also psi row q's floor maximum
-        if constexpr (FUSE) lds[C::OFF_SC + 64 * ((q - 1) & (C::RING - 1)) + l] = M;
-#pragma unroll
-        for (int j = 0; j < NB; ++j) acc[j] = M;
-      }
-      if (FB) {
-        scale = __builtin_amdgcn_rcpf(cs);
-        lds[C::OFF_SC + 64 * ((q - 1) & (C::RING - 1)) + l] = cs;  // c_{q-1}: one conflict-free store
-      }
-      if constexpr (TW > 0) {
-#pragma unroll
-        for (int k = 0; k < TW; ++k)
-#pragma unroll
-          for (int j = 0; j < NB; ++j) {
-            const float v = at(src, j, TD0 + k);
-            acc[j] = FB ? fmaf(v, wv[j][k], acc[j]) : fmaxf(acc[j], v + wv[j][k]);
-          }
-      } else {
-        const float* wsrc = KIND == kFbBeta ? ybuf + ((q - 1) & 1) * NP : row;
-#pragma unroll
-        for (int j = 0; j < NB; ++j)
-#pragma unroll
-          for (int k = 0; k < WW; ++k) {
-            const float v = wsrc[lo[j] + k];
-            acc[j] = FB ? fmaf(v, wv[j][k], acc[j]) : fmaxf(acc[j], v + wv[j][k]);
-          }
-      }
-#pragma unroll
-      for (int j = 0; j < NB; ++j) {
-        // padded states: the staged emission is 0 (FB) / -inf (Viterbi) and the floors 0
-        if (KIND == kFbAlpha) y[j] = acc[j] * (scale * eo[j]);
-        else if (KIND == kFbBeta) y[j] = acc[j] * scale;
-        else y[j] = acc[j] + eo[j];
-      }
-    };
-
-    auto run_blocks = [&](auto UA) {
-      for (int kb = 0; kb < nblocks; ++kb) {
-        const int q0 = kb * 16 < 1 ? 1 : kb * 16;
-        const int q1 = (kb + 1) * 16 < T ? (kb + 1) * 16 : T;
-        if (q0 < q1) ld(erow(q0 - EL), en);
-        if (q0 == kb * 16 && q1 == kb * 16 + 16) {
-#pragma unroll
-          for (int jj = 0; jj < 16; ++jj) step(kb * 16 + jj, jj, jj == 15, UA);
-        } else {
-          for (int q = q0; q < q1; ++q) step(q, q - kb * 16, q + 1 == q1, UA);
-        }
-        if (!(kAbl & 16384)) lds_barrier();  // B_{kb+1}: block kb+1 staged by the helpers, rows of block kb-1 written
-      }
-    };
-    if constexpr (KIND == kFbAlpha) {
-      if (uafl) run_blocks(std::true_type{});
-      else run_blocks(std::false_type{});
-    } else {
-      run_blocks(std::false_type{});
-    }
-    float* row = lds + C::OFF_RING + ((T - 1) & (C::RING - 1)) * NP;
-    st(row + NB * l, y);
-    if (KIND == kFbAlpha && a.loglik) {
-      float t = 0.f;
-#pragma unroll
-      for (int j = 0; j < NB; ++j) t += y[j];
-      const float cs = wave_sum_bcast(t);
-      if (l == 0) lds[C::OFF_SC + 64 * ((T - 1) & (C::RING - 1))] = cs;
-    }
-    lds_barrier();
+    band_chain<NP, KIND, WP, TD0, TW>(a, lds, b, d);
   } else {
     // ---------------------------------------------------------------- helper waves
     // Fused psi (vit_psi_kernel's banded rule, psi_band_rows in viterbi.hip), on the
@@ -837,7 +876,7 @@ __device__ __forceinline__ void rec_band(const RecArgs& a, float* lds, int b, co
       const int kload = kb + 3 < nblocks ? kb + 3 : nblocks - 1;
 #pragma unroll
       for (int h = 0; h < HV; ++h) {
-        const int vw = (w - 1) + h * NH;
+        const int vw = vw_of(w, h);
         if (vw < C::NW && !(kAbl & 32768)) {
           if (!(kAbl & 64)) {
             rec_stage<NP, KIND>(a, lds, kb + 1, vw, l, ernext[h]);
@@ -872,7 +911,7 @@ __device__ __forceinline__ void rec_band(const RecArgs& a, float* lds, int b, co
     lds_barrier();  // the chain's last row and c_{T-1}
 #pragma unroll
     for (int h = 0; h < HV; ++h) {
-      const int vw = (w - 1) + h * NH;
+      const int vw = vw_of(w, h);
       if (vw < C::NW) {
         if (nblocks >= 2) rec_flush<NP, KIND>(a, lds, b, nblocks - 2, l + 64 * vw, base);
         rec_flush<NP, KIND>(a, lds, b, nblocks - 1, l + 64 * vw, base);

@@ -8,9 +8,10 @@
 //   computing the max only, on the serial-chain skeleton of recur.h (wave w owns input
 //   slice 16w..16w+15, delta_{t-1} broadcast by DPP row_newbcast folded into
 //   v_add_f32_dpp, two candidates per v_max3_f32: 1.5 VALU per cell; per-wave partial maxima
-//   combined through LDS after the step's one barrier).  The max of a set of fp32 values is order-independent and each delta is one fp32
-//   add, so delta is bit-identical to the reference given identical log-emissions.  The
-//   emission log(x + 1e-8) is formed in fp32 and the log taken in fp64, rounded once.
+//   combined through LDS after the step's one barrier).  The max of a set of fp32 values is
+//   order-independent and each delta is one fp32 add, so delta is bit-identical to the
+//   reference given identical log-emissions.  The emission log(x + 1e-8) is formed in fp32
+//   and the log correctly rounded (logcr.h) while the emissions are staged.
 //
 // Kernel 2, vit_psi<NP> (one workgroup per (sequence, 64-step chunk), ~1000 workgroups):
 //   the argmax pointers psi_t[j] = first argmax_i(delta_{t-1}[i] + logP[i,j]) recomputed
@@ -31,27 +32,6 @@
 #include "post.h"
 
 namespace hmm355 {
-
-// log_obs = log(x + 1e-8) (hmm.py:152), fp32 add then fp64 log rounded once (common.h)
-__global__ void __launch_bounds__(256) log_obs_kernel(const float* __restrict__ x, float* __restrict__ y, size_t n,
-                                                      int vec4) {
-  const size_t n4 = vec4 ? n / 4 : 0;
-  const size_t stride = (size_t)gridDim.x * blockDim.x;
-  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += stride) {
-    const float4 v = reinterpret_cast<const float4*>(x)[i];
-    reinterpret_cast<float4*>(y)[i] = make_float4(log_obs_cr(v.x), log_obs_cr(v.y), log_obs_cr(v.z), log_obs_cr(v.w));
-  }
-  for (size_t i = n4 * 4 + (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) y[i] = log_obs_cr(x[i]);
-}
-
-static hipError_t launch_log_obs(const float* x, float* y, size_t n, hipStream_t st) {
-  if (n == 0) return hipSuccess;
-  size_t blocks = (n / 4 + 255) / 256;
-  blocks = blocks < 4096 ? (blocks > 0 ? blocks : 1) : 4096;
-  const int vec4 = ((reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(y)) & 15) == 0;
-  hipLaunchKernelGGL(log_obs_kernel, dim3((unsigned)blocks), dim3(256), 0, st, x, y, n, vec4);
-  return hipGetLastError();
-}
 
 template <int NP>
 __global__ void __launch_bounds__(RC<NP>::NT) vit_fwd_kernel(RecArgs ra) {
@@ -275,8 +255,7 @@ HMM355_API size_t hmm355_viterbi_workspace_bytes(int B, int T, int N) {
   if (B < 0 || T < 1 || N < 1 || N > 256) return 0;
   const size_t NP = pad_states(N);
   const size_t nc = (T + kChunk - 1) / kChunk;
-  return align_up((size_t)B * T * NP, 256) + align_up((size_t)B * nc * NP, 256) + align_up(sizeof(BandDesc), 256) +
-         align_up((size_t)B * T * N * sizeof(float), 256);
+  return align_up((size_t)B * T * NP, 256) + align_up((size_t)B * nc * NP, 256) + align_up(sizeof(BandDesc), 256);
 }
 
 HMM355_API int hmm355_viterbi_plan_f32(const float* obs, int obs_mode, const float* log_P, const float* init,
@@ -298,17 +277,9 @@ HMM355_API int hmm355_viterbi_plan_f32(const float* obs, int obs_mode, const flo
   BandDesc* band = use_band() ? (plan ? static_cast<BandDesc*>(const_cast<void*>(plan))
                                       : reinterpret_cast<BandDesc*>(bandp))
                                : nullptr;
-  hipStream_t sm0 = static_cast<hipStream_t>(stream);
-  if (obs_mode == HMM355_OBS_PROB) {
-    // log(x + 1e-8) once over the whole tensor, full chip (fp64 log, rounded once): the
-    // serial chain then stages plain copies (forming the fp64 logs in the chain's helper
-    // waves instead measured 0.51 ms vs 0.32 ms per call at B=32, T=2000, N=128)
-    float* lo = reinterpret_cast<float*>(bandp + align_up(sizeof(BandDesc), 256));
-    const hipError_t e0 = launch_log_obs(obs, lo, (size_t)B * T * N, sm0);
-    if (e0 != hipSuccess) return (int)e0;
-    obs = lo;
-    obs_mode = HMM355_OBS_LOG;
-  }
+  // OBS_PROB: the chain's staging takes log(x + 1e-8) itself (logcr.h, ~12 fp64 operations
+  // per element on the helper waves), so the emissions are read once and no log_obs tensor
+  // round-trips through HBM
   VitArgs va{obs, log_P, init, log_delta, final_score, states, psi, G, B, T, N, obs_mode, nc, band};
   hipStream_t sm = static_cast<hipStream_t>(stream);
   hipError_t e;

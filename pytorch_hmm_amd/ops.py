@@ -16,6 +16,8 @@ shape-only fake implementations; their only real implementation is the HIP libra
 """
 from typing import Optional, Tuple
 
+import os
+
 import torch
 from torch import Tensor
 
@@ -24,6 +26,7 @@ from . import _native as nat
 OBS_PROB = nat.OBS_PROB
 OBS_LOG = nat.OBS_LOG
 FB_POSTERIOR = nat.FB_POSTERIOR
+FB_PAIR = nat.FB_PAIR
 FB_FORWARD = nat.FB_FORWARD
 FB_BACKWARD = nat.FB_BACKWARD
 
@@ -49,6 +52,12 @@ def make_plan(log_P: Tensor) -> Tensor:
     plan = torch.empty(L.hmm355_plan_bytes(N), dtype=torch.uint8, device=log_P.device)
     with torch.cuda.device(log_P.device):
         nat.check(L.hmm355_plan_f32(nat.ptr(log_P), N, nat.ptr(plan), nat.stream_of(log_P.device)))
+        # banded in both directions: forward_backward then runs both chains of a sequence in
+        # one workgroup (HMM355_FB_PAIR, csrc/fbpair.h).  One synchronous read per plan.
+        banded = L.hmm355_plan_banded(nat.ptr(plan), nat.stream_of(log_P.device))
+    if banded < 0:
+        nat.check(banded)
+    plan._hmm355_banded = banded == 1
     return plan
 
 
@@ -88,6 +97,11 @@ def forward_backward(obs: Tensor, log_P: Tensor, log_p0: Tensor, obs_mode: int,
         return post, fwd, bwd, loglik, lik_ref
     nbytes = L.hmm355_fb_workspace_bytes(B, T, N)
     ws = _workspace(nbytes, dev)
+    if plan is not None and getattr(plan, "_hmm355_banded", False) and os.environ.get("HMM355_PAIR") == "1":
+        # opt-in (csrc/fbpair.h): one workgroup per sequence, no posterior pass.  Measured at
+        # B=32, T=2000, N=128 it is slower than the two-kernel path (0.38 vs 0.24 ms: the helper
+        # waves' row work outlasts the chains), so it is not the default
+        out_mask |= FB_PAIR
     with torch.cuda.device(dev):
         nat.check(L.hmm355_forward_backward_plan_f32(
             nat.ptr(obs), obs_mode, nat.ptr(log_P), nat.ptr(log_p0), nat.ptr(plan), None, B, T, N, out_mask,

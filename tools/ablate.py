@@ -41,9 +41,9 @@ for v in VARIANTS:
     libs[v] = L
 post = torch.empty(B, T, N, device=dev); fwd = torch.empty_like(post); bwd = torch.empty_like(post)
 ll = torch.empty(B, device=dev); lr = torch.empty(B, device=dev)
-ws = torch.empty(libs[0].hmm355_fb_workspace_bytes(B, T, N), dtype=torch.uint8, device=dev)
+ws = torch.empty(max(L.hmm355_fb_workspace_bytes(B, T, N) for L in libs.values()), dtype=torch.uint8, device=dev)
 states = torch.empty(B, T, dtype=torch.int64, device=dev); delta = torch.empty(B, T, N, device=dev); fin = torch.empty(B, device=dev)
-wsv = torch.empty(libs[0].hmm355_viterbi_workspace_bytes(B, T, N), dtype=torch.uint8, device=dev)
+wsv = torch.empty(max(L.hmm355_viterbi_workspace_bytes(B, T, N) for L in libs.values()), dtype=torch.uint8, device=dev)
 st = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
 p = lambda t: ctypes.c_void_p(t.data_ptr())
 def fb(L):
