@@ -133,6 +133,49 @@ def cpu_baseline(B, T, N, budget, P):
 VALU_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md: FP32 vector peak (spec)
 
 
+def kernel_profile(step, steps=3):
+    """{kernel name: (launches, total device ms)} over `steps` extra steps, from torch.profiler
+    (roctracer kernel records on ROCm).  Empty if the profiler yields no device events."""
+    from torch.profiler import ProfilerActivity, profile
+    with profile(activities=[ProfilerActivity.CUDA]) as prof:
+        for _ in range(steps):
+            step()
+        torch.cuda.synchronize()
+    out = {}
+    for e in prof.key_averages():
+        t_us = getattr(e, "self_device_time_total", None)
+        if t_us is None:
+            t_us = getattr(e, "self_cuda_time_total", 0.0)
+        if t_us and t_us > 0 and e.count > 0:
+            out[e.key] = (e.count / steps, t_us / 1e3 / steps)
+    return out
+
+
+def kernel_roofline(kprof, models, frames):
+    """The roofline of the kernel that takes the most device time per step, from its OWN
+    average launch duration and its algorithmic bytes / flops per frame (`models`: name
+    substring -> ("hbm", bytes/frame) | ("valu", flops/frame)); None if it has no model."""
+    if not kprof:
+        return None
+    name, (launches, ms) = max(kprof.items(), key=lambda kv: kv[1][1])
+    for sub, (bound, per_frame) in models.items():
+        if sub in name:
+            avg_ms = ms / launches
+            amount = per_frame * frames
+            if bound == "valu":
+                ach = amount / (avg_ms * 1e-3) / 1e12
+                return {"bound": "valu", "kernel": name, "achieved": ach, "peak": VALU_PEAK_TFLOPS, "unit": "TFLOP/s",
+                        "frac": ach / VALU_PEAK_TFLOPS, "traffic": None, "flops_per_launch": amount,
+                        "avg_launch_ms": avg_ms, "launches_per_step": launches, "share_of_step_device_time":
+                        ms / sum(v[1] for v in kprof.values()), "source": "torch.profiler kernel records"}
+            ach = amount / (avg_ms * 1e-3) / 1e9
+            return {"bound": "hbm", "kernel": name, "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                    "frac": ach / HBM_PEAK_GBS, "traffic": None, "bytes_per_launch": amount, "avg_launch_ms": avg_ms,
+                    "launches_per_step": launches, "share_of_step_device_time": ms / sum(v[1] for v in kprof.values()),
+                    "source": "torch.profiler kernel records"}
+    return {"kernel": name, "avg_launch_ms": ms / launches, "note": "dominant kernel has no algorithmic model"}
+
+
 def layer_workload(args, rank, world, dev):
     """BASELINE configs 1/2/3/5 through the drop-in layers.
     One step = the config's reference call sequence on one synthetic batch (random-init layer
@@ -158,6 +201,7 @@ def layer_workload(args, rank, world, dev):
         desc = {"workload": "HMMLayer(5) train forward-backward + eval Viterbi", "batch_per_gpu": B,
                 "seq_len": T, "num_states": K}
         dom, flops, bytes_ = "hmm_layer_pair", None, (16 * K + 8 * K + 8) * B * T
+        models = {"fb_recur": ("hbm", 16 * K), "vit_fwd": ("hbm", 8 * K), "fb_posterior": ("hbm", 20 * K)}
     elif wl == "c2":
         B, T, K, D = 32, 2000, 64, 80
         layer = ph.GaussianHMMLayer(K, D).to(dev)
@@ -172,6 +216,8 @@ def layer_workload(args, rank, world, dev):
         desc = {"workload": "GaussianHMMLayer(64,80) train forward-backward + eval Viterbi", "batch_per_gpu": B,
                 "seq_len": T, "num_states": K, "feature_dim": D}
         dom, flops, bytes_ = "gaussian_pair", None, (2 * 4 * D + 8 * K + 12 * K) * B * T
+        models = {"gmm_score": ("valu", 4.0 * K * D), "fb_recur": ("hbm", 16 * K), "vit_fwd": ("hbm", 8 * K),
+                  "fb_posterior": ("hbm", 20 * K)}
     elif wl == "c3":
         B, T, S, C, D = 32, 2000, 128, 4, 80
         layer = ph.MixtureGaussianHMMLayer(S, D, num_components=C).to(dev)
@@ -182,6 +228,7 @@ def layer_workload(args, rank, world, dev):
         desc = {"workload": "MixtureGaussianHMMLayer(128,80,num_components=4) forward (emission + Viterbi)",
                 "batch_per_gpu": B, "seq_len": T, "num_states": S, "num_components": C, "feature_dim": D}
         dom, flops, bytes_ = "gmm_score_kernel", 4.0 * S * C * D * B * T, (4 * D + 4 * S) * B * T
+        models = {"gmm_score": ("valu", 4.0 * S * C * D), "vit_fwd": ("hbm", 8 * S)}
     elif wl == "neural":
         # NeuralHMM recursions (neural.py:391-511) at the north-star shape with a transition
         # matrix per (sequence, step): the network outputs log_obs (B,T,N) and
@@ -218,6 +265,7 @@ def layer_workload(args, rank, world, dev):
         # algorithmic bytes per frame: FB reads its step's matrix and emissions, writes
         # posterior/forward/backward; Viterbi reads matrix + emissions, writes delta + state
         dom, flops, bytes_ = "tv_pair", None, (8 * N * N + 24 * N + 8) * B * T
+        models = {"tv_fb": ("hbm", 2 * 4 * N * N + 4 * N), "tv_vit": ("hbm", 4 * N * N + 8 * N)}
     elif wl == "smk":
         # SemiMarkovHMM.viterbi_decode (semi_markov.py:455-570) batched over the C5 shape
         # (the BASELINE C5 text names semi_markov.py): quad scorer + segment Viterbi + backtrace
@@ -231,6 +279,7 @@ def layer_workload(args, rank, world, dev):
         desc = {"workload": "SemiMarkovHMM(64,80,max_duration=40) viterbi_decode (segment Viterbi)",
                 "batch_per_gpu": B, "seq_len": T, "num_states": S, "max_duration": Dm, "feature_dim": D}
         dom, flops, bytes_ = "smk_fwd_kernel", 2.0 * (S * S * Dm + S * S) * B * T, (4 * D + 8) * B * T
+        models = {"smk_fwd": ("valu", 2.0 * (S * S * Dm + S * S)), "smk_quad": ("valu", 3.0 * S * D)}
     elif wl == "stream":
         # StreamingHMMProcessor decode (streaming.py:267-377) for many concurrent streams: one
         # 160-frame chunk (the reference's default chunk_size) per stream, emission net
@@ -256,6 +305,7 @@ def layer_workload(args, rank, world, dev):
         desc = {"workload": "StreamingHMMProcessor chunk decode (emission net + greedy + beam K=8), concurrent streams",
                 "batch_per_gpu": B, "seq_len": T, "num_states": N, "feature_dim": D, "beam_width": K}
         dom, flops, bytes_ = "stream_beam_kernel", None, (4 * D + 8 * N + 16 + 4 * K) * B * T
+        models = {"stream_beam": ("hbm", 4 * N + 8 + 4 * K), "stream_greedy": ("hbm", 4 * N + 8)}
     else:  # c5
         B, T, S, D, Dm = 16, 2000, 64, 80, 40
         layer = ph.HSMMLayer(S, D, max_duration=Dm).to(dev)
@@ -267,6 +317,7 @@ def layer_workload(args, rank, world, dev):
                 "seq_len": T, "num_states": S, "max_duration": Dm, "feature_dim": D}
         # reorganised recursion: per start, S*S*Dmax (max over d') + S*S (candidates) adds/max
         dom, flops, bytes_ = "hsmm_fwd_kernel", 2.0 * (S * S * Dm + S * S) * B * T, (4 * S + 8) * B * T
+        models = {"hsmm_fwd": ("valu", 2.0 * (S * S * Dm + S * S)), "gmm_score": ("valu", 4.0 * S * D)}
 
     with torch.no_grad():
         for _ in range(max(args.warmup, 1)):
@@ -293,7 +344,16 @@ def layer_workload(args, rank, world, dev):
     step_ms = e0.elapsed_time(e1) / args.steps
     frames = desc["batch_per_gpu"] * desc["seq_len"]
     value = frames * world * args.steps / elapsed
-    if flops is not None:
+    kroof = None
+    if os.environ.get("HMM355_BENCH_NO_KPROF") != "1":
+        try:
+            with torch.no_grad():
+                kroof = kernel_roofline(kernel_profile(step), models, frames)
+        except Exception as exc:  # the profiler is a measurement aid, not part of the step
+            kroof = {"note": f"torch.profiler unavailable: {type(exc).__name__}"}
+    if kroof is not None and "frac" in kroof:
+        roof = kroof
+    elif flops is not None:
         achieved = flops / (step_ms * 1e-3) / 1e12
         roof = {"bound": "valu", "kernel": dom, "achieved": achieved, "peak": VALU_PEAK_TFLOPS, "unit": "TFLOP/s",
                 "frac": achieved / VALU_PEAK_TFLOPS, "traffic": None, "flops_per_launch": flops,
@@ -309,6 +369,8 @@ def layer_workload(args, rank, world, dev):
            "data": "synthetic: randn features, random-init layer (seed 0)",
            "config": dict(desc, global_batch=desc["batch_per_gpu"] * world, parallelism=f"batch-sharded x{world}"),
            "roofline": roof}
+    if kroof is not None and roof is not kroof:
+        out["kernel_profile"] = kroof
     if rank == 0 and world == 1 and args.cpu_seconds > 0:
         out["cpu_baseline"] = layer_cpu_baseline(wl, layer, args.cpu_seconds)
         out["cpu_baseline"]["speedup_gpu_over_cpu"] = value / out["cpu_baseline"]["value"]

@@ -8,7 +8,8 @@ mixture_gaussian.py:59-105) so state_dicts load unchanged.  The emission
 gfx950 GMM scorer without the reference's (B,T,S,C,D) temporary; Viterbi (:290-338) runs
 in the recursion kernels with the reference's uniform start lp_0 - log(S) and returns
 max delta_{T-1} as the sequence score.  Covariance 'diag', 'tied' and 'spherical' map
-onto per-dimension log-variances; 'full' (Cholesky, :216-240) is outside the hot path.
+onto per-dimension log-variances; 'full' (Cholesky, :216-240) whitens with W = L^-1 through
+chunked hipBLASLt GEMMs (_full_log_probs) and shares the Viterbi kernel.
 """
 import math
 import warnings
@@ -89,7 +90,49 @@ class MixtureGaussianHMMLayer(nn.Module):
             return self.log_vars.view(1, 1, D).expand(S, C, D)
         if self.covariance_type == "spherical":
             return self.log_vars.unsqueeze(-1).expand(S, C, D)
-        raise NotImplementedError("covariance_type='full' (Cholesky solve) is outside the gfx950 hot path")
+        raise ValueError("covariance_type='full' has no per-dimension variances (see _full_log_probs)")
+
+    def _get_cholesky_factors(self) -> torch.Tensor:
+        """(S,C,D,D) lower-triangular factors, exp on the diagonal (mixture_gaussian.py:271-289)."""
+        S, C, D = self.num_states, self.num_components, self.feature_dim
+        L = torch.zeros(S * C, D, D, device=self.cholesky_params.device, dtype=self.cholesky_params.dtype)
+        ti = torch.tril_indices(D, D, device=L.device)
+        L[:, ti[0], ti[1]] = self.cholesky_params.view(-1, self.cholesky_params.size(-1))
+        di = torch.arange(D, device=L.device)
+        L[:, di, di] = torch.exp(L[:, di, di])
+        return L.view(S, C, D, D)
+
+    # frames per whitening GEMM: keeps the (frames, S*C*D) product near 256 MiB
+    _FULL_CHUNK_BYTES = 256 << 20
+
+    def _full_log_probs(self, observations: torch.Tensor, log_w: torch.Tensor) -> torch.Tensor:
+        """covariance_type='full' (mixture_gaussian.py:216-240, LSE :141-155).  The reference
+        solves L z = x - mu per (frame, state, component) (a (B,T,S,C,D) temporary: 10.5 GB at
+        config 3).  Here W = L^-1 and b = W mu are formed once per call (S*C triangular solves
+        of D x D), and ||W x - b||^2 for every frame is one GEMM over a chunk of frames
+        (hipBLASLt): (frames, D) x (D, S*C*D), squared and summed per (state, component).
+        Same math as the reference's triangular solve; fp32 rounding differs (tests: 1e-4)."""
+        B, T, D = observations.shape
+        S, C = self.num_states, self.num_components
+        L = self._get_cholesky_factors()
+        eye = torch.eye(D, device=L.device, dtype=L.dtype).expand(S, C, D, D)
+        W = torch.linalg.solve_triangular(L, eye, upper=False)                  # (S,C,D,D)
+        bias = (W @ self.means.unsqueeze(-1)).squeeze(-1)                       # (S,C,D)
+        log_det = 2 * torch.sum(torch.log(torch.diagonal(L, dim1=-2, dim2=-1) + self.eps), dim=-1)  # (S,C)
+        Wt = W.reshape(S * C * D, D).t()                                        # (D, S*C*D)
+        bflat = bias.reshape(S * C * D)
+        const = log_det + D * math.log(2 * math.pi)                             # (S,C)
+        x = observations.reshape(B * T, D)
+        rows = max(1, self._FULL_CHUNK_BYTES // (4 * S * C * D))
+        out = []
+        for r0 in range(0, B * T, rows):
+            z = torch.addmm(-bflat, x[r0:r0 + rows], Wt)                        # W x - W mu
+            mahal = z.square().view(-1, S, C, D).sum(-1)                         # (n,S,C)
+            lpc = -0.5 * (mahal + const) + log_w                                 # (n,S,C)
+            m = lpc.max(dim=-1, keepdim=True)[0]
+            m = torch.where(torch.isinf(m), torch.zeros_like(m), m)
+            out.append(self._safe_log(torch.exp(lpc - m).sum(-1)) + m.squeeze(-1))
+        return torch.cat(out, 0).view(B, T, S)
 
     def get_observation_log_probs(self, observations: torch.Tensor) -> torch.Tensor:
         """(B,T,D) -> (B,T,S): log sum_c w_sc N(x; mu_sc, diag exp(log_vars_sc))
@@ -98,6 +141,9 @@ class MixtureGaussianHMMLayer(nn.Module):
         if T > self.max_sequence_length:
             warnings.warn(f"Sequence length {T} exceeds recommended maximum "
                           f"{self.max_sequence_length}. Consider chunked processing.")
+        if self.covariance_type == "full":
+            # torch ops on the device (differentiable by autograd), then the Viterbi kernel
+            return self._full_log_probs(observations, self._safe_log(F.softmax(self.mixture_weights_logits, dim=-1)))
         if needs_grad(observations, *self.parameters()):
             log_w = self._safe_log(F.softmax(self.mixture_weights_logits, dim=-1))
             return GmmLogProb.apply(observations, self.means, self._component_log_vars(), log_w, 1)

@@ -201,6 +201,24 @@ def fx_mixture(name, S, D, C, B, T, seed, x=None):
          states=npf(states), scores=npf(scores), input_sha256=sha(npf(x)))
 
 
+def fx_mixture_full(name, S, D, C, B, T, seed):
+    """MixtureGaussianHMMLayer(covariance_type='full') (mixture_gaussian.py:216-240, 271-289):
+    Cholesky parameters perturbed off the diagonal so the triangular solve is exercised."""
+    torch.manual_seed(seed)
+    m = MixtureGaussianHMMLayer(S, D, num_components=C, covariance_type="full")
+    with torch.no_grad():
+        m.cholesky_params.add_(0.15 * torch.randn_like(m.cholesky_params))
+    x = torch.randn(B, T, D)
+    with torch.no_grad():
+        lp = m.get_observation_log_probs(x)
+        log_T = m._safe_log(m.get_transition_matrix())
+        states, scores = m(x, return_log_probs=True)
+    save(name, x=npf(x), transition_logits=npf(m.transition_logits),
+         mixture_weights_logits=npf(m.mixture_weights_logits), means=npf(m.means),
+         cholesky_params=npf(m.cholesky_params), log_probs=npf(lp), log_T=npf(log_T),
+         states=npf(states), scores=npf(scores), input_sha256=sha(npf(x)))
+
+
 def fx_hsmm(name, S, D, Dmax, B, T, seed):
     """HSMMLayer segment Viterbi (hsmm.py:181-354); the literal 5-deep loop, small sizes only."""
     torch.manual_seed(seed)
@@ -412,6 +430,7 @@ def main():
         ("mixture_s16", lambda: fx_mixture("mixture_s16", 16, 80, 4, 2, 256, 0)),
         ("mixture_s128", lambda: fx_mixture("mixture_s128", 128, 80, 4, 1, 64, 0)),
         ("mixture_single", lambda: fx_mixture("mixture_single", 1, 10, 1, 1, 20, 3)),
+        ("mixture_full", lambda: fx_mixture_full("mixture_full", 6, 7, 3, 2, 40, 11)),
         ("hsmm_s5", lambda: fx_hsmm("hsmm_s5", 5, 30, 20, 2, 30, 0)),
         ("hsmm_s2", lambda: fx_hsmm("hsmm_s2", 2, 3, 2, 1, 4, 1)),
         ("hsmm_s8", lambda: fx_hsmm("hsmm_s8", 8, 20, 10, 1, 40, 2)),

@@ -78,6 +78,32 @@ def test_mixture_layer(name, S, D, C, seed):
     assert none is None and torch.equal(s2, states)
 
 
+def test_mixture_full_covariance():
+    """covariance_type='full' (mixture_gaussian.py:216-240): whitening GEMMs vs the
+    reference's triangular solve (fixture made by the reference; fp32 rounding differs, so the
+    log-probs match to 1e-4 and the Viterbi path is compared on the reference's own log-probs
+    bit-exactly, and end to end)."""
+    g = golden("mixture_full")
+    m = ph.MixtureGaussianHMMLayer(6, 7, num_components=3, covariance_type="full").to(DEV)
+    with torch.no_grad():
+        for k in ("transition_logits", "mixture_weights_logits", "means", "cholesky_params"):
+            getattr(m, k).copy_(t(g[k]))
+    x = t(g["x"])
+    with torch.no_grad():
+        lp = m.get_observation_log_probs(x)
+    np.testing.assert_allclose(lp.cpu().numpy(), g["log_probs"], rtol=1e-4, atol=1e-4)
+    with torch.no_grad():
+        states, scores = m._viterbi_decode(t(g["log_probs"]), t(g["log_T"]))
+    assert np.array_equal(states.cpu().numpy(), g["states"])
+    np.testing.assert_allclose(scores.cpu().numpy(), g["scores"], rtol=2e-6)
+    s2, sc2 = m(x, return_log_probs=True)
+    assert np.array_equal(s2.cpu().numpy(), g["states"])
+    np.testing.assert_allclose(sc2.detach().cpu().numpy(), g["scores"], rtol=1e-4)
+    # trainable: gradients reach the Cholesky parameters through the whitening GEMMs
+    sc2.sum().backward()
+    assert m.cholesky_params.grad is not None and torch.isfinite(m.cholesky_params.grad).all()
+
+
 @pytest.mark.parametrize("name,S,D,Dm,seed", [("hsmm_s5", 5, 30, 20, 0), ("hsmm_s2", 2, 3, 2, 1),
                                               ("hsmm_s8", 8, 20, 10, 2)])
 def test_hsmm_layer(name, S, D, Dm, seed):

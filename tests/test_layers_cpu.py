@@ -99,3 +99,34 @@ def test_no_cpu_fallback():
         with pytest.raises(RuntimeError):
             with torch.no_grad():
                 fn(obs)
+
+
+def test_mixture_full_init_and_cholesky_match_reference():
+    """covariance_type='full': the reference's draws (mixture_gaussian.py:59-105) and its
+    Cholesky reconstruction (:271-289); the whitening form's math (L^-1 x - L^-1 mu) equals the
+    reference's triangular solve on the fixture's parameters (torch-CPU, fp64)."""
+    g = golden("mixture_full")
+    torch.manual_seed(11)
+    m = ph.MixtureGaussianHMMLayer(6, 7, num_components=3, covariance_type="full")
+    base = m.state_dict()
+    diff = g["cholesky_params"] - base["cholesky_params"].numpy()   # the fixture's perturbation only
+    assert eq(base["means"], g["means"]) and eq(base["transition_logits"], g["transition_logits"])
+    assert np.abs(diff).max() < 1.0
+    with torch.no_grad():
+        m.cholesky_params.copy_(torch.from_numpy(g["cholesky_params"]))
+    L = m._get_cholesky_factors().double()
+    x = torch.from_numpy(g["x"]).double()
+    mu = m.means.detach().double()
+    W = torch.linalg.inv(L)
+    z1 = torch.einsum("scij,btj->btsci", W, x) - torch.einsum("scij,scj->sci", W, mu)
+    z2 = torch.linalg.solve_triangular(L[None, None], (x[:, :, None, None, :] - mu[None, None]).unsqueeze(-1),
+                                       upper=False).squeeze(-1)
+    assert torch.allclose(z1, z2, rtol=1e-9, atol=1e-9)
+
+
+def test_hsmm_layer_rejects_sizes_beyond_the_kernel():
+    with pytest.raises(ValueError):
+        ph.HSMMLayer(65, 4)
+    with pytest.raises(ValueError):
+        ph.HSMMLayer(8, 4, max_duration=64)
+    ph.HSMMLayer(64, 4, max_duration=63)   # BASELINE config 5 is S = 64, Dmax = 40
