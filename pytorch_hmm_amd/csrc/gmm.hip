@@ -21,9 +21,9 @@
 //
 // Layout.  gmm_prep (one thread per (p,d)) writes the scales w and offsets -mu*w in fp64,
 // d-major ([d][P]: one coalesced 8-byte load per lane).  gmm_xt converts the frames to fp64
-// in tiles [frame tile][d chunk][64 frames][8 dims], so a frame's 8-dim chunk is one
-// s_load_dwordx16 and every FMA takes its x operand from SGPRs.  gmm_score: a workgroup owns
-// 64 frames x floor(256/C) states, a lane one component.  Per 8-dim chunk the lane holds 16
+// in tiles [frame tile][d chunk][64 frames][8 dims]: a chunk (4 KiB) is staged in LDS by the
+// workgroup and every lane reads a frame's 8 dims as broadcast LDS reads.  gmm_score: a workgroup owns
+// 64 frames x floor(nt/C) states (nt = 64..256 threads, sized to S*C), a lane one component.  Per 8-dim chunk the lane holds 16
 // fp64 parameters in VGPRs and updates the 64 frames' accumulators (two v_fma_f64 per (frame,
 // component, d), no LDS or vector-memory traffic in the inner loop).  The components' LSE
 // over c runs through a 16-frame LDS tile; rows leave as fp32.
@@ -83,7 +83,8 @@ __global__ void __launch_bounds__(kGmmThreads) gmm_score_kernel(const double* __
                                                                int S, int C, int mix_lse) {
   __shared__ double tile[kGmmSub][kGmmThreads];
   const int tid = threadIdx.x;
-  const int spb = kGmmThreads / C;  // states per workgroup
+  const int nt = blockDim.x;        // 64..256: sized to S*C by the host (a lane per component)
+  const int spb = nt / C;           // states per workgroup
   const int s0 = blockIdx.y * spb;
   const int sl = tid / C, c = tid - sl * C;
   const int s = s0 + sl;
@@ -92,24 +93,53 @@ __global__ void __launch_bounds__(kGmmThreads) gmm_score_kernel(const double* __
   const int p = active ? s * C + c : 0;
   const size_t ft = blockIdx.x;
 
+  // The frames' 8-dim chunks go through an LDS double buffer (one coalesced 16-B load per
+  // lane per chunk, prefetched a chunk ahead) and reach the FMAs as broadcast LDS reads.
+  // Taking them as wave-uniform scalar loads instead left one s_load -> s_waitcnt pair per
+  // frame in the inner loop: the scalar-load latency per 16 FMAs (619 us at config 3).
+  constexpr int CH2 = kGmmFrames * kGmmDc / 2;  // double2 per chunk (256)
+  __shared__ double2 xs[2][CH2];
   double q[kGmmFrames];
 #pragma unroll
   for (int f = 0; f < kGmmFrames; ++f) q[f] = 0.0;
-  const double* xtile = xt + ft * (size_t)NDC * kGmmFrames * kGmmDc;
+  const double2* xtile = reinterpret_cast<const double2*>(xt + ft * (size_t)NDC * kGmmFrames * kGmmDc);
+  const int nt0 = blockDim.x;
+  double2 pre[4];
+  auto fetch = [&](int dc) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int i = tid + j * nt0;
+      pre[j] = i < CH2 ? xtile[(size_t)dc * CH2 + i] : make_double2(0.0, 0.0);
+    }
+  };
+  fetch(0);
   for (int dc = 0; dc < NDC; ++dc) {
+    double2* xb = xs[dc & 1];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int i = tid + j * nt0;
+      if (i < CH2) xb[i] = pre[j];
+    }
+    __syncthreads();
+    if (dc + 1 < NDC) fetch(dc + 1);
     double w[kGmmDc], mw[kGmmDc];
 #pragma unroll
     for (int k = 0; k < kGmmDc; ++k) {
       w[k] = pw[(size_t)(dc * kGmmDc + k) * P + p];
       mw[k] = pmw[(size_t)(dc * kGmmDc + k) * P + p];
     }
-    // wave-uniform address: the frames' chunks arrive by scalar loads (SGPR operands)
-    const double* xc = xtile + (size_t)dc * kGmmFrames * kGmmDc;
 #pragma unroll
     for (int f = 0; f < kGmmFrames; ++f) {
+      double xv[kGmmDc];
+#pragma unroll
+      for (int k2 = 0; k2 < kGmmDc / 2; ++k2) {
+        const double2 v = xb[f * (kGmmDc / 2) + k2];  // same address in every lane: broadcast
+        xv[2 * k2] = v.x;
+        xv[2 * k2 + 1] = v.y;
+      }
 #pragma unroll
       for (int k = 0; k < kGmmDc; ++k) {
-        const double z = fma(xc[f * kGmmDc + k], w[k], mw[k]);
+        const double z = fma(xv[k], w[k], mw[k]);
         q[f] = fma(z, z, q[f]);
       }
     }
@@ -121,7 +151,7 @@ __global__ void __launch_bounds__(kGmmThreads) gmm_score_kernel(const double* __
 #pragma unroll
     for (int fi = 0; fi < kGmmSub; ++fi) tile[fi][tid] = -0.5 * (q[f0 + fi] + kp) + lw;
     __syncthreads();
-    for (int pair = tid; pair < kGmmSub * spb; pair += kGmmThreads) {
+    for (int pair = tid; pair < kGmmSub * spb; pair += nt) {
       const int fi = pair / spb, sj = pair - fi * spb;
       const size_t frame = f_begin + f0 + fi;
       const int ss = s0 + sj;
@@ -203,9 +233,12 @@ HMM355_API int hmm355_gmm_diag_logprob_f32(const float* x, const float* means, c
   hipLaunchKernelGGL(gmm_xt_kernel, dim3((unsigned)blocks), dim3(256), 0, st, x, w.xt, nframes, D, NDC, total);
   e = hipGetLastError();
   if (e != hipSuccess) return (int)e;
-  const int spb = kGmmThreads / C;
+  // a lane per (state, component): small S*C (GaussianHMMLayer / HSMMLayer, C = 1) gets
+  // 64- or 128-thread workgroups instead of 256 threads of which most would idle
+  const int nt = P <= 64 ? 64 : (P <= 128 ? 128 : (P <= 192 ? 192 : kGmmThreads));
+  const int spb = nt / C;
   dim3 grid((unsigned)ntiles, (S + spb - 1) / spb);
-  hipLaunchKernelGGL(gmm_score_kernel, grid, dim3(kGmmThreads), 0, st, w.xt, w.pw, w.pmw, w.cst, out, nframes, NDC,
+  hipLaunchKernelGGL(gmm_score_kernel, grid, dim3(nt), 0, st, w.xt, w.pw, w.pmw, w.cst, out, nframes, NDC,
                      S, C, mix_lse);
   e = hipGetLastError();
   return e == hipSuccess ? HMM355_OK : (int)e;
