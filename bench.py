@@ -604,12 +604,13 @@ def main():
     tdesc = {"left_to_right": "left_to_right(0.7)", "ergodic": "ergodic",
              "random": "random dense softmax(randn(N,N))"}[args.transition]
     # roofline of the dominant op, algorithmic bytes per SURVEY.md §8(d)
+    pair = plan is not None and getattr(plan, "_hmm355_banded", False) and ops._use_pair(B, dev)
     if fb_ms >= vit_ms:
         dom, dur_ms, bytes_per_launch = "forward_backward", fb_ms, 16 * N * B * T
-        kernels = "fb_recur_kernel + fb_posterior_kernel"
+        kernels = "fb_pair_kernel" if pair else "fb_recur_kernel + fb_posterior_kernel"
     else:
         dom, dur_ms, bytes_per_launch = "viterbi", vit_ms, (8 * N + 8) * B * T
-        kernels = "log_obs_kernel + vit_fwd_kernel + vit_psi_kernel + vit_backtrace_kernel"
+        kernels = "vit_fwd_kernel + vit_psi_kernel + vit_backtrace_kernel"
     achieved = bytes_per_launch / (dur_ms * 1e-3) / 1e9
     traffic, traffic_src = profiled_traffic(dom, B, T, N, args.transition)
     out = {
@@ -623,7 +624,8 @@ def main():
                    "parallelism": f"batch-sharded x{world}",
                    "streams": 1 if args.serial else 2, "gather": bool(args.gather and world > 1),
                    "hip_graph": graph is not None, "step_pipelining": "per-op streams, no per-step join",
-                   "transition_plan": plan is not None},
+                   "transition_plan": plan is not None,
+                   "fb_kernel": "pair (both chains + outputs in one workgroup)" if pair else "two-kernel"},
         "op_ms": {"forward_backward": fb_ms, "viterbi": vit_ms},
         "roofline": {"bound": "hbm", "kernel": dom, "kernels": kernels, "achieved": achieved,
                      "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,

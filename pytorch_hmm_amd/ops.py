@@ -80,6 +80,24 @@ def plan_info(plan: Optional[Tensor]) -> dict:
     return {"forward": col, "viterbi": col, "backward": name(wr, trw, trd0)}
 
 
+_CUS = {}
+
+
+def _use_pair(B: int, dev) -> bool:
+    """Both chains of a sequence in one workgroup (csrc/fbpair.h, HMM355_FB_PAIR) when the
+    batch is larger than half the CUs: the two-kernel path then needs more CU-owning
+    workgroups (2B) than the chip has and runs in two rounds, while the pair kernel needs B.
+    Measured: B=32 two-kernel 0.24 ms vs pair 0.38 ms; B=256 FB op 0.90 vs 0.51
+    ms.  HMM355_PAIR=1 / 0 forces it on / off."""
+    env = os.environ.get("HMM355_PAIR")
+    if env in ("0", "1"):
+        return env == "1"
+    key = str(dev)
+    if key not in _CUS:
+        _CUS[key] = torch.cuda.get_device_properties(dev).multi_processor_count
+    return B > _CUS[key] // 2
+
+
 @torch.library.custom_op("hmm355::forward_backward", mutates_args=())
 def forward_backward(obs: Tensor, log_P: Tensor, log_p0: Tensor, obs_mode: int,
                      out_mask: int, plan: Optional[Tensor] = None) -> Tuple[Tensor, Tensor, Tensor, Tensor, Tensor]:
@@ -97,10 +115,7 @@ def forward_backward(obs: Tensor, log_P: Tensor, log_p0: Tensor, obs_mode: int,
         return post, fwd, bwd, loglik, lik_ref
     nbytes = L.hmm355_fb_workspace_bytes(B, T, N)
     ws = _workspace(nbytes, dev)
-    if plan is not None and getattr(plan, "_hmm355_banded", False) and os.environ.get("HMM355_PAIR") == "1":
-        # opt-in (csrc/fbpair.h): one workgroup per sequence, no posterior pass.  Measured at
-        # B=32, T=2000, N=128 it is slower than the two-kernel path (0.38 vs 0.24 ms: the helper
-        # waves' row work outlasts the chains), so it is not the default
+    if plan is not None and getattr(plan, "_hmm355_banded", False) and _use_pair(B, dev):
         out_mask |= FB_PAIR
     with torch.cuda.device(dev):
         nat.check(L.hmm355_forward_backward_plan_f32(
