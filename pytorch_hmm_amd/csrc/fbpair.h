@@ -60,7 +60,6 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t buf_rsrc(const void* p, unsign
 }
 template <int K, int AUX>
 __device__ __forceinline__ void buf_store(__amdgpu_buffer_rsrc_t r, int off, const float (&v)[K]) {
-  if ((kAbl & (1 << 24)) && __builtin_amdgcn_readfirstlane(off) == kBufOOB) return;  // (diag: skip dropped rows)
   if constexpr (K == 1) {
     __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v[0]), r, off, 0, AUX);
   } else {
@@ -297,7 +296,7 @@ __global__ void __launch_bounds__(PairL<NP>::NT) fb_pair_kernel(PairArgs p) {
       for (int kk = 0; kk < K; ++kk) {
         x[q][kk] = lx[C::OFF_RING + (rho & (C::RING - 1)) * NP + K * l + kk];
         const float yv = ly[C::OFF_RING + (rhoY & (C::RING - 1)) * NP + K * l + kk];
-        y[q][kk] = (near || (kAbl & (1 << 24))) ? yv : pf[q][kk];  // (diag 1 << 24: no scratch reads used)
+        y[q][kk] = near ? yv : pf[q][kk];
       }
     }
 #pragma unroll
