@@ -524,6 +524,188 @@ __device__ __forceinline__ void rec_run(const RecArgs& a, float* lds, int b) {
   }
 }
 
+// ---------------------------------------------------------------------------------------
+// Dense chain, register-operand form (NP <= 128; round 2).  Same lane layout as rec_run
+// (wave w owns outputs 16w + c, the lane's row r owns inputs 64*blk + 16r + n), but the
+// previous vector is not broadcast by DPP: every lane reads its row's 16 inputs per block
+// from LDS (4 ds_read_b128 at one address per 16-lane row: broadcasts, conflict-free) and
+// the products run as packed fp32 (v_pk_fma_f32, two inputs per instruction; Viterbi
+// v_pk_add_f32 + v_max3).  rec_run's v_fmac_f32_dpp issues at half rate, so its compute
+// phase was ~680 cycles per step on the slower wave of each SIMD (tools/stamps.py); here
+// the same 16K products are 16 packed ops per wave.  The four row groups are summed in
+// registers (permlane32 + permlane16 swaps), so each step writes ONE value per output
+// (lanes 0..15): Y[2][NP] holds the rows, and for beta P[2][NP] its product input v * e.
+template <int NP, int KIND>
+__device__ __forceinline__ void rec_run_bc(const RecArgs& a, float* lds, int b) {
+  using C = RC<NP>;
+  static_assert(NP <= 128, "register-operand dense chain: NP <= 128");
+  constexpr bool FB = KIND != kVit;
+  constexpr int NBK = C::NBLK;
+  typedef float f2 __attribute__((ext_vector_type(2)));
+  const int tid = threadIdx.x;
+  const int w = tid >> 6, l = tid & 63, r = l >> 4, c = l & 15;
+  const int o = 16 * w + c;  // output of this lane
+  const int T = a.T, N = a.N;
+  float* Y = lds + C::OFF_PART;            // [2][NP] rows (alpha u, beta v, Viterbi delta)
+  float* Pv = lds + C::OFF_PART + 2 * NP;  // [2][NP] beta: product input v * e
+
+  // matrix slice as pairs: M2[blk][m] = (Mat[i][o], Mat[i+1][o]) (beta: Mat[o][i]),
+  // i = 64 blk + 16 r + 2 m
+  f2 M2[NBK][8];
+#pragma unroll
+  for (int blk = 0; blk < NBK; ++blk)
+#pragma unroll
+    for (int n = 0; n < 16; ++n) {
+      const int i = 64 * blk + 16 * r + n;
+      const bool ok = i < N && o < N;
+      const size_t idx = ok ? (KIND == kFbBeta ? (size_t)o * N + i : (size_t)i * N + o) : 0;
+      const float v = a.mat[idx];
+      M2[blk][n >> 1][n & 1] = FB ? __expf(ok ? v : -INFINITY) : (ok ? v : -INFINITY);
+    }
+
+  const int nblocks = (T + 15) / 16;
+  float er0[5], er1[5];
+  if (KIND == kVit) rec_logt_fill<NP>(lds, l);
+  rec_load<NP, KIND>(a, b, 0, w, l, er0);
+  rec_stage<NP, KIND>(a, lds, 0, w, l, er0);
+  if (nblocks > 1) rec_load<NP, KIND>(a, b, 1, w, l, er1);
+  lds_barrier();
+
+  auto emis = [&](int rho, int idx) { return lds[C::OFF_EMIS + (((rho >> 4) % 3) * 16 + (rho & 15)) * NP + idx]; };
+  {
+    float v0;
+    const int oo = o < N ? o : 0;
+    if (KIND == kFbAlpha) v0 = o < N ? __expf(a.init[oo]) * emis(0, o) : 0.f;  // alpha_0 = p0 * e_0
+    else if (KIND == kFbBeta) v0 = o < N ? (a.binit ? a.binit[(size_t)b * NP + o] : 1.f) : 0.f;  // beta_{T-1}
+    else v0 = o < N ? a.init[oo] + emis(0, o) : -INFINITY;                      // delta_0 = init + lo_0
+    if (l < 16) {
+      Y[o] = v0;
+      if (KIND == kFbBeta) Pv[o] = v0 * emis(0, o);
+    }
+  }
+  lds_barrier();
+
+  double base = (KIND == kFbBeta && a.bscale) ? (double)a.bscale[b] : 0.0;
+  unsigned long long st_acc[4] = {0, 0, 0, 0}, st_prev = 0, st_t0 = 0, st_steps = 0;
+  long long rt0 = 0;
+  if (kStamp) { st_t0 = stamp(); st_prev = st_t0; rt0 = __builtin_amdgcn_s_memrealtime(); }
+  auto mark = [&](int k) {
+    if (kStamp) { const unsigned long long t = stamp(); st_acc[k] += t - st_prev; st_prev = t; }
+  };
+  auto keep_row = [&](int rho, const float (&y)[NBK]) {
+    if (w == 0) {
+#pragma unroll
+      for (int blk = 0; blk < NBK; ++blk) lds[C::OFF_RING + (rho & (C::RING - 1)) * NP + 64 * blk + l] = y[blk];
+    }
+  };
+
+  auto run_block = [&](int kb, float(&ernext)[5], float(&erfree)[5]) {
+    rec_stage<NP, KIND>(a, lds, kb + 1, w, l, ernext);
+    rec_load<NP, KIND>(a, b, kb + 2 < nblocks ? kb + 2 : nblocks - 1, w, l, erfree);
+    if (kb >= 2) rec_flush<NP, KIND>(a, lds, b, kb - 2, tid, base);
+    const int q0 = kb * 16 < 1 ? 1 : kb * 16;
+    const int q1 = (kb + 1) * 16 < T ? (kb + 1) * 16 : T;
+    for (int q = q0; q < q1; ++q) {
+      const int prv = (q - 1) & 1, cur = q & 1;
+      const float eo = emis(q, o);  // alpha / Viterbi: emission of output o; beta: of v_q -> P
+      if (kStamp) mark(3);
+      const float* src = (KIND == kFbBeta ? Pv : Y) + prv * NP;
+      f2 yin[NBK][8];
+      float yown[NBK], cx = 0.f;
+#pragma unroll
+      for (int blk = 0; blk < NBK; ++blk) {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const float4 v4 = *reinterpret_cast<const float4*>(src + 64 * blk + 16 * r + 4 * k);
+          yin[blk][2 * k] = f2{v4.x, v4.y};
+          yin[blk][2 * k + 1] = f2{v4.z, v4.w};
+        }
+        yown[blk] = Y[prv * NP + 64 * blk + l];
+        if (FB) cx += src[64 * blk + l];  // the normaliser's input (beta: sum of v * e)
+      }
+      if (kStamp) { keep(yown[0]); mark(0); }
+      keep_row(q - 1, yown);
+      float h;
+      float cs = 0.f;
+      if (FB) {
+        f2 acc0 = {0.f, 0.f}, acc1 = {0.f, 0.f};
+#pragma unroll
+        for (int blk = 0; blk < NBK; ++blk)
+#pragma unroll
+          for (int m = 0; m < 8; m += 2) {
+            acc0 = __builtin_elementwise_fma(yin[blk][m], M2[blk][m], acc0);
+            acc1 = __builtin_elementwise_fma(yin[blk][m + 1], M2[blk][m + 1], acc1);
+          }
+        cs = wave_sum_bcast(cx);  // c_{q-1}, beside the products
+        h = (acc0.x + acc0.y) + (acc1.x + acc1.y);
+      } else {
+        float m0 = -INFINITY, m1 = -INFINITY;
+#pragma unroll
+        for (int blk = 0; blk < NBK; ++blk)
+#pragma unroll
+          for (int m = 0; m < 8; m += 2) {
+            const f2 t0 = yin[blk][m] + M2[blk][m];
+            const f2 t1 = yin[blk][m + 1] + M2[blk][m + 1];
+            m0 = fmaxf(m0, fmaxf(t0.x, t0.y));
+            m1 = fmaxf(m1, fmaxf(t1.x, t1.y));
+          }
+        h = fmaxf(m0, m1);
+      }
+      // the four row groups: rows {0,2} / {1,3} (permlane32), then {0,1} (permlane16)
+      float h1 = h;
+      permlane32_swap(h, h1);
+      h = FB ? h + h1 : fmaxf(h, h1);
+      float h2 = h;
+      permlane16_swap(h, h2);
+      h = FB ? h + h2 : fmaxf(h, h2);
+      float val, pval = 0.f;
+      if (FB) {
+        const float scale = __builtin_amdgcn_rcpf(cs);
+        if (tid == 0) lds[C::OFF_SC + 64 * ((q - 1) & (C::RING - 1))] = cs;
+        val = KIND == kFbAlpha ? h * (scale * eo) : h * scale;  // alpha: u_q = z e_q / c;  beta: v_q = z / c
+        if (KIND == kFbBeta) pval = val * eo;
+      } else {
+        val = h + eo;  // delta_q = max(...) + lo_q (exact: monotone)
+      }
+      if (kStamp) { keep(val); mark(1); }
+      if (l < 16) {
+        Y[cur * NP + o] = val;
+        if (KIND == kFbBeta) Pv[cur * NP + o] = pval;
+      }
+      if (kStamp) { mark(2); ++st_steps; }
+      step_barrier();
+    }
+  };
+  for (int k = 0; k < nblocks; k += 2) {
+    run_block(k, er1, er0);
+    if (k + 1 < nblocks) run_block(k + 1, er0, er1);
+  }
+  if (kStamp && (tid & 63) == 0) {
+    const unsigned long long t1 = stamp();
+    const long long rt1 = __builtin_amdgcn_s_memrealtime();
+    unsigned long long* o8 = g_rec_stamps + ((size_t)(blockIdx.x * C::NW + w) % kStampWaves) * 8;
+    o8[0] = st_acc[0]; o8[1] = st_acc[1]; o8[2] = st_acc[2]; o8[3] = st_acc[3];
+    o8[4] = st_steps; o8[5] = t1 - st_t0; o8[6] = t1 - st_t0; o8[7] = (unsigned long long)(rt1 - rt0);
+  }
+  float y[NBK];
+#pragma unroll
+  for (int blk = 0; blk < NBK; ++blk) y[blk] = Y[((T - 1) & 1) * NP + 64 * blk + l];
+  keep_row(T - 1, y);
+  if (KIND == kFbAlpha && a.loglik && w == C::NW - 1) {
+    float ys = y[0];
+#pragma unroll
+    for (int blk = 1; blk < NBK; ++blk) ys += y[blk];
+    const float cs = wave_sum_bcast(ys);
+    if (l == 0) lds[C::OFF_SC + 64 * ((T - 1) & (C::RING - 1))] = cs;  // c_{T-1} (loglik only)
+  }
+  lds_barrier();
+  if (nblocks >= 2) rec_flush<NP, KIND>(a, lds, b, nblocks - 2, tid, base);
+  rec_flush<NP, KIND>(a, lds, b, nblocks - 1, tid, base);
+  if (KIND == kFbAlpha && a.loglik && tid == C::NT - 64) {
+    a.loglik[b] = (float)(base + (double)__logf(lds[C::OFF_SC + 64 * ((T - 1) & (C::RING - 1))]));
+  }
+}
+
 // The banded chain wave (wave 0 of rec_band; waves 0 and 1 of the forward-backward pair
 // kernel, fbpair.h): the whole recursion of one sequence in one wave, one lds_barrier per
 // 16-step block and one after the last row, matching the helpers' barriers.  `lds` is the
@@ -956,7 +1138,11 @@ __device__ __forceinline__ void rec_dispatch(const RecArgs& a, float* lds, int b
     case 16 * 3 - 2 + 2: rec_band<NP, KIND, 2, -2, 3>(a, lds, b, a.band); break;
     case 16 * 3 - 1 + 2: rec_band<NP, KIND, 2, -1, 3>(a, lds, b, a.band); break;
     case 16 * 3 + 0 + 2: rec_band<NP, KIND, 2, 0, 3>(a, lds, b, a.band); break;
-    default: rec_run<NP, KIND>(a, lds, b); break;
+    default:
+      // (diagnostic ablation bit 1 << 24: the DPP-broadcast dense chain for NP <= 128)
+      if constexpr (NP <= 128 && !(kAbl & (1 << 24))) rec_run_bc<NP, KIND>(a, lds, b);
+      else rec_run<NP, KIND>(a, lds, b);
+      break;
   }
 }
 
