@@ -19,8 +19,8 @@
 // dense-matrix path and the path that keeps the scaled rows for the adjoint (autograd.py).
 //
 // Kernel 2, fb_posterior<NP>: one wave per (b,t) row, grid-stride, HBM-bound:
-//   posterior = (u*v)/sum(u*v) (scale-invariant), forward = exp(log u + LA),
-//   backward = exp(log v + LB), and the reference's compute_likelihood value
+//   posterior = (u*v)/sum(u*v) (scale-invariant) and the reference's compute_likelihood value
+//   (forward = exp(log u + LA) and backward = exp(log v + LB) are written by kernel 1's flushes)
 //   logsumexp_j(log(forward_{T-1}[j] + 1e-8)) (hmm.py:206) for t = T-1.
 #include "recur.h"
 #include "post.h"
@@ -176,8 +176,8 @@ HMM355_API int hmm355_forward_backward_plan_f32(const float* obs, int obs_mode, 
     if (e1 != hipSuccess) return (int)e1;
     rmax = w.rmax;
   }
-  RecArgs fa{obs, log_P, log_p0, w.U, w.LA, loglik, B, T, N, obs_mode, NP, band, nullptr, nullptr, nullptr, rmax};
-  RecArgs fb{obs, log_P, log_p0, w.V, w.LB, nullptr, B, T, N, obs_mode, NP, band, binit, bscale, nullptr, rmax};
+  RecArgs fa{obs, log_P, log_p0, w.U, w.LA, loglik, B, T, N, obs_mode, NP, band, nullptr, nullptr, nullptr, rmax, nullptr};
+  RecArgs fb{obs, log_P, log_p0, w.V, w.LB, nullptr, B, T, N, obs_mode, NP, band, binit, bscale, nullptr, rmax, nullptr};
   hipStream_t st0 = static_cast<hipStream_t>(stream);
   if ((out_mask & HMM355_FB_PAIR) && plan && band && NP <= 128 && !log_beta_T &&
       (size_t)T * NP * sizeof(float) < ((size_t)1 << 31)) {
@@ -196,7 +196,12 @@ HMM355_API int hmm355_forward_backward_plan_f32(const float* obs, int obs_mode, 
     if (e == hipSuccess) e = hipGetLastError();
     return e == hipSuccess ? HMM355_OK : (int)e;
   }
-  PostArgs pa{w.U, w.V, w.LA, w.LB, posterior, forward, backward, lik_ref, B, T, N, out_mask};
+  // the chains' flushes write forward / backward (exp(log u + LA), exp(log v + LB)) from their
+  // LDS rows; the posterior pass then reads U / V and writes the posterior only
+  fa.out_exp = (out_mask & HMM355_FB_FORWARD) ? forward : nullptr;
+  fb.out_exp = (out_mask & HMM355_FB_BACKWARD) ? backward : nullptr;
+  PostArgs pa{w.U, w.V, w.LA, w.LB, posterior, forward, backward, lik_ref, B, T, N,
+              out_mask & ~(HMM355_FB_FORWARD | HMM355_FB_BACKWARD)};
   hipError_t e;
   switch (NP) {
     case 64: e = launch_fb<64>(fa, fb, pa, plan == nullptr, st); break;

@@ -185,6 +185,7 @@ struct RecArgs {
   const float* bscale;   // backward only: (B) log-scale of binit
   uint8_t* psi;          // Viterbi, fused banded chain only: (B,T,NP) argmax pointers (kVitFused)
   const float* rmax;     // FB with OBS_LOG: (B,T) row maxima M_t (e_t = exp(lo_t - M_t)), else null
+  float* out_exp;        // FB: (B,T,N) forward (alpha) / backward (beta) output written at flush, or null
 };
 
 // The banded Viterbi chain computes the argmax pointers psi itself (helper waves on the idle
@@ -272,9 +273,45 @@ __device__ __forceinline__ void rec_stage(const RecArgs& a, float* lds, int blk,
   *reinterpret_cast<float4*>(lds + C::OFF_EMIS + ((blk % 3) * 16 + sq) * NP + col) = make_float4(e[0], e[1], e[2], e[3]);
 }
 
-// ---- flush the 16 stored rows of staging block `blk` (+ their log-scales for FB)
+// ---- the Rabiner log-scales of the 16 rows of staging block `blk` (FB):
+// LS_rho = LS_{rho-1} + log c_{rho-1}, a 16-lane inclusive scan with the running base in
+// double.  Every flushing wave computes it (so each knows its rows' log-scales for the exp
+// outputs and keeps its own `base`); the one with write_ls stores LA / LB.  Lane j < 16
+// returns LS of row 16*blk + j.
 template <int NP, int KIND>
-__device__ __forceinline__ void rec_flush(const RecArgs& a, const float* lds, int b, int blk, int tid, double& base) {
+__device__ __forceinline__ float rec_ls_scan(const RecArgs& a, const float* lds, int b, int blk, double& base,
+                                             bool write_ls) {
+  using C = RC<NP>;
+  if constexpr (KIND == kVit) return 0.f;
+  const int lane = threadIdx.x & 63, j = lane & 15;
+  const int rho = blk * 16 + j;
+  const float c = lds[C::OFF_SC + 64 * ((rho - 1) & (C::RING - 1))];  // unconditional (see rec_flush)
+  float x = (lane < 16 && rho >= 1 && rho < a.T) ? __logf(c) : 0.f;
+  if (a.obs_mode == HMM355_OBS_LOG) {
+    // shifted emissions: alpha row rho used M_{tau(rho)}, beta row rho used M_{tau(rho)+1}
+    // (the row staged as rho - 1); beta row 0 (the terminal vector) none
+    const int src = KIND == kFbBeta ? rho - 1 : rho;
+    const float m = lds[C::OFF_M + (src & (C::MRING - 1))];
+    x += (lane < 16 && src >= 0 && rho < a.T) ? m : 0.f;
+  }
+  x += dpp_f<0x111>(x);  // row_shr:1
+  x += dpp_f<0x112>(x);  // row_shr:2
+  x += dpp_f<0x114>(x);  // row_shr:4
+  x += dpp_f<0x118>(x);  // row_shr:8
+  const float lsv = (float)(base + (double)x);
+  if (write_ls && lane < 16 && rho < a.T) a.ls[(size_t)b * a.T + rec_tau<KIND>(rho, a.T)] = lsv;
+  base += (double)__builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, x), 15));
+  return lsv;
+}
+
+// ---- flush the 16 stored rows of staging block `blk`; FB with a.out_exp also writes the
+// reference's output row exp(log x + LS) (forward = exp(log alpha) for alpha, backward for
+// beta, hmm.py:127-128) from the same LDS row, so the posterior pass only forms the posterior.
+// lsv: rec_ls_scan's vector (LS of row j in lane j).  A row whose log-scale is below -110 is
+// exactly 0 (x <= N <= 256 < e^6 and e^-104 is below the smallest fp32 denormal), as the
+// reference's exp underflows: no transcendentals for it.
+template <int NP, int KIND>
+__device__ __forceinline__ void rec_flush(const RecArgs& a, const float* lds, int b, int blk, int tid, float lsv) {
   using C = RC<NP>;
   const int q_base = blk * 16;
   if (a.row_stride == NP) {
@@ -284,7 +321,26 @@ __device__ __forceinline__ void rec_flush(const RecArgs& a, const float* lds, in
     // the LDS read is unconditional (only the store is guarded): a read under the guard
     // ends in an s_waitcnt vmcnt(0) join that drains the helper's emission prefetches
     const float4 v = *reinterpret_cast<const float4*>(lds + C::OFF_RING + (q & (C::RING - 1)) * NP + c4);
-    if (q < a.T) *reinterpret_cast<float4*>(a.rows + ((size_t)b * a.T + rec_tau<KIND>(q, a.T)) * NP + c4) = v;
+    const size_t tr = (size_t)b * a.T + rec_tau<KIND>(q, a.T);
+    if (q < a.T) *reinterpret_cast<float4*>(a.rows + tr * NP + c4) = v;
+    if constexpr (KIND != kVit) {
+      if (a.out_exp) {
+        const float ls = __shfl(lsv, row);
+        const bool live = ls >= -110.f;
+        float ov[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+        for (int k = 0; k < 4; ++k) ov[k] = live ? __expf(__logf(ov[k]) + ls) : 0.f;
+        if (q < a.T) {
+          if (a.N == NP) {
+            *reinterpret_cast<float4*>(a.out_exp + tr * NP + c4) = make_float4(ov[0], ov[1], ov[2], ov[3]);
+          } else {
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+              if (c4 + k < a.N) a.out_exp[tr * a.N + c4 + k] = ov[k];
+          }
+        }
+      }
+    }
   } else {
     for (int idx = tid; idx < 16 * a.N; idx += C::NT) {
       const int row = idx / a.N, col = idx - row * a.N;
@@ -293,26 +349,6 @@ __device__ __forceinline__ void rec_flush(const RecArgs& a, const float* lds, in
         a.rows[((size_t)b * a.T + rec_tau<KIND>(q, a.T)) * a.row_stride + col] =
             lds[C::OFF_RING + (q & (C::RING - 1)) * NP + col];
     }
-  }
-  if (KIND != kVit && (tid >> 6) == C::NW - 1) {
-    // LS_rho = LS_{rho-1} + log c_{rho-1}: 16-lane inclusive scan, running base in double
-    const int j = tid & 15, lane = tid & 63;
-    const int rho = q_base + j;
-    const float c = lds[C::OFF_SC + 64 * ((rho - 1) & (C::RING - 1))];  // unconditional (as above)
-    float x = (lane < 16 && rho >= 1 && rho < a.T) ? __logf(c) : 0.f;
-    if (a.obs_mode == HMM355_OBS_LOG) {
-      // shifted emissions: alpha row rho used M_{tau(rho)}, beta row rho used M_{tau(rho)+1}
-      // (the row staged as rho - 1); beta row 0 (the terminal vector) none
-      const int src = KIND == kFbBeta ? rho - 1 : rho;
-      const float m = lds[C::OFF_M + (src & (C::MRING - 1))];
-      x += (lane < 16 && src >= 0 && rho < a.T) ? m : 0.f;
-    }
-    x += dpp_f<0x111>(x);  // row_shr:1
-    x += dpp_f<0x112>(x);  // row_shr:2
-    x += dpp_f<0x114>(x);  // row_shr:4
-    x += dpp_f<0x118>(x);  // row_shr:8
-    if (lane < 16 && rho < a.T) a.ls[(size_t)b * a.T + rec_tau<KIND>(rho, a.T)] = (float)(base + (double)x);
-    base += (double)__builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, x), 15));
   }
 }
 
@@ -389,7 +425,7 @@ __device__ __forceinline__ void rec_run(const RecArgs& a, float* lds, int b) {
       // last one), as in the banded helpers: exact waitcnt counts
       rec_stage<NP, KIND>(a, lds, kb + 1, w, l, ernext);
       rec_load<NP, KIND>(a, b, kb + 2 < nblocks ? kb + 2 : nblocks - 1, w, l, erfree);
-      if (kb >= 2) rec_flush<NP, KIND>(a, lds, b, kb - 2, tid, base);
+      if (kb >= 2) rec_flush<NP, KIND>(a, lds, b, kb - 2, tid, rec_ls_scan<NP, KIND>(a, lds, b, kb - 2, base, w == C::NW - 1));
     }
     const int q0 = kb * 16 < 1 ? 1 : kb * 16;
     const int q1 = (kb + 1) * 16 < T ? (kb + 1) * 16 : T;
@@ -516,8 +552,9 @@ __device__ __forceinline__ void rec_run(const RecArgs& a, float* lds, int b) {
     if (l == 0) lds[C::OFF_SC + 64 * ((T - 1) & (C::RING - 1))] = cs;  // c_{T-1} (loglik only)
   }
   lds_barrier();
-  if (nblocks >= 2) rec_flush<NP, KIND>(a, lds, b, nblocks - 2, tid, base);
-  rec_flush<NP, KIND>(a, lds, b, nblocks - 1, tid, base);
+  if (nblocks >= 2)
+    rec_flush<NP, KIND>(a, lds, b, nblocks - 2, tid, rec_ls_scan<NP, KIND>(a, lds, b, nblocks - 2, base, w == C::NW - 1));
+  rec_flush<NP, KIND>(a, lds, b, nblocks - 1, tid, rec_ls_scan<NP, KIND>(a, lds, b, nblocks - 1, base, w == C::NW - 1));
   if (KIND == kFbAlpha && a.loglik && tid == C::NT - 64) {
     // loglik = LS_{T-1} + log c_{T-1}; `base` (wave NW-1) now holds LS_{T-1}
     a.loglik[b] = (float)(base + (double)__logf(lds[C::OFF_SC + 64 * ((T - 1) & (C::RING - 1))]));
@@ -602,7 +639,7 @@ __device__ __forceinline__ void rec_run_bc(const RecArgs& a, float* lds, int b) 
   auto run_block = [&](int kb, float(&ernext)[5], float(&erfree)[5]) {
     rec_stage<NP, KIND>(a, lds, kb + 1, w, l, ernext);
     rec_load<NP, KIND>(a, b, kb + 2 < nblocks ? kb + 2 : nblocks - 1, w, l, erfree);
-    if (kb >= 2) rec_flush<NP, KIND>(a, lds, b, kb - 2, tid, base);
+    if (kb >= 2) rec_flush<NP, KIND>(a, lds, b, kb - 2, tid, rec_ls_scan<NP, KIND>(a, lds, b, kb - 2, base, w == C::NW - 1));
     const int q0 = kb * 16 < 1 ? 1 : kb * 16;
     const int q1 = (kb + 1) * 16 < T ? (kb + 1) * 16 : T;
     for (int q = q0; q < q1; ++q) {
@@ -699,8 +736,9 @@ __device__ __forceinline__ void rec_run_bc(const RecArgs& a, float* lds, int b) 
     if (l == 0) lds[C::OFF_SC + 64 * ((T - 1) & (C::RING - 1))] = cs;  // c_{T-1} (loglik only)
   }
   lds_barrier();
-  if (nblocks >= 2) rec_flush<NP, KIND>(a, lds, b, nblocks - 2, tid, base);
-  rec_flush<NP, KIND>(a, lds, b, nblocks - 1, tid, base);
+  if (nblocks >= 2)
+    rec_flush<NP, KIND>(a, lds, b, nblocks - 2, tid, rec_ls_scan<NP, KIND>(a, lds, b, nblocks - 2, base, w == C::NW - 1));
+  rec_flush<NP, KIND>(a, lds, b, nblocks - 1, tid, rec_ls_scan<NP, KIND>(a, lds, b, nblocks - 1, base, w == C::NW - 1));
   if (KIND == kFbAlpha && a.loglik && tid == C::NT - 64) {
     a.loglik[b] = (float)(base + (double)__logf(lds[C::OFF_SC + 64 * ((T - 1) & (C::RING - 1))]));
   }
@@ -1056,6 +1094,9 @@ __device__ __forceinline__ void rec_band(const RecArgs& a, float* lds, int b, co
     // keeps exact counts and never drains the in-flight prefetches or the flush stores.
     auto block_work = [&](int kb, float(&ernext)[HV][5], float(&erfree)[HV][5], auto FULLC) {
       const int kload = kb + 3 < nblocks ? kb + 3 : nblocks - 1;
+      // the block's log-scales once per helper (its own base); helper 1 writes LA / LB
+      float lsv = 0.f;
+      if (!(kAbl & 32) && kb >= 2) lsv = rec_ls_scan<NP, KIND>(a, lds, b, kb - 2, base, w == 1);
 #pragma unroll
       for (int h = 0; h < HV; ++h) {
         const int vw = vw_of(w, h);
@@ -1064,7 +1105,7 @@ __device__ __forceinline__ void rec_band(const RecArgs& a, float* lds, int b, co
             rec_stage<NP, KIND>(a, lds, kb + 1, vw, l, ernext[h]);
             rec_load<NP, KIND, decltype(FULLC)::value>(a, b, kload, vw, l, erfree[h]);
           }
-          if (!(kAbl & 32) && kb >= 2) rec_flush<NP, KIND>(a, lds, b, kb - 2, l + 64 * vw, base);
+          if (!(kAbl & 32) && kb >= 2) rec_flush<NP, KIND>(a, lds, b, kb - 2, l + 64 * vw, lsv);
         }
       }
       if (!(kAbl & 16384)) lds_barrier();
@@ -1091,12 +1132,14 @@ __device__ __forceinline__ void rec_band(const RecArgs& a, float* lds, int b, co
     if (a.N == NP && (reinterpret_cast<uintptr_t>(a.obs) & 15) == 0) helper_loop(std::true_type{});
     else helper_loop(std::false_type{});
     lds_barrier();  // the chain's last row and c_{T-1}
+    const float lsv2 = nblocks >= 2 ? rec_ls_scan<NP, KIND>(a, lds, b, nblocks - 2, base, w == 1) : 0.f;
+    const float lsv1 = rec_ls_scan<NP, KIND>(a, lds, b, nblocks - 1, base, w == 1);
 #pragma unroll
     for (int h = 0; h < HV; ++h) {
       const int vw = vw_of(w, h);
       if (vw < C::NW) {
-        if (nblocks >= 2) rec_flush<NP, KIND>(a, lds, b, nblocks - 2, l + 64 * vw, base);
-        rec_flush<NP, KIND>(a, lds, b, nblocks - 1, l + 64 * vw, base);
+        if (nblocks >= 2) rec_flush<NP, KIND>(a, lds, b, nblocks - 2, l + 64 * vw, lsv2);
+        rec_flush<NP, KIND>(a, lds, b, nblocks - 1, l + 64 * vw, lsv1);
         if (KIND == kFbAlpha && a.loglik && vw == C::NW - 1 && l == 0)
           a.loglik[b] = (float)(base + (double)__logf(lds[C::OFF_SC + 64 * ((T - 1) & (C::RING - 1))]));
       }
