@@ -21,7 +21,7 @@ struct PostArgs {
   unsigned mask;
 };
 
-constexpr int kPostWaves = 16384;  // waves of the posterior pass (grid-stride; 8192 measured 2.4 us slower)
+constexpr int kPostWaves = 32768;  // waves of the posterior pass (grid-stride; 8192 measured 2.4 us slower than 16384)
 
 template <int NP>
 __global__ void __launch_bounds__(256) fb_posterior_kernel(PostArgs a) {
@@ -72,12 +72,23 @@ __global__ void __launch_bounds__(256) fb_posterior_kernel(PostArgs a) {
     s = wave_sum_dpp(s);
     const float is = s > 0.f ? 1.f / s : 0.f;
     const bool last = (row % a.T) == (size_t)(a.T - 1);
+    // forward / backward only where they are stored (fb.hip's chains write them at flush
+    // time) or the reference's likelihood needs the last forward row: the transcendentals
+    // are most of this pass's issue otherwise
     float fw[K], bw[K];
 #pragma unroll
     for (int k = 0; k < K; ++k) {
       p[k] *= is;
-      fw[k] = __expf(__logf(u[k]) + la);
-      bw[k] = __expf(__logf(v[k]) + lb);
+      fw[k] = 0.f;
+      bw[k] = 0.f;
+    }
+    if ((a.mask & HMM355_FB_FORWARD) || (last && a.lik_ref)) {
+#pragma unroll
+      for (int k = 0; k < K; ++k) fw[k] = __expf(__logf(u[k]) + la);
+    }
+    if (a.mask & HMM355_FB_BACKWARD) {
+#pragma unroll
+      for (int k = 0; k < K; ++k) bw[k] = __expf(__logf(v[k]) + lb);
     }
     if (vec) {
       VecK t;
