@@ -491,10 +491,12 @@ def main():
     s_vit = s_fb if args.serial else torch.cuda.Stream(dev)
     ev = {k: [] for k in ("fb", "vit")}
 
-    gather_bufs = None
-    if args.gather and world > 1 and rank == 0:
-        gather_bufs = ([torch.empty(B, T, N, device=dev) for _ in range(world)],
-                       [torch.empty(B, T, dtype=torch.int64, device=dev) for _ in range(world)])
+    gatherer = None
+    if args.gather and world > 1:
+        # receive buffers allocated once (pytorch_hmm_amd.distributed.BatchGather, the code
+        # path tests/test_distributed.py runs over gloo)
+        from pytorch_hmm_amd.distributed import BatchGather
+        gatherer = BatchGather([torch.empty(B, T, N, device=dev), torch.empty(B, T, dtype=torch.int64, device=dev)])
 
     def fb_op(record=False):
         e0 = torch.cuda.Event(enable_timing=True) if record else None
@@ -519,12 +521,7 @@ def main():
         return out
 
     def gather(post, states):
-        if rank == 0:
-            dist.gather(post, gather_bufs[0], dst=0)
-            dist.gather(states, gather_bufs[1], dst=0)
-        else:
-            dist.gather(post, None, dst=0)
-            dist.gather(states, None, dst=0)
+        gatherer(post, states)
 
     # A step is one forward_backward (posterior, forward, backward) and one viterbi_decode of
     # the batch.  The two ops are independent, so each runs on its own stream; consecutive

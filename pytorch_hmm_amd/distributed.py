@@ -6,7 +6,7 @@ recursion.  The only exchange is the optional gather of the per-sequence results
 rank after compute (BASELINE config 4), done with torch.distributed (RCCL on ROCm for
 GPU tensors, gloo for the CPU tests).
 """
-from typing import Optional, Tuple
+from typing import List, Optional, Sequence, Tuple
 
 import torch
 import torch.distributed as dist
@@ -49,3 +49,24 @@ def gather_batch(local: torch.Tensor, B: int, dst: int = 0, group=None) -> Optio
         return torch.cat([b[: e - s] for b, (s, e) in zip(bufs, sizes)], 0)
     dist.gather(padded, None, dst=dst, group=group)
     return None
+
+
+class BatchGather:
+    """The per-step gather of bench.py (BASELINE config 4): every rank holds equal slices
+    (B per rank) of the same outputs; `dst` receives them into buffers allocated once, so a
+    timed step allocates nothing.  One dist.gather per output (RCCL on ROCm: point-to-point
+    transfers into dst over xGMI).  `full(i)` is output i's (world * B, ...) batch on dst."""
+
+    def __init__(self, like: Sequence[torch.Tensor], dst: int = 0, group=None):
+        self.world = dist.get_world_size(group)
+        self.rank = dist.get_rank(group)
+        self.dst, self.group = dst, group
+        self.bufs: List[Optional[List[torch.Tensor]]] = [
+            [torch.empty_like(t) for _ in range(self.world)] if self.rank == dst else None for t in like]
+
+    def __call__(self, *tensors: torch.Tensor) -> None:
+        for t, bufs in zip(tensors, self.bufs):
+            dist.gather(t.contiguous(), bufs, dst=self.dst, group=self.group)
+
+    def full(self, i: int) -> Optional[torch.Tensor]:
+        return torch.cat(self.bufs[i], 0) if self.bufs[i] is not None else None

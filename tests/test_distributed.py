@@ -73,3 +73,48 @@ def test_batch_slice_balanced():
             assert max(sizes) - min(sizes) <= 1
     with pytest.raises(ValueError):
         batch_slice(4, 2, 2)
+
+
+def _bench_gather_worker(rank, world, port, q):
+    """bench.py --gather's step: each rank decodes its own B-sequence batch (weak scaling, global
+    B = B * world), then BatchGather moves posteriors and states to rank 0 into buffers
+    allocated once; repeated steps reuse them."""
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from oracle import hmm_oracle as O
+        from pytorch_hmm_amd.distributed import BatchGather
+        B, T, N = 3, 30, 5
+        lP, lp0 = O.hmm_params(O.left_to_right_matrix(N, 0.7))
+        gatherer = BatchGather([torch.empty(B, T, N), torch.empty(B, T, dtype=torch.int64)])
+        ok = True
+        for step in range(2):
+            g = torch.Generator().manual_seed(1000 * step + rank)
+            obs = torch.softmax(torch.randn(B, T, N, generator=g), -1)
+            states, _ = O.viterbi_decode(obs, lP, lp0)
+            post = O.forward_backward(obs, lP, lp0)[0]
+            gatherer(post, states)
+            if rank == 0:
+                for r in range(world):
+                    gr = torch.Generator().manual_seed(1000 * step + r)
+                    o_r = torch.softmax(torch.randn(B, T, N, generator=gr), -1)
+                    ok &= torch.equal(gatherer.full(0)[r * B:(r + 1) * B], O.forward_backward(o_r, lP, lp0)[0])
+                    ok &= torch.equal(gatherer.full(1)[r * B:(r + 1) * B], O.viterbi_decode(o_r, lP, lp0)[0])
+        q.put(bool(ok) if rank == 0 else gatherer.full(0) is None)
+    finally:
+        dist.destroy_process_group()
+
+
+def test_bench_gather_path():
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_bench_gather_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(120)
+        assert p.exitcode == 0
+    assert all(q.get(timeout=10) for _ in range(world))
