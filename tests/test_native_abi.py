@@ -28,8 +28,9 @@ def header_functions():
 
 
 def header_defines():
-    return dict((m.group(1), int(m.group(2).rstrip("u")))
-                for m in re.finditer(r"#define\s+(HMM355_[A-Z0-9_]+)\s+\(?(-?\d+u?)\)?", open(HEADER).read()))
+    return dict((m.group(1), int(m.group(2).rstrip("u"), 0))
+                for m in re.finditer(r"#define\s+(HMM355_[A-Z0-9_]+)\s+\(?(-?(?:0x[0-9a-fA-F]+|\d+)u?)\)?",
+                                     open(HEADER).read()))
 
 
 def test_exports_match_header(L):
@@ -49,6 +50,7 @@ def test_constants_match_header():
     assert d["HMM355_OBS_PROB"] == nat.OBS_PROB and d["HMM355_OBS_LOG"] == nat.OBS_LOG
     assert (d["HMM355_FB_POSTERIOR"], d["HMM355_FB_FORWARD"], d["HMM355_FB_BACKWARD"]) == \
         (nat.FB_POSTERIOR, nat.FB_FORWARD, nat.FB_BACKWARD)
+    assert d["HMM355_FB_PAIR"] == nat.FB_PAIR == 0x100
     assert d["HMM355_OK"] == 0
 
 
