@@ -223,9 +223,13 @@ class SemiMarkovHMM(nn.Module):
     def _param_tables(self, dev):
         """Device copies of the parameter tables, rebuilt only when a parameter changes
         (storage or in-place version), so repeated decodes pay one host pass per update."""
-        key = (str(dev),) + tuple((p.data_ptr(), p._version) for p in self.parameters())
+        params = tuple(self.parameters())
+        key = (str(dev),) + tuple((p.data_ptr(), p._version) for p in params)
         cached = getattr(self, "_tab_cache", None)
-        if cached is None or cached[0] != key:
+        # identity as well as (address, version): a freed parameter's storage can be reused
+        # by a new tensor at version 0, which must not hit the old tables
+        if (cached is None or cached[0] != key or len(cached[2]) != len(params)
+                or any(a is not b for a, b in zip(cached[2], params))):
             with torch.no_grad():
                 if self.observation_model_type == "gaussian":
                     cs, var = self._gaussian_tables()
@@ -234,7 +238,7 @@ class SemiMarkovHMM(nn.Module):
                     cs = var_t = None
                 tabs = (cs, var_t, self._log_initial().to(dev), self._log_transitions().to(dev),
                         self.duration_model.candidate_table().to(dev))
-            self._tab_cache = cached = (key, tabs)
+            self._tab_cache = cached = (key, tabs, params)
         return cached[1]
 
     def _tables(self, observations):
