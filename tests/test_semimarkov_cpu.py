@@ -152,3 +152,19 @@ def test_duration_model_api_shapes():
     st, du, obs = m.sample(num_states=5, max_length=50)
     assert len(st) == len(du) and obs.shape[1] == 6
     assert sum(int(d) for d in du.tolist()) == obs.shape[0] <= 50  # frames per segment = int(duration)
+
+
+def test_param_table_cache_rebuilds_on_new_parameter():
+    """A replaced parameter must invalidate the device tables even if its storage address and
+    version coincide with the old one (ADVICE: address + version keys alone can alias)."""
+    torch.manual_seed(0)
+    m = SemiMarkovHMM(3, 4, max_duration=6)
+    t0 = m._param_tables(torch.device("cpu"))
+    assert m._param_tables(torch.device("cpu")) is t0  # unchanged parameters: cache hit
+    m.transition_logits = torch.nn.Parameter(torch.randn(3, 3))
+    t1 = m._param_tables(torch.device("cpu"))
+    assert t1 is not t0
+    assert not torch.equal(t1[3], t0[3])
+    with torch.no_grad():
+        m.initial_logits.add_(1.0)  # in-place update bumps the version
+    assert m._param_tables(torch.device("cpu")) is not t1
