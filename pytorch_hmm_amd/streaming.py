@@ -86,6 +86,13 @@ class StreamingHMMProcessor(nn.Module):
         return lt.to(self.transition_logits.device)
 
     # -- async helpers (streaming.py:123-181) -----------------------------------------------
+    # Same public calls and drop semantics as the reference (a full input queue refuses the
+    # chunk, a full result queue drops the result, a failing chunk warns and the worker keeps
+    # serving). The worker blocks on the queue instead of polling it, and stop() wakes it with
+    # a sentinel, so an idle stream costs no CPU and stop() returns as soon as the current
+    # chunk is done.
+    _STOP = object()
+
     def start_async_processing(self):
         if self.is_processing:
             return
@@ -94,22 +101,39 @@ class StreamingHMMProcessor(nn.Module):
         self.processing_thread.start()
 
     def stop_async_processing(self):
+        if not self.is_processing:
+            return
         self.is_processing = False
-        if self.processing_thread:
-            self.processing_thread.join()
+        th, self.processing_thread = self.processing_thread, None
+        if th is not None:
+            while th.is_alive():
+                try:  # the sentinel needs one free slot; retry while the worker drains
+                    self.processing_queue.put(self._STOP, timeout=0.05)
+                    break
+                except queue.Full:
+                    continue
+            th.join()
 
     def _async_processing_loop(self):
-        while self.is_processing:
+        q = self.processing_queue
+        while True:
+            chunk = q.get()
             try:
-                chunk = self.processing_queue.get(timeout=0.1)
-                result = self.process_chunk(chunk)
-                if not self.result_queue.full():
-                    self.result_queue.put(result)
-                self.processing_queue.task_done()
-            except queue.Empty:
-                continue
-            except Exception as e:  # noqa: BLE001 — the reference warns and keeps serving
-                warnings.warn(f"Error in async processing: {e}")
+                if chunk is self._STOP:
+                    return
+                if not self.is_processing:
+                    continue  # chunks queued behind a stop are discarded, as the reference does
+                try:
+                    result = self.process_chunk(chunk)
+                except Exception as e:  # noqa: BLE001 — the reference warns and keeps serving
+                    warnings.warn(f"Error in async processing: {e}")
+                    continue
+                try:
+                    self.result_queue.put_nowait(result)
+                except queue.Full:
+                    pass
+            finally:
+                q.task_done()
 
     def add_audio_chunk_async(self, audio_chunk: torch.Tensor) -> bool:
         try:

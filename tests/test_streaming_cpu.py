@@ -72,3 +72,41 @@ def test_adaptive_latency_controller():
     rec = c.update(200.0, 0)
     assert rec["chunk_size"] == 144 and rec["use_beam_search"] is False and rec["beam_width"] == 3
     assert c.update(200.0, 0) == {}   # cooldown
+
+
+def test_async_worker_queue_semantics():
+    """start/add/get/stop of the async path (reference streaming.py:123-181), with the chunk
+    decode replaced by a host stub so no GPU is needed: results come back in order, a
+    failing chunk warns and the worker keeps serving, stop() joins promptly."""
+    import time as _t
+    import warnings as _w
+    from pytorch_hmm_amd.streaming import StreamingHMMProcessor
+    p = StreamingHMMProcessor(num_states=4, feature_dim=3, chunk_size=4)
+    calls = []
+
+    def fake(chunk):
+        if chunk.numel() == 0:
+            raise RuntimeError("empty")
+        calls.append(int(chunk[0, 0]))
+        return int(chunk[0, 0])
+    p.process_chunk = fake
+    p.start_async_processing()
+    p.start_async_processing()  # idempotent
+    with _w.catch_warnings(record=True) as rec:
+        _w.simplefilter("always")
+        assert p.add_audio_chunk_async(torch.zeros(0, 3))
+        for i in range(3):
+            assert p.add_audio_chunk_async(torch.full((2, 3), float(i)))
+        got, t_end = [], _t.time() + 10
+        while len(got) < 3 and _t.time() < t_end:
+            r = p.get_result_async()
+            if r is None:
+                _t.sleep(0.01)
+            else:
+                got.append(r)
+    assert got == [0, 1, 2] and calls == [0, 1, 2]
+    assert any("Error in async processing" in str(x.message) for x in rec)
+    t0 = _t.time()
+    p.stop_async_processing()
+    assert _t.time() - t0 < 2 and p.processing_thread is None and not p.is_processing
+    assert p.get_result_async() is None
