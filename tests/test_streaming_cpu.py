@@ -47,7 +47,10 @@ def test_greedy_oracle_matches_reference(name):
     for i in range(int(g["config"][6])):
         st, sc = O.c_stream_greedy(g[f"emis{i}"], g["log_T"], prev, log_n)
         assert np.array_equal(st, g[f"greedy_states{i}"])
-        assert np.array_equal(torch.exp(torch.from_numpy(sc)).numpy(), g[f"greedy_conf{i}"])
+        # the score is the oracle's; confidence = exp(score) goes through torch-CPU's exp, whose
+        # vector path differs by an ulp between host ISAs (AVX2 here vs AVX-512 on the GPU box)
+        np.testing.assert_allclose(torch.exp(torch.from_numpy(sc)).numpy(), g[f"greedy_conf{i}"],
+                                   rtol=2.5e-7, atol=0)
         prev = int(st[-1])
 
 
