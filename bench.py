@@ -6,9 +6,10 @@ left-to-right (0.7) transition matrix, B=32 sequences of T=2000 frames per GPU, 
 softmax(randn(B,T,N)) (examples/benchmark.py:160-162), synthetic, resident in HBM.
 One step = HMMPyTorch.forward_backward (posterior, forward, backward) + viterbi_decode
 (states, trellis) over the batch; the two run on two HIP streams of the same GPU.
-N GPUs = one process per GPU (torchrun), B=32 per rank (weak scaling; BASELINE config 4
-is B=256 over 8 GPUs), no collective in the data path; with --gather the posteriors and
-states are gathered to rank 0 over RCCL after every step (config 4's gather).
+N GPUs = one process per GPU (torchrun), B=32 per rank (weak scaling; --strong splits a
+global B=32 over the ranks instead); with world > 1 every step also gathers the posteriors
+and states to rank 0 over RCCL (BASELINE config 4's gather; --no-gather leaves it out and
+the JSON line says so), on a third stream, event-ordered and double-buffered (NsStep).
 
 Prints ONE JSON line on rank 0.  Besides the contract fields it carries
   roofline     for the dominant kernel (HIP events on its stream, over the timed steps)
@@ -39,7 +40,13 @@ def parse():
     p.add_argument("--batch", type=int, default=32, help="sequences per GPU")
     p.add_argument("--T", type=int, default=2000)
     p.add_argument("--N", type=int, default=128)
-    p.add_argument("--gather", action="store_true", help="RCCL gather of posteriors+states to rank 0 each step")
+    p.add_argument("--no-gather", action="store_true",
+                   help="world > 1: leave out the RCCL gather of posteriors + states to rank 0 that every "
+                        "multi-GPU step does by default (BASELINE config 4); the JSON line records it")
+    p.add_argument("--gather", action="store_true", help=argparse.SUPPRESS)   # the default since round 3
+    p.add_argument("--strong", action="store_true",
+                   help="strong scaling: --batch is the GLOBAL batch, split over the ranks "
+                        "(default: weak scaling, --batch sequences per rank)")
     p.add_argument("--serial", action="store_true", help="run FB and Viterbi on one stream")
     p.add_argument("--cpu-seconds", type=float, default=12.0, help="bounded CPU-baseline budget (0 = skip)")
     p.add_argument("--no-graph", action="store_true",
@@ -460,6 +467,95 @@ def layer_cpu_baseline(wl, layer, budget):
             "sample": f"{reps} x ({kind_note}) oracle restatement of the reference op sequence, {elapsed:.1f}s"}
 
 
+class NsStep:
+    """One bench step of the NS workload: `ops["fb"]()` (forward-backward; posterior first in
+    its outputs) and `ops["vit"]()` (Viterbi; states first), each on its own HIP stream and
+    replayed from a captured HIP graph, then — with a `gatherer` (world > 1, BASELINE config 4)
+    — the RCCL gather of posteriors + states to rank 0 on a third stream.
+
+    Ordering is by events only: the gather stream waits for the two ops' end events of the same
+    step; an op stream waits only for the gather that last read the output slot it is about to
+    overwrite.  Outputs are double-buffered (two captured graphs per op, each with its own
+    outputs), so step k's gather overlaps step k+1's compute and no step joins the streams.
+    On a CPU device (the gloo tests) the same control flow runs without streams or graphs:
+    each op is called and its outputs are gathered in program order."""
+
+    def __init__(self, ops_, dev, gatherer=None, use_graph=True, serial=False):
+        self.ops, self.dev, self.gatherer = ops_, dev, gatherer
+        self.cuda = dev.type == "cuda"
+        self.use_graph = use_graph and self.cuda
+        self.nbuf = 2 if gatherer is not None else 1
+        self.names = ("fb", "vit")
+        self.out = [dict() for _ in range(self.nbuf)]
+        self.graph = [dict() for _ in range(self.nbuf)]
+        self.k = 0
+        if self.cuda:
+            s_fb = torch.cuda.Stream(dev)
+            self.stream = {"fb": s_fb, "vit": s_fb if serial else torch.cuda.Stream(dev)}
+            self.s_comm = torch.cuda.Stream(dev) if gatherer is not None else None
+            self.op_end = [{n: torch.cuda.Event() for n in self.names} for _ in range(self.nbuf)]
+            self.read_done = [None] * self.nbuf   # event: the gather that read slot i finished
+        if self.use_graph:
+            self._capture()
+
+    def _capture(self):
+        main_s = torch.cuda.current_stream(self.dev)
+        for n in self.names:   # warm the op (workspace allocation, plan) before capture
+            s_ = self.stream[n]
+            s_.wait_stream(main_s)
+            with torch.cuda.stream(s_):
+                for _ in range(2):
+                    self.ops[n]()
+        torch.cuda.synchronize(self.dev)
+        for slot in range(self.nbuf):
+            for n in self.names:
+                gr = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(gr, stream=self.stream[n]):
+                    self.out[slot][n] = self.ops[n]()
+                self.graph[slot][n] = gr
+        torch.cuda.synchronize(self.dev)
+
+    def outputs(self, slot=None):
+        """(posterior, states) of the most recent step (or of `slot`)."""
+        o = self.out[(self.k - 1) % self.nbuf if slot is None else slot]
+        return o["fb"][0], o["vit"][0]
+
+    def __call__(self):
+        slot = self.k % self.nbuf
+        if not self.cuda:
+            for n in self.names:
+                self.out[slot][n] = self.ops[n]()
+            if self.gatherer is not None:
+                self.gatherer(*self.outputs(slot))
+            self.k += 1
+            return
+        for n in self.names:
+            s_ = self.stream[n]
+            if self.read_done[slot] is not None:
+                s_.wait_event(self.read_done[slot])
+            with torch.cuda.stream(s_):
+                if self.use_graph:
+                    self.graph[slot][n].replay()
+                else:
+                    self.out[slot][n] = self.ops[n]()
+                if self.gatherer is not None:
+                    self.op_end[slot][n].record(s_)
+        if self.gatherer is not None:
+            sc = self.s_comm
+            for n in self.names:
+                sc.wait_event(self.op_end[slot][n])
+            post, states = self.outputs(slot)
+            if not self.use_graph:   # eager outputs come from the op streams' allocator pools
+                post.record_stream(sc)
+                states.record_stream(sc)
+            with torch.cuda.stream(sc):
+                self.gatherer(post, states)
+                ev = torch.cuda.Event()
+                ev.record(sc)
+            self.read_done[slot] = ev
+        self.k += 1
+
+
 def main():
     args = parse()
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
@@ -473,8 +569,17 @@ def main():
     dev = torch.device("cuda", local)
     import pytorch_hmm_amd as ph
     from pytorch_hmm_amd import ops
+    from pytorch_hmm_amd.distributed import BatchGather, batch_slice
 
-    B, T, N = args.batch, args.T, args.N
+    T, N = args.T, args.N
+    if args.strong:
+        # strong scaling: --batch is the global batch, each rank takes a contiguous slice of it
+        if args.batch % world:
+            sys.exit(f"bench.py --strong: global batch {args.batch} is not divisible by {world} ranks")
+        s0, s1 = batch_slice(args.batch, rank, world)
+        B = s1 - s0
+    else:
+        B = args.batch
     if args.transition == "ergodic":
         hmm = ph.HMMPyTorch(ph.create_transition_matrix(N, "ergodic"))
     elif args.transition == "random":
@@ -482,98 +587,40 @@ def main():
         hmm = ph.HMMPyTorch(torch.softmax(torch.randn(N, N, generator=gp), dim=-1))
     else:
         hmm = ph.HMMPyTorch(ph.create_left_to_right_matrix(N, 0.7))
-    g = torch.Generator(device=dev).manual_seed(1234 + rank)
-    obs = torch.softmax(torch.randn(B, T, N, device=dev, generator=g), dim=-1)
+    if args.strong:
+        g = torch.Generator(device=dev).manual_seed(1234)
+        obs = torch.softmax(torch.randn(args.batch, T, N, device=dev, generator=g), dim=-1)[s0:s1].contiguous()
+    else:
+        g = torch.Generator(device=dev).manual_seed(1234 + rank)
+        obs = torch.softmax(torch.randn(B, T, N, device=dev, generator=g), dim=-1)
     lP, lp0, plan = hmm._device_params(dev)   # what HMMPyTorch passes (log_P fixed at init)
     chains = ops.plan_info(plan)               # the chains that actually run (band.h)
 
-    s_fb = torch.cuda.Stream(dev)
-    s_vit = s_fb if args.serial else torch.cuda.Stream(dev)
-    ev = {k: [] for k in ("fb", "vit")}
-
+    gather = world > 1 and not args.no_gather
     gatherer = None
-    if args.gather and world > 1:
-        # receive buffers allocated once (pytorch_hmm_amd.distributed.BatchGather, the code
-        # path tests/test_distributed.py runs over gloo)
-        from pytorch_hmm_amd.distributed import BatchGather
+    if gather:
+        # BASELINE config 4: posteriors + states of every rank gathered to rank 0 each step,
+        # into receive buffers allocated once (pytorch_hmm_amd.distributed.BatchGather; the
+        # same NsStep + BatchGather run over gloo in tests/test_distributed.py)
         gatherer = BatchGather([torch.empty(B, T, N, device=dev), torch.empty(B, T, dtype=torch.int64, device=dev)])
 
-    def fb_op(record=False):
-        e0 = torch.cuda.Event(enable_timing=True) if record else None
-        if record:
-            e0.record()
-        out = ops.forward_backward(obs, lP, lp0, ops.OBS_PROB, 7, plan)
-        if record:
-            e1 = torch.cuda.Event(enable_timing=True)
-            e1.record()
-            ev["fb"].append((e0, e1))
-        return out
-
-    def vit_op(record=False):
-        v0 = torch.cuda.Event(enable_timing=True) if record else None
-        if record:
-            v0.record()
-        out = ops.viterbi(obs, lP, lp0, ops.OBS_PROB, plan)
-        if record:
-            v1 = torch.cuda.Event(enable_timing=True)
-            v1.record()
-            ev["vit"].append((v0, v1))
-        return out
-
-    def gather(post, states):
-        gatherer(post, states)
-
     # A step is one forward_backward (posterior, forward, backward) and one viterbi_decode of
-    # the batch.  The two ops are independent, so each runs on its own stream; consecutive
-    # steps are stream-ordered per op and pipeline across the two streams (no per-step
-    # cross-stream join: it costs two cross-queue signal hops, ~35 us, per step).
-    use_graph = not args.no_graph and not (args.gather and world > 1)
-    graphs = []
-    if use_graph:
-        # each op captured once as a HIP graph on its stream: the timed loop replays them,
-        # so the host launch path (op dispatch, workspace allocation, ctypes) is out of the step
-        main_s = torch.cuda.current_stream(dev)
-        for s_, op in ((s_fb, fb_op), (s_vit, vit_op)):
-            s_.wait_stream(main_s)
-            with torch.cuda.stream(s_):
-                for _ in range(2):
-                    op()
-        torch.cuda.synchronize(dev)
-        for s_, op in ((s_fb, fb_op), (s_vit, vit_op)):
-            gr = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(gr, stream=s_):
-                op()
-            graphs.append((s_, gr))
-        torch.cuda.synchronize(dev)
-    graph = graphs[0][1] if graphs else None
-
-    def run_step():
-        if graphs:
-            for s_, gr in graphs:
-                with torch.cuda.stream(s_):
-                    gr.replay()
-            return
-        with torch.cuda.stream(s_fb):
-            post = fb_op()[0]
-        with torch.cuda.stream(s_vit):
-            states = vit_op()[0]
-        if args.gather and world > 1:
-            main_s = torch.cuda.current_stream(dev)
-            main_s.wait_stream(s_fb)
-            main_s.wait_stream(s_vit)
-            gather(post, states)
-            s_fb.wait_stream(main_s)
-            s_vit.wait_stream(main_s)
+    # the batch (+ the gather when world > 1).  The two ops are independent, so each runs on
+    # its own stream, replayed from a HIP graph; consecutive steps pipeline across the streams
+    # (no per-step join: a cross-stream join costs two cross-queue signal hops, ~35 us).
+    step = NsStep({"fb": lambda: ops.forward_backward(obs, lP, lp0, ops.OBS_PROB, 7, plan),
+                   "vit": lambda: ops.viterbi(obs, lP, lp0, ops.OBS_PROB, plan)},
+                  dev, gatherer, use_graph=not args.no_graph, serial=args.serial)
 
     for _ in range(args.warmup):
-        run_step()
+        step()
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        run_step()
+        step()
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
@@ -583,19 +630,23 @@ def main():
         tt = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         elapsed = float(tt.item())
+
     # per-op launch durations for the roofline: the same ops, eagerly, HIP events on the
     # stream each op's kernels run on
+    ev = {k: [] for k in step.names}
     for _ in range(min(args.steps, 10)):
-        with torch.cuda.stream(s_fb):
-            fb_op(True)
-        with torch.cuda.stream(s_vit):
-            vit_op(True)
+        for n in step.names:
+            with torch.cuda.stream(step.stream[n]):
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record()
+                step.ops[n]()
+                e1.record()
+                ev[n].append((e0, e1))
     torch.cuda.synchronize(dev)
-
     fb_ms = sum(a.elapsed_time(b) for a, b in ev["fb"]) / len(ev["fb"])
     vit_ms = sum(a.elapsed_time(b) for a, b in ev["vit"]) / len(ev["vit"])
-    frames_total = B * T * world * args.steps
-    value = frames_total / elapsed
+    global_b = args.batch if args.strong else B * world
+    value = global_b * T * args.steps / elapsed
     ms_per_step = elapsed / args.steps * 1e3
 
     tdesc = {"left_to_right": "left_to_right(0.7)", "ergodic": "ergodic",
@@ -613,14 +664,17 @@ def main():
     out = {
         "metric": "frames/sec forward-backward+Viterbi, B=32 T=2000 N=128, 1/2/4/8 GPU",
         "value": value, "unit": "frames/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
-        "ms_per_step": ms_per_step, "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+        "ms_per_step": ms_per_step, "higher_is_better": True, "scaling": "strong" if args.strong else "weak",
+        "vs_baseline": None,
         "dtype": "f32", "data": f"synthetic: softmax(randn(B,T,N)) emissions, {tdesc} transitions",
         "config": {"workload": "HMMPyTorch forward_backward + viterbi_decode", "batch_per_gpu": B,
-                   "global_batch": B * world, "seq_len": T, "num_states": N,
+                   "global_batch": global_b, "seq_len": T, "num_states": N,
                    "transition": tdesc, "chain": chains, "world_size_seen": world,
                    "parallelism": f"batch-sharded x{world}",
-                   "streams": 1 if args.serial else 2, "gather": bool(args.gather and world > 1),
-                   "hip_graph": graph is not None, "step_pipelining": "per-op streams, no per-step join",
+                   "streams": 1 if args.serial else 2,
+                   "gather": ("RCCL gather of posteriors + states to rank 0 every step (double-buffered, "
+                              "event-ordered)") if gather else (False if world == 1 else "skipped (--no-gather)"),
+                   "hip_graph": step.use_graph, "step_pipelining": "per-op streams, no per-step join",
                    "transition_plan": plan is not None,
                    "fb_kernel": "pair (both chains + outputs in one workgroup)" if pair else "two-kernel"},
         "op_ms": {"forward_backward": fb_ms, "viterbi": vit_ms},

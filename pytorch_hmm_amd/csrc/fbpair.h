@@ -93,15 +93,15 @@ __device__ __forceinline__ void band_chain_dispatch(const RecArgs& a, float* lds
   }
 }
 
-// Wrong-hint fallback: the dense chains one after the other (rec_run_bc writes U/LA and V/LB),
+// Wrong-hint fallback: the dense chains one after the other (rec_run_rb writes U/LA and V/LB),
 // then the posterior rows of this sequence, one wave per row.
 template <int NP>
 __device__ __forceinline__ void fb_pair_dense(const PairArgs& p, float* lds, int b) {
   constexpr int K = NP / 64;
   if ((int)(threadIdx.x >> 6) >= RC<NP>::NW) return;  // rec_run uses NW waves (ended waves skip barriers)
-  rec_run_bc<NP, kFbAlpha>(p.fa, lds, b);
+  rec_run_rb<NP, kFbAlpha>(p.fa, lds, b);
   __syncthreads();
-  rec_run_bc<NP, kFbBeta>(p.fb, lds, b);
+  rec_run_rb<NP, kFbBeta>(p.fb, lds, b);
   __syncthreads();
   const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
   const int T = p.fa.T, N = p.fa.N;

@@ -96,6 +96,23 @@ HMM355_DPP_OP(dpp_fmac_shr1, "v_fmac_f32_dpp", "wave_shr:1")  // dst += src[l-1]
 HMM355_DPP_OP(dpp_fmac_shl1, "v_fmac_f32_dpp", "wave_shl:1")  // dst += src[l+1] * w (lane 63 keeps)
 #undef HMM355_DPP_OP
 
+// dst = dst (op) src[perm(lane)] as ONE VALU instruction, for the in-row reductions of the
+// register-blocked dense chain (hipcc emits a separate v_mov_b32_dpp plus a zeroed "old"
+// operand for each of these)
+#define HMM355_DPP_RED(name, op, ctrl)                                                        \
+  __device__ __forceinline__ void name(float& dst, float src) {                               \
+    asm("s_nop 1\n\t" op " %0, %1, %0 " ctrl " row_mask:0xf bank_mask:0xf" : "+v"(dst) : "v"(src)); \
+  }
+HMM355_DPP_RED(red_add_mirror, "v_add_f32_dpp", "row_mirror")
+HMM355_DPP_RED(red_add_hmirror, "v_add_f32_dpp", "row_half_mirror")
+HMM355_DPP_RED(red_add_q3210, "v_add_f32_dpp", "quad_perm:[3,2,1,0]")
+HMM355_DPP_RED(red_add_q1032, "v_add_f32_dpp", "quad_perm:[1,0,3,2]")
+HMM355_DPP_RED(red_max_mirror, "v_max_f32_dpp", "row_mirror")
+HMM355_DPP_RED(red_max_hmirror, "v_max_f32_dpp", "row_half_mirror")
+HMM355_DPP_RED(red_max_q3210, "v_max_f32_dpp", "quad_perm:[3,2,1,0]")
+HMM355_DPP_RED(red_max_q1032, "v_max_f32_dpp", "quad_perm:[1,0,3,2]")
+#undef HMM355_DPP_RED
+
 // Window term of slot offset DD in {-1, +1} for state vector v (state 64*blk + lane), weights
 // w: Viterbi -> t = v(s + DD) + w (neutral -inf past the ends); FB -> acc += v(s + DD) * w.
 template <int NB, bool FB, int DD>
@@ -744,6 +761,207 @@ __device__ __forceinline__ void rec_run_bc(const RecArgs& a, float* lds, int b) 
   }
 }
 
+// ---------------------------------------------------------------------------------------
+// Dense chain, register-blocked form (round 3; every NP).  rec_run_bc gives each lane ONE
+// output and 16 inputs per 64-block, so every step moves NP * NP * 4 bytes out of LDS
+// (64 KiB at NP = 128: 64 ds_read_b128 = 256 LDS-array cycles, the largest term of its
+// ~830-cycle step).  Here each lane owns FOUR outputs and NP/16 inputs, so the same products
+// need a quarter of the LDS traffic (2 ds_read_b128 per lane at NP = 128):
+//   * wave w, row r (lane >> 4) owns output group g = 4w + r, i.e. outputs 4g .. 4g+3; lane
+//     c (lane & 15) of the row owns inputs 64m + 4c .. 64m + 4c + 3 (m < NP/64), read as one
+//     float4 per block (the four rows of a wave read the same addresses: broadcasts; the 16
+//     lanes of each ds_read_b128 lane group read 16 distinct 16-B slots: conflict-free);
+//   * the 4 x NP/16 products per lane run as packed fp32 (v_pk_fma_f32 over input pairs;
+//     Viterbi v_pk_add_f32 + v_max3_f32) into four per-output accumulators;
+//   * the 16 lanes of a row are reduced by a reduce-scatter of DPP adds / maxes with no
+//     selects: register slot k of lane c holds output k ^ (c >> 2) (the matrix slice is loaded
+//     in that order), so row_mirror (c <-> 15 - c) pairs slots {0,1} with the partner's {3,2},
+//     row_half_mirror (c <-> c ^ 7) slot 0 with the partner's slot 1, and two quad_perms finish:
+//     5 DPP operations, after which quad c >> 2 holds output 4g + (c >> 2);
+//   * lane (c & 3) == 0 of each quad writes it straight into the row ring (the ring row q is
+//     both the exchange buffer the next step reads and the row that is flushed), so a step is
+//     2 reads, ~25 (FB) / ~37 (Viterbi) VALU operations, 1 write and one s_barrier.
+// Forward-backward keeps Rabiner scaling: c_{q-1} = sum of the step's input vector, formed
+// by each row from its 16 lanes' partial sums (4 more DPP adds beside the products, the same
+// bits in every row).  Beta's product input v * e sits in Pv[2][NP] (OFF_PART).
+template <int NP, int KIND>
+__device__ __forceinline__ void rec_run_rb(const RecArgs& a, float* lds, int b) {
+  using C = RC<NP>;
+  constexpr bool FB = KIND != kVit;
+  constexpr int NM = NP / 64;  // float4 input blocks per lane
+  typedef float f2 __attribute__((ext_vector_type(2)));
+  const int tid = threadIdx.x;
+  const int w = tid >> 6, l = tid & 63, r = l >> 4, c = l & 15;
+  const int g = 4 * w + r;      // output group
+  const int x = c >> 2;         // register slot k holds output 4g + (k ^ x)
+  const int o = 4 * g + x;      // the output this lane's quad finishes
+  const int T = a.T, N = a.N;
+  float* ring = lds + C::OFF_RING;
+  float* Pv = lds + C::OFF_PART;  // [2][NP] beta: product input v * e
+
+  // matrix slice: Mk[k][m][p] = (Mat[i][ok], Mat[i+1][ok]) for inputs i = 64m + 4c + 2p,
+  // output ok = 4g + (k ^ x); beta takes Mat[ok][i]; FB stores exp(log P)
+  f2 Mk[4][NM][2];
+#pragma unroll
+  for (int k = 0; k < 4; ++k)
+#pragma unroll
+    for (int m = 0; m < NM; ++m)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int i = 64 * m + 4 * c + e, ok = 4 * g + (k ^ x);
+        const bool in = i < N && ok < N;
+        const size_t idx = in ? (KIND == kFbBeta ? (size_t)ok * N + i : (size_t)i * N + ok) : 0;
+        const float v = a.mat[idx];
+        Mk[k][m][e >> 1][e & 1] = FB ? __expf(in ? v : -INFINITY) : (in ? v : -INFINITY);
+      }
+
+  const int nblocks = (T + 15) / 16;
+  float er0[5], er1[5];
+  if (KIND == kVit) rec_logt_fill<NP>(lds, l);
+  rec_load<NP, KIND>(a, b, 0, w, l, er0);
+  rec_stage<NP, KIND>(a, lds, 0, w, l, er0);
+  if (nblocks > 1) rec_load<NP, KIND>(a, b, 1, w, l, er1);
+  lds_barrier();
+
+  auto emis = [&](int rho, int idx) { return lds[C::OFF_EMIS + (((rho >> 4) % 3) * 16 + (rho & 15)) * NP + idx]; };
+  const bool writer = (c & 3) == 0;
+  {
+    float v0;
+    const int oo = o < N ? o : 0;
+    if (KIND == kFbAlpha) v0 = o < N ? __expf(a.init[oo]) * emis(0, o) : 0.f;  // alpha_0 = p0 * e_0
+    else if (KIND == kFbBeta) v0 = o < N ? (a.binit ? a.binit[(size_t)b * NP + o] : 1.f) : 0.f;  // beta_{T-1}
+    else v0 = o < N ? a.init[oo] + emis(0, o) : -INFINITY;                      // delta_0 = init + lo_0
+    if (writer) {
+      ring[o] = v0;
+      if (KIND == kFbBeta) Pv[o] = v0 * emis(0, o);
+    }
+  }
+  lds_barrier();
+
+  double base = (KIND == kFbBeta && a.bscale) ? (double)a.bscale[b] : 0.0;
+  unsigned long long st_acc[4] = {0, 0, 0, 0}, st_prev = 0, st_t0 = 0, st_steps = 0;
+  long long rt0 = 0;
+  if (kStamp) { st_t0 = stamp(); st_prev = st_t0; rt0 = __builtin_amdgcn_s_memrealtime(); }
+  auto mark = [&](int k) {
+    if (kStamp) { const unsigned long long t = stamp(); st_acc[k] += t - st_prev; st_prev = t; }
+  };
+
+  auto run_block = [&](int kb, float(&ernext)[5], float(&erfree)[5]) {
+    rec_stage<NP, KIND>(a, lds, kb + 1, w, l, ernext);
+    rec_load<NP, KIND>(a, b, kb + 2 < nblocks ? kb + 2 : nblocks - 1, w, l, erfree);
+    if (kb >= 2) rec_flush<NP, KIND>(a, lds, b, kb - 2, tid, rec_ls_scan<NP, KIND>(a, lds, b, kb - 2, base, w == C::NW - 1));
+    const int q0 = kb * 16 < 1 ? 1 : kb * 16;
+    const int q1 = (kb + 1) * 16 < T ? (kb + 1) * 16 : T;
+    for (int q = q0; q < q1; ++q) {
+      if (kStamp) mark(3);
+      const float* src = KIND == kFbBeta ? Pv + ((q - 1) & 1) * NP : ring + ((q - 1) & (C::RING - 1)) * NP;
+      // alpha / Viterbi: emission of output o; beta: of v_q -> P.  Read first and pinned below:
+      // used only by the writer lanes, it would otherwise sink behind the reduction into their
+      // branch and put an LDS round trip on the chain
+      float eo = emis(q, o);
+      f2 yin[NM][2];
+#pragma unroll
+      for (int m = 0; m < NM; ++m) {
+        const float4 v4 = *reinterpret_cast<const float4*>(src + 64 * m + 4 * c);
+        yin[m][0] = f2{v4.x, v4.y};
+        yin[m][1] = f2{v4.z, v4.w};
+      }
+      keep(eo);
+      if (kStamp) { keep(yin[0][0]); mark(0); }
+      float s0, s1, s2, s3;
+      float cs = 0.f;
+      if (FB) {
+        f2 acc[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) acc[k] = f2{0.f, 0.f};
+        f2 ysum = f2{0.f, 0.f};
+#pragma unroll
+        for (int m = 0; m < NM; ++m)
+#pragma unroll
+          for (int p = 0; p < 2; ++p) {
+#pragma unroll
+            for (int k = 0; k < 4; ++k) acc[k] = __builtin_elementwise_fma(yin[m][p], Mk[k][m][p], acc[k]);
+            ysum += yin[m][p];
+          }
+        // c_{q-1}: the row's 16 lanes hold all NP inputs; an all-reduce of their sums (every
+        // lane, every row and every wave ends with the same bits)
+        float cx = ysum.x + ysum.y;
+        s0 = acc[0].x + acc[0].y; s1 = acc[1].x + acc[1].y;
+        s2 = acc[2].x + acc[2].y; s3 = acc[3].x + acc[3].y;
+        // the two reductions interleaved (issue is in order within a wave)
+        red_add_mirror(cx, cx);
+        red_add_mirror(s0, s3);
+        red_add_mirror(s1, s2);
+        red_add_hmirror(cx, cx);
+        red_add_hmirror(s0, s1);
+        red_add_q3210(cx, cx);
+        red_add_q3210(s0, s0);
+        red_add_q1032(cx, cx);
+        red_add_q1032(s0, s0);
+        cs = cx;
+      } else {
+        float mx[4] = {-INFINITY, -INFINITY, -INFINITY, -INFINITY};
+#pragma unroll
+        for (int m = 0; m < NM; ++m)
+#pragma unroll
+          for (int p = 0; p < 2; ++p)
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+              const f2 t = yin[m][p] + Mk[k][m][p];
+              mx[k] = fmaxf(mx[k], fmaxf(t.x, t.y));
+            }
+        s0 = mx[0]; s1 = mx[1]; s2 = mx[2]; s3 = mx[3];
+        red_max_mirror(s0, s3);
+        red_max_mirror(s1, s2);
+        red_max_hmirror(s0, s1);
+        red_max_q3210(s0, s0);
+        red_max_q1032(s0, s0);
+      }
+      if (kStamp) { keep(s0); mark(1); }
+      float val, pval = 0.f;
+      if (FB) {
+        const float scale = __builtin_amdgcn_rcpf(cs);
+        if (tid == 0) lds[C::OFF_SC + 64 * ((q - 1) & (C::RING - 1))] = cs;
+        val = KIND == kFbAlpha ? s0 * (scale * eo) : s0 * scale;  // alpha: u_q = z e_q / c;  beta: v_q = z / c
+        if (KIND == kFbBeta) pval = val * eo;
+      } else {
+        val = s0 + eo;  // delta_q = max(...) + lo_q (exact: monotone)
+      }
+      if (writer) {
+        ring[(q & (C::RING - 1)) * NP + o] = val;
+        if (KIND == kFbBeta) Pv[(q & 1) * NP + o] = pval;
+      }
+      if (kStamp) { mark(2); ++st_steps; }
+      step_barrier();
+    }
+  };
+  for (int k = 0; k < nblocks; k += 2) {
+    run_block(k, er1, er0);
+    if (k + 1 < nblocks) run_block(k + 1, er0, er1);
+  }
+  if (kStamp && (tid & 63) == 0) {
+    const unsigned long long t1 = stamp();
+    const long long rt1 = __builtin_amdgcn_s_memrealtime();
+    unsigned long long* o8 = g_rec_stamps + ((size_t)(blockIdx.x * C::NW + w) % kStampWaves) * 8;
+    o8[0] = st_acc[0]; o8[1] = st_acc[1]; o8[2] = st_acc[2]; o8[3] = st_acc[3];
+    o8[4] = st_steps; o8[5] = t1 - st_t0; o8[6] = t1 - st_t0; o8[7] = (unsigned long long)(rt1 - rt0);
+  }
+  if (KIND == kFbAlpha && a.loglik && w == C::NW - 1) {
+    float ys = 0.f;
+#pragma unroll
+    for (int m = 0; m < NM; ++m) ys += ring[((T - 1) & (C::RING - 1)) * NP + 64 * m + l];
+    const float cs = wave_sum_bcast(ys);
+    if (l == 0) lds[C::OFF_SC + 64 * ((T - 1) & (C::RING - 1))] = cs;  // c_{T-1} (loglik only)
+  }
+  lds_barrier();
+  if (nblocks >= 2)
+    rec_flush<NP, KIND>(a, lds, b, nblocks - 2, tid, rec_ls_scan<NP, KIND>(a, lds, b, nblocks - 2, base, w == C::NW - 1));
+  rec_flush<NP, KIND>(a, lds, b, nblocks - 1, tid, rec_ls_scan<NP, KIND>(a, lds, b, nblocks - 1, base, w == C::NW - 1));
+  if (KIND == kFbAlpha && a.loglik && tid == C::NT - 64) {
+    a.loglik[b] = (float)(base + (double)__logf(lds[C::OFF_SC + 64 * ((T - 1) & (C::RING - 1))]));
+  }
+}
+
 // The banded chain wave (wave 0 of rec_band; waves 0 and 1 of the forward-backward pair
 // kernel, fbpair.h): the whole recursion of one sequence in one wave, one lds_barrier per
 // 16-step block and one after the last row, matching the helpers' barriers.  `lds` is the
@@ -1182,8 +1400,10 @@ __device__ __forceinline__ void rec_dispatch(const RecArgs& a, float* lds, int b
     case 16 * 3 - 1 + 2: rec_band<NP, KIND, 2, -1, 3>(a, lds, b, a.band); break;
     case 16 * 3 + 0 + 2: rec_band<NP, KIND, 2, 0, 3>(a, lds, b, a.band); break;
     default:
-      // (diagnostic ablation bit 1 << 24: the DPP-broadcast dense chain for NP <= 128)
-      if constexpr (NP <= 128 && !(kAbl & (1 << 24))) rec_run_bc<NP, KIND>(a, lds, b);
+      // (diagnostic ablation bits: 1 << 25 the round-2 register-operand chain (NP <= 128),
+      // 1 << 24 the DPP-broadcast chain)
+      if constexpr (!(kAbl & (3 << 24))) rec_run_rb<NP, KIND>(a, lds, b);
+      else if constexpr (NP <= 128 && !(kAbl & (1 << 24))) rec_run_bc<NP, KIND>(a, lds, b);
       else rec_run<NP, KIND>(a, lds, b);
       break;
   }

@@ -414,6 +414,40 @@ def fx_fullsize_mixture():
          lp_rows=npf(lp[:, :4]), lp_sha256=sha(npf(lp)), input_sha256=sha(npf(x)))
 
 
+def fx_fullsize_gaussian():
+    """BASELINE config 2 at full size: GaussianHMMLayer(64, 80), seed-0 init, B=32, T=2000
+    (hmm_layer.py:220-359), machine-independent x in [-2, 2).  At D = 80 every Gaussian
+    density underflows in exp (hmm_layer.py:325-340), so the HMM sees constant emissions
+    exp(lp) = 0 -> log(0 + 1e-8) everywhere: the Viterbi recursion is
+    2000 steps of first-index ties (hmm.py:167, :174) on the 64-state chain.  Same call
+    order as fx_gaussian: train FB (call 1), eval Viterbi (call 2), compute_loss (call 3)."""
+    B, T, K, D = 32, 2000, 64, 80
+    x = torch.from_numpy(uniform_obs(11, (B, T, D), -2.0, 2.0))
+    torch.manual_seed(0)
+    layer = GaussianHMMLayer(K, D)
+    with torch.no_grad():
+        t0 = time.time()
+        lp = layer._compute_gaussian_log_probs(x)
+        probs = torch.exp(lp)
+        layer.train()
+        post = layer(x)                                              # call 1 (FB)
+        layer.eval()
+        onehot, states = layer.hmm_layer(probs, return_alignment=True)   # call 2 (Viterbi)
+        loss = layer.compute_loss(x)                                 # call 3
+        print(f"    C2 reference: {time.time()-t0:.2f}s, max lp {float(lp.max()):.1f}, "
+              f"nonzero probs {int((probs > 0).sum())}")
+    rows = np.arange(0, T, 20)
+    post_np, st_np = npf(post), npf(states)
+    save("fullsize_gaussian", shape=np.array([B, T, K, D]), x_seed=np.int64(11),
+         means=npf(layer.means), log_scales=npf(layer.log_scales),
+         logits=npf(layer.hmm_layer.log_transition_logits),
+         init_logits=npf(layer.hmm_layer.log_initial_logits),
+         lp_rows=npf(lp[:, :4]), lp_max=np.float32(lp.max()), probs_nonzero=np.int64((probs > 0).sum()),
+         states=st_np.astype(np.uint8), post_rows=rows, posterior_rows=post_np[:, rows],
+         posterior_seq_equal=np.bool_(bool((post_np == post_np[:1]).all())),
+         loss=npf(loss), input_sha256=sha(npf(x)))
+
+
 def main():
     only = set(sys.argv[1:])
     jobs = [
@@ -453,6 +487,7 @@ def main():
         ("contextual_small", lambda: fx_contextual("contextual_small", 6, 10, 50, 32, 8, 2, 15, 6)),
         ("fullsize_ns", fx_fullsize_ns),
         ("fullsize_mixture", fx_fullsize_mixture),
+        ("fullsize_gaussian", fx_fullsize_gaussian),
     ]
     for name, fn in jobs:
         if only and name not in only:

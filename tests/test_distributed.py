@@ -76,32 +76,45 @@ def test_batch_slice_balanced():
 
 
 def _bench_gather_worker(rank, world, port, q):
-    """bench.py --gather's step: each rank decodes its own B-sequence batch (weak scaling, global
-    B = B * world), then BatchGather moves posteriors and states to rank 0 into buffers
-    allocated once; repeated steps reuse them."""
+    """bench.py's own step object (bench.NsStep) with stub ops on the CPU: each step, each
+    rank's "forward-backward" and "Viterbi" stubs produce a fresh (B,T,N) posterior and (B,T)
+    states batch, and the step's gather (pytorch_hmm_amd.distributed.BatchGather, receive
+    buffers allocated once) moves them to rank 0; the output slots alternate (double
+    buffering), and repeated steps reuse the same receive buffers."""
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
-        from oracle import hmm_oracle as O
+        import bench
         from pytorch_hmm_amd.distributed import BatchGather
         B, T, N = 3, 30, 5
-        lP, lp0 = O.hmm_params(O.left_to_right_matrix(N, 0.7))
+        calls = {"fb": 0, "vit": 0}
+
+        def stub(kind, r, k):
+            g = torch.Generator().manual_seed(1000 * k + 10 * r + (kind == "vit"))
+            if kind == "fb":
+                return (torch.softmax(torch.randn(B, T, N, generator=g), -1), None)
+            return (torch.randint(0, N, (B, T), generator=g), None)
+
+        def op(kind):
+            def f():
+                calls[kind] += 1
+                return stub(kind, rank, calls[kind])
+            return f
         gatherer = BatchGather([torch.empty(B, T, N), torch.empty(B, T, dtype=torch.int64)])
-        ok = True
-        for step in range(2):
-            g = torch.Generator().manual_seed(1000 * step + rank)
-            obs = torch.softmax(torch.randn(B, T, N, generator=g), -1)
-            states, _ = O.viterbi_decode(obs, lP, lp0)
-            post = O.forward_backward(obs, lP, lp0)[0]
-            gatherer(post, states)
+        step = bench.NsStep({"fb": op("fb"), "vit": op("vit")}, torch.device("cpu"), gatherer)
+        ok = step.nbuf == 2 and not step.use_graph
+        bufs = [id(b) for b in gatherer.bufs[0]] if rank == 0 else None
+        for k in range(1, 4):
+            step()
+            post, states = step.outputs()
+            ok &= torch.equal(post, stub("fb", rank, k)[0]) and torch.equal(states, stub("vit", rank, k)[0])
             if rank == 0:
+                ok &= [id(b) for b in gatherer.bufs[0]] == bufs
                 for r in range(world):
-                    gr = torch.Generator().manual_seed(1000 * step + r)
-                    o_r = torch.softmax(torch.randn(B, T, N, generator=gr), -1)
-                    ok &= torch.equal(gatherer.full(0)[r * B:(r + 1) * B], O.forward_backward(o_r, lP, lp0)[0])
-                    ok &= torch.equal(gatherer.full(1)[r * B:(r + 1) * B], O.viterbi_decode(o_r, lP, lp0)[0])
-        q.put(bool(ok) if rank == 0 else gatherer.full(0) is None)
+                    ok &= torch.equal(gatherer.full(0)[r * B:(r + 1) * B], stub("fb", r, k)[0])
+                    ok &= torch.equal(gatherer.full(1)[r * B:(r + 1) * B], stub("vit", r, k)[0])
+        q.put(bool(ok) if rank == 0 else (bool(ok) and gatherer.full(0) is None))
     finally:
         dist.destroy_process_group()
 
@@ -118,3 +131,19 @@ def test_bench_gather_path():
         p.join(120)
         assert p.exitcode == 0
     assert all(q.get(timeout=10) for _ in range(world))
+
+
+def test_bench_flags():
+    """Multi-GPU defaults: the gather is on unless --no-gather; --strong splits the batch."""
+    import sys
+    import bench
+    argv = sys.argv
+    try:
+        sys.argv = ["bench.py", "--gpus", "2"]
+        a = bench.parse()
+        assert not a.no_gather and not a.strong
+        sys.argv = ["bench.py", "--gpus", "4", "--strong", "--no-gather"]
+        a = bench.parse()
+        assert a.no_gather and a.strong
+    finally:
+        sys.argv = argv
