@@ -225,6 +225,14 @@ int hmm355_tv_forward_backward_ex_f32(const float* log_obs, const float* log_A, 
                                       unsigned out_mask, float* posterior, float* forward,
                                       float* backward, float* loglik, float* lik_ref,
                                       void* workspace, size_t workspace_bytes, void* stream);
+/* Adjoint of the time-varying forward-backward outputs (NeuralHMM training through its
+ * posteriors, neural.py:355-461): hmm355_fb_adjoint_f32's two chains with matrix k
+ * (exp(log_A[b,k]), linking steps k and k+1, strides as above) in place of one log_P.  E, the
+ * sources and W / P are (B,T,N) with row stride N; scale_w / scale_z (B,T). */
+int hmm355_tv_fb_adjoint_f32(const float* E, const float* log_A, long long a_bstride,
+                             long long a_tstride, const float* src_w, const float* scale_w,
+                             const float* src_z, const float* scale_z, int B, int T, int N,
+                             float* W, float* P, void* stream);
 size_t hmm355_tv_viterbi_workspace_bytes(int B, int T, int N);
 int hmm355_tv_viterbi_f32(const float* log_obs, const float* log_A, long long a_bstride,
                           long long a_tstride, const float* init, int B, int T, int N,

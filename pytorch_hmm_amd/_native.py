@@ -31,7 +31,7 @@ EXPORTS = (
     "hmm355_semimarkov_viterbi_f32", "hmm355_semimarkov_forward_f32",
     "hmm355_stream_greedy_f32", "hmm355_stream_beam_f32",
     "hmm355_plan_bytes", "hmm355_plan_f32", "hmm355_plan_banded", "hmm355_forward_backward_plan_f32", "hmm355_viterbi_plan_f32",
-    "hmm355_fb_adjoint_f32",
+    "hmm355_fb_adjoint_f32", "hmm355_tv_fb_adjoint_f32",
 )
 
 _lib = None
@@ -96,6 +96,9 @@ def lib():
     L.hmm355_stream_beam_f32.argtypes = [P, P, I, I, I, I, I, P, P, P, P, P, P, P, P]
     L.hmm355_stream_beam_f32.restype = I
     L.hmm355_fb_adjoint_f32.argtypes, L.hmm355_fb_adjoint_f32.restype = [P, P, P, P, P, P, I, I, I, P, P, P], I
+    LL = ctypes.c_longlong
+    L.hmm355_tv_fb_adjoint_f32.argtypes = [P, P, LL, LL, P, P, P, P, I, I, I, P, P, P]
+    L.hmm355_tv_fb_adjoint_f32.restype = I
     _lib = L
     return L
 

@@ -21,7 +21,9 @@ Losses: 'ref'   = the reference's compute_likelihood value LSE_j log(exp(log alp
         'exact' = log sum_j alpha_{T-1,j}  (HMMPyTorch.log_likelihood).
 Back-propagating THROUGH the posteriors / forward / backward outputs (HMMLayer training,
 the supervised cross-entropy of compute_loss) is ForwardBackwardFn: the adjoint of both
-recursions with per-step sources, on hmm355_fb_adjoint_f32 (csrc/adjoint.hip).
+recursions with per-step sources, on hmm355_fb_adjoint_f32 (csrc/adjoint.hip); with one
+transition matrix per step (NeuralHMM) TvForwardBackwardFn on hmm355_tv_fb_adjoint_f32
+(csrc/tv.hip).
 """
 import math
 
@@ -134,21 +136,26 @@ class SequenceLogLik(torch.autograd.Function):
         return grad_obs, grad_lP, grad_l0, None, None
 
 
-def _run_tv_fb(log_obs, A, sb, st, log_p0, log_beta_T=None, posterior=False):
-    """One hmm355_tv_forward_backward_ex_f32 call; returns (posterior|None, loglik, lik_ref, U, V, E)."""
+def _run_tv_fb(log_obs, A, sb, st, log_p0, log_beta_T=None, posterior=False, out_mask=None):
+    """One hmm355_tv_forward_backward_ex_f32 call; returns (posterior|None, loglik, lik_ref, U, V, E, LA),
+    with `out_mask` the first item is the (posterior, forward, backward) tuple per the mask."""
     B, T, N = log_obs.shape
     NP = _pad(N)
     dev = log_obs.device
     L = nat.lib()
     ws = torch.empty(L.hmm355_tv_fb_workspace_bytes(B, T, N), dtype=torch.uint8, device=dev)
-    post = torch.empty(B, T, N, device=dev) if posterior else None
+    mask = out_mask if out_mask is not None else (nat.FB_POSTERIOR if posterior else 0)
+    mk = lambda bit: torch.empty(B, T, N, device=dev) if mask & bit else None
+    post, fwd, bwd = mk(nat.FB_POSTERIOR), mk(nat.FB_FORWARD), mk(nat.FB_BACKWARD)
     loglik = torch.empty(B, device=dev)
     lik_ref = torch.empty(B, device=dev)
     with torch.cuda.device(dev):
         nat.check(L.hmm355_tv_forward_backward_ex_f32(
             nat.ptr(log_obs), nat.ptr(A), sb, st, nat.ptr(log_p0), nat.ptr(log_beta_T), B, T, N,
-            nat.FB_POSTERIOR if posterior else 0, nat.ptr(post), None, None, nat.ptr(loglik), nat.ptr(lik_ref),
+            mask, nat.ptr(post), nat.ptr(fwd), nat.ptr(bwd), nat.ptr(loglik), nat.ptr(lik_ref),
             nat.ptr(ws), ws.numel(), nat.stream_of(dev)))
+    if out_mask is not None:
+        post = (post, fwd, bwd)
     rows = B * T
     al = lambda n: ((n + 255) // 256) * 256
     fl = ws.view(torch.float32)
@@ -216,6 +223,35 @@ class TvSequenceLogLik(torch.autograd.Function):
         return grad_lo, grad_A, grad_l0, None
 
 
+def _adjoint_sources(U, V, E, post, fwd, bwd, gp, gf, gb):
+    """Per-step sources and scales of the two adjoint chains (ForwardBackwardFn's docstring):
+    srcW = v (Gp - <gamma, Gp>) / sum(u v) + Gf exp(LA), srcZ = u (Gp - <gamma, Gp>) / sum(u v)
+    + Gb exp(LB) (Gf exp(LA) = Gf forward / u), Fw_t = 1 / sum u_t, Fz_t = 1 / sum v_t E_t
+    (t >= 1).  Formed in fp64 from the stored fp32 rows, returned as contiguous fp32."""
+    B, T, N = U.shape
+    U64, V64 = U.double(), V.double()
+    Suv = (U64 * V64).sum(-1, keepdim=True)
+    srcW = torch.zeros(B, T, N, dtype=torch.float64, device=U.device)
+    srcZ = torch.zeros_like(srcW)
+    if gp is not None:
+        g64 = gp.double()
+        q = (g64 - (post.double() * g64).sum(-1, keepdim=True)) / torch.where(Suv > 0, Suv, torch.ones_like(Suv))
+        q = torch.where(Suv > 0, q, torch.zeros_like(q))
+        srcW += V64 * q
+        srcZ += U64 * q
+    if gf is not None:
+        srcW += torch.where(U64 > 0, gf.double() * fwd.double() / torch.where(U64 > 0, U64, torch.ones_like(U64)),
+                            torch.zeros_like(U64))
+    if gb is not None:
+        srcZ += torch.where(V64 > 0, gb.double() * bwd.double() / torch.where(V64 > 0, V64, torch.ones_like(V64)),
+                            torch.zeros_like(V64))
+    Fw = (1.0 / U64.sum(-1)).float().contiguous()                              # 1/c_t
+    Fz = torch.zeros(B, T, device=U.device)
+    if T > 1:
+        Fz[:, 1:] = (1.0 / (V64[:, 1:] * E[:, 1:].double()).sum(-1)).float()   # 1/c'_{t-1}
+    return srcW.float().contiguous(), Fw, srcZ.float().contiguous(), Fz
+
+
 class ForwardBackwardFn(torch.autograd.Function):
     """HMMPyTorch.forward_backward outputs (posterior, forward, backward) per `out_mask`,
     differentiable in obs, log_P and log_p0 — the reference back-propagates through its
@@ -261,29 +297,8 @@ class ForwardBackwardFn(torch.autograd.Function):
                     if ctx.out_mask & bit]
         got = dict(zip(returned, grads))
         gp, gf, gb = got.get("p"), got.get("f"), got.get("b")
-        E = _staged_emissions(obs, ctx.obs_mode)
-        U64, V64 = U.double(), V.double()
-        Suv = (U64 * V64).sum(-1, keepdim=True)
-        srcW = torch.zeros(B, T, N, dtype=torch.float64, device=obs.device)
-        srcZ = torch.zeros_like(srcW)
-        if gp is not None:
-            g64 = gp.double()
-            q = (g64 - (post.double() * g64).sum(-1, keepdim=True)) / torch.where(Suv > 0, Suv, torch.ones_like(Suv))
-            q = torch.where(Suv > 0, q, torch.zeros_like(q))
-            srcW += V64 * q
-            srcZ += U64 * q
-        if gf is not None:
-            srcW += torch.where(U64 > 0, gf.double() * fwd.double() / torch.where(U64 > 0, U64, torch.ones_like(U64)),
-                                torch.zeros_like(U64))
-        if gb is not None:
-            srcZ += torch.where(V64 > 0, gb.double() * bwd.double() / torch.where(V64 > 0, V64, torch.ones_like(V64)),
-                                torch.zeros_like(V64))
-        srcW, srcZ = srcW.float().contiguous(), srcZ.float().contiguous()
-        Fw = (1.0 / U64.sum(-1)).float().contiguous()                       # 1/c_t
-        Fz = torch.zeros(B, T, device=obs.device)
-        if T > 1:
-            Fz[:, 1:] = (1.0 / (V64[:, 1:] * E[:, 1:].double()).sum(-1)).float()   # 1/c'_{t-1}
-        E = E.contiguous()
+        E = _staged_emissions(obs, ctx.obs_mode).contiguous()
+        srcW, Fw, srcZ, Fz = _adjoint_sources(U, V, E, post, fwd, bwd, gp, gf, gb)
         W = torch.empty(B, T, N, device=obs.device)
         P = torch.empty(B, T, N, device=obs.device)
         L = nat.lib()
@@ -307,24 +322,80 @@ class ForwardBackwardFn(torch.autograd.Function):
         return grad_obs, grad_lP, grad_l0, None, None, None
 
 
-class _TvNoPosteriorGrad(torch.autograd.Function):
-    """NeuralHMM forward-backward outputs in a graph whose inputs require grad: the values are
-    exact; back-propagating through the posteriors of the per-step-matrix recursion is not
-    implemented (its likelihood is differentiable: TvSequenceLogLik)."""
+class TvForwardBackwardFn(torch.autograd.Function):
+    """NeuralHMM.forward outputs (posterior, forward, backward) per `out_mask` under per-step
+    transition matrices, differentiable in log_obs, log_A ((N,N) or (B,T,N,N)) and log_p0 —
+    the reference back-propagates through its per-step logsumexp loops (neural.py:391-461).
+    Forward: csrc/tv.hip's chains (log-emissions staged as E_t = exp(lo_t - M_t)).  Backward:
+    ForwardBackwardFn's adjoint with the step's own matrix: hmm355_tv_fb_adjoint_f32 runs the
+    W / Z chains streaming A_k = exp(log_A_k) as the forward does, then
+        dL/d log_obs_t = u_t W_t + v_t P_t,   dL/d log_p0 = sum_b u_0 W_0,
+        dL/d log_A_k   = exp(log_A_k) * [ (u_k / c_k) (x) (E_{k+1} W_{k+1})
+                                          + Z_k (x) (E_{k+1} v_{k+1} / c'_k) ]   (k <= T-2; 0 at k = T-1)
+    (summed over (b, k) for one static matrix)."""
 
     @staticmethod
-    def forward(ctx, obs, log_P, log_p0, *outs):
-        return tuple(o.clone() for o in outs)
+    def forward(ctx, log_obs, log_A, log_p0, out_mask):
+        from .ops import _tv_matrix
+        nat.require_gpu(log_obs, log_A, log_p0)
+        lo = log_obs.detach().to(torch.float32).contiguous()
+        l0 = log_p0.detach().to(torch.float32).contiguous()
+        B, T, N = lo.shape
+        A, sb, st = _tv_matrix(log_A.detach(), B, T, N)
+        outs, _, _, U, V, E, _ = _run_tv_fb(lo, A, sb, st, l0, out_mask=out_mask | nat.FB_POSTERIOR)
+        post, fwd, bwd = outs
+        ctx.save_for_backward(lo, A, l0, U, V, E, post, fwd, bwd)
+        ctx.sb, ctx.st, ctx.static, ctx.out_mask = sb, st, log_A.dim() == 2, out_mask
+        ctx.a_shape = tuple(log_A.shape)
+        ctx.set_materialize_grads(False)
+        return tuple(o for bit, o in ((nat.FB_POSTERIOR, post), (nat.FB_FORWARD, fwd), (nat.FB_BACKWARD, bwd))
+                     if out_mask & bit)
 
     @staticmethod
     def backward(ctx, *grads):
-        raise NotImplementedError(
-            "gradients through NeuralHMM forward-backward posteriors are not implemented on the MI355X path; "
-            "differentiate compute_likelihood instead")
+        lo, A, l0, U, V, E, post, fwd, bwd = ctx.saved_tensors
+        B, T, N = lo.shape
+        returned = [k for bit, k in ((nat.FB_POSTERIOR, "p"), (nat.FB_FORWARD, "f"), (nat.FB_BACKWARD, "b"))
+                    if ctx.out_mask & bit]
+        got = dict(zip(returned, grads))
+        E = E.contiguous()
+        srcW, Fw, srcZ, Fz = _adjoint_sources(U, V, E, post, fwd, bwd, got.get("p"), got.get("f"), got.get("b"))
+        W = torch.empty(B, T, N, device=lo.device)
+        P = torch.empty(B, T, N, device=lo.device)
+        L = nat.lib()
+        with torch.cuda.device(lo.device):
+            nat.check(L.hmm355_tv_fb_adjoint_f32(nat.ptr(E), nat.ptr(A), ctx.sb, ctx.st, nat.ptr(srcW), nat.ptr(Fw),
+                                                 nat.ptr(srcZ), nat.ptr(Fz), B, T, N, nat.ptr(W), nat.ptr(P),
+                                                 nat.stream_of(lo.device)))
+        grad_lo = U * W + V * P
+        grad_l0 = (U[:, 0] * W[:, 0]).sum(0)
+        grad_A = None
+        if ctx.needs_input_grad[1]:
+            if ctx.static:
+                M = torch.zeros(N, N, device=lo.device)
+                if T > 1:
+                    X1 = U[:, :-1] * Fw[:, :-1, None]
+                    Y1 = E[:, 1:] * W[:, 1:]
+                    Y2 = E[:, 1:] * V[:, 1:] * Fz[:, 1:, None]
+                    M = torch.einsum("bti,btj->ij", X1, Y1) + torch.einsum("bti,btj->ij", (srcZ + P)[:, :-1], Y2)
+                grad_A = torch.exp(A) * M
+            else:
+                # matrices k = 0 .. T-2 are used; any further ones (log_A may carry T or more
+                # steps, neural.py:377-381) get a zero gradient
+                grad_A = torch.zeros(ctx.a_shape, device=lo.device)
+                if T > 1:
+                    # both outer products of a step as one K = 2 batched GEMM, then * exp(log_A_k)
+                    Lf = torch.stack([U[:, :-1] * Fw[:, :-1, None], (srcZ + P)[:, :-1]], -1)        # (B,T-1,N,2)
+                    Rf = torch.stack([E[:, 1:] * W[:, 1:], E[:, 1:] * V[:, 1:] * Fz[:, 1:, None]], -2)  # (B,T-1,2,N)
+                    g = torch.matmul(Lf, Rf)
+                    g.mul_(torch.exp(A.expand(ctx.a_shape)[:, :T - 1]))
+                    grad_A[:, :T - 1] = g
+        return grad_lo, grad_A, grad_l0, None
 
 
-def tv_forward_backward_with_grad(obs, log_A, log_p0, outs):
-    return _TvNoPosteriorGrad.apply(obs, log_A, log_p0, *outs)
+def tv_forward_backward_with_grad(log_obs, log_A, log_p0, out_mask):
+    """Differentiable NeuralHMM forward-backward outputs (tuple per out_mask)."""
+    return TvForwardBackwardFn.apply(log_obs, log_A, log_p0, out_mask)
 
 
 def forward_backward_with_grad(obs, log_P, log_p0, obs_mode, out_mask, plan=None):

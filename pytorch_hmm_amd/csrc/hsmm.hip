@@ -148,12 +148,19 @@ __global__ void __launch_bounds__(kHsThreads) hsmm_fwd_kernel(HsArgs a) {
   // One end time.  Lane `sub` owns slots k = 4*sub + j, so the new element's position in its
   // segment's group of four, (t - k) & 3 = (U - j) & 3 with U = t & 3, is a compile-time
   // constant of the unrolled copy: each slot runs only its own accumulator update.
+  // Branch-free: every LDS read of the step is issued before its first use (a guarded read
+  // ends in its own s_waitcnt, which serialised four duration-table round trips per step).
+  // Rows s >= S of the tables hold -inf / 0, so the unguarded reads are in range and inert.
   auto end_step = [&](const int t, auto Uc) -> bool {
     constexpr int U = decltype(Uc)::value;
-    const float x = live ? L.lpr[t % kHsL][s] : 0.f;
-    float v[kHsNJ];
+    const float x = L.lpr[t % kHsL][s];
+    float v[kHsNJ], du[kHsNJ];
     int dd[kHsNJ];
     float mx = -INFINITY;
+    static_for<0, kHsNJ>([&](auto Jc) {
+      constexpr int j = decltype(Jc)::value;
+      du[j] = L.dur[s][(t - (4 * sub + j)) & (kHsR - 1)];  // dur[s][d - 1], -inf for d > Dm
+    });
     static_for<0, kHsNJ>([&](auto Jc) {
       constexpr int j = decltype(Jc)::value;
       const int age = (t - (4 * sub + j)) & (kHsR - 1);
@@ -176,22 +183,21 @@ __global__ void __launch_bounds__(kHsThreads) hsmm_fwd_kernel(HsArgs a) {
         Q[j][pos] = G[j][pos] + x;
         A0[j] = A0[j] + x;
       }
-      v[j] = -INFINITY;
-      if (live && d <= Dm && st >= 0) {
-        float o = 0.f + A0[j];
-        o = o + G[j][1];
-        o = o + G[j][2];
-        o = o + G[j][3];
-        const float u = L.dur[s][d - 1];
-        if (st == 0) v[j] = o + u;                                              // hsmm.py:269-274
-        else v[j] = (mp[j] == -INFINITY) ? -INFINITY : (mp[j] + o) + u;          // hsmm.py:304-314
-      }
+      float o = 0.f + A0[j];
+      o = o + G[j][1];
+      o = o + G[j][2];
+      o = o + G[j][3];
+      const float u = du[j];
+      // hsmm.py:269-274 (st == 0: no predecessor) / :304-314; mp == -inf (no predecessor path)
+      // gives (mp + o) + u == -inf since o is finite
+      const float val = st == 0 ? o + u : (mp[j] + o) + u;
+      v[j] = (live && d <= Dm && st >= 0) ? val : -INFINITY;
       mx = fmaxf(mx, v[j]);
     });
     mx = row_max16(mx);
-    if (live && sub == 0) {
-      L.dmx[t & 1][s] = mx;
-      a.Dg[((size_t)b * T + t) * S + s] = mx;
+    if (sub == 0) {
+      L.dmx[t & 1][s] = mx;  // -inf for the padding states s >= S (read unguarded below)
+      if (live) a.Dg[((size_t)b * T + t) * S + s] = mx;
     }
     if (t == T - 1) {
       // best over (s asc, d asc) of delta[T-1][s][d-1], strict > (hsmm.py:319-329)
@@ -220,12 +226,17 @@ __global__ void __launch_bounds__(kHsThreads) hsmm_fwd_kernel(HsArgs a) {
     {
       float lm = -INFINITY;
       int ls = 0x7fff;
+      float dmv[kHsNJ];
+#pragma unroll
+      for (int j = 0; j < kHsNJ; ++j) dmv[j] = L.dmx[t & 1][sub + kHsSub * j];  // all reads first
 #pragma unroll
       for (int j = 0; j < kHsNJ; ++j) {
         const int sp = sub + kHsSub * j;
-        const float dm = L.dmx[t & 1][sp < S ? sp : 0];
-        const float c = (lt[j] == -INFINITY || dm == -INFINITY) ? -INFINITY : dm + lt[j];
-        if (c > lm) { lm = c; ls = sp; }
+        // lt == -inf (excluded s') or dm == -inf: the sum is -inf (never +inf: no NaN)
+        const float c = dmv[j] + lt[j];
+        const bool gt = c > lm;
+        lm = gt ? c : lm;
+        ls = gt ? sp : ls;
       }
       const float M = row_max16(lm);
       const int s1 = row_min16_i((lm == M && M != -INFINITY) ? ls : 0x7fff);

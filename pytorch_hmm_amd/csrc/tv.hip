@@ -482,6 +482,221 @@ __global__ void __launch_bounds__(512) tv_vit_kernel(TvArgs va) {
   tv_chain<NP, kTvVit, VEC>(va, lds, blockIdx.x);
 }
 
+// ---------------------------------------------------------------------------------------
+// Adjoint of the time-varying forward-backward OUTPUTS (NeuralHMM training through its
+// posteriors / forward / backward; reference neural.py:355-461, where autograd runs back
+// through the per-step logsumexp loops).  The same two linear chains as csrc/adjoint.hip
+// (pytorch_hmm_amd/autograd.py derives them), with the step's own matrix A_k = exp(lA_k)
+// (k links steps k and k+1) streamed from HBM exactly as the forward chains stream it:
+//   W (beta layout, backward in time):  W_{T-1} = S_{T-1};
+//        W_t[i] = S_t[i] + F_t * sum_j A_t[i][j] E_{t+1}[j] W_{t+1}[j]
+//   Z (alpha layout, forward in time):  Z_0 = R_0;  Z_t = R_t + P_t,
+//        P_t[j] = G_t * E_t[j] * sum_i Z_{t-1}[i] A_{t-1}[i][j]
+// Outputs W and P (B,T,N) (P_0 = 0; P kept apart from R so that V * P never cancels).  The
+// alpha layout's row parts hold PARTIAL sums (linear in the previous vector), so the P
+// partials go to Pbuf and R_t to a row of its own (Rbuf); a reader forms Z = sum P + R, the
+// published row is sum P alone.  Per-step loads (source, emission, scale) are issued PD steps
+// ahead beside the matrix prefetch.
+struct TvAdjArgs {
+  const float* lA;
+  long long sb, st;
+  const float* E;    // (B,T,N) staged emissions exp(lo - M)
+  const float* src;  // (B,T,N) S (W chain) / R (Z chain)
+  const float* sc;   // (B,T)   F_t (W chain) / G_t (Z chain)
+  float* out;        // (B,T,N) W / P
+  int B, T, N;
+};
+
+template <int NP, int CH, bool VEC>
+__device__ void tv_adj_chain(const TvAdjArgs& j, float* lds, int b) {
+  using G = TvGeo<NP>;
+  constexpr int PD = G::PD;
+  constexpr int KIND = CH == 0 ? kTvBeta : kTvAlpha;   // matrix slice layout (tv_load)
+  const int tid = threadIdx.x, w = tid >> 6, l = tid & 63;
+  const int T = j.T, N = j.N;
+  // tv_load reads lA / sb / st / N from a TvArgs
+  TvArgs ta{nullptr, j.lA, j.sb, j.st, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, j.B, T, N};
+  int jo;
+  bool writer;
+  const int part = w / G::CB, r8 = l >> 3;
+  if (CH == 0) {
+    int kk = 0;
+    if (G::KB == 2) kk = (l >> 2) & 1;
+    if (G::KB == 4) kk = 2 * ((l >> 2) & 1) + ((l >> 1) & 1);
+    jo = G::SLICE * w + r8 + 8 * kk;
+    writer = G::KB == 1 ? (l & 7) == 0 : (G::KB == 2 ? (l & 3) == 0 : (l & 1) == 0);
+  } else {
+    const int cc = 2 * (l >> 5) + ((l >> 4) & 1);
+    jo = 32 * (w % G::CB) + 4 * (l & 7) + cc;
+    writer = (l & 8) == 0;
+  }
+  const bool jok = jo < N;
+  const int jc = jok ? jo : 0;
+  auto perm = [&](int i) { return (i / G::RPP) * G::RPP + (i % 8) * G::KA + (i % G::RPP) / 8; };
+  const bool rowout = CH == 1 && (w % G::CB) == 0 && (l & 7) < G::KA;
+  constexpr int BUFZ = (G::RH + 1) * NP;  // Z chain per parity: P partials [RH][NP] + R [NP]
+  auto Pbuf = [&](int par) { return lds + par * BUFZ; };
+  auto Rbuf = [&](int par) { return lds + par * BUFZ + G::RH * NP; };
+  float* xbuf = lds;  // W chain: [2][NP] product input E W
+
+  const size_t rb = (size_t)b * T;
+  auto kmat_of = [&](int q) { return CH == 0 ? T - 1 - q : q - 1; };
+  auto tout_of = [&](int q) { return CH == 0 ? T - 1 - q : q; };
+  auto prefetch = [&](int q, float4 (&rw)[G::NV]) {
+    __builtin_amdgcn_sched_barrier(0);
+    tv_load<NP, KIND, VEC>(ta, b, kmat_of(q < T ? q : T - 1), rw);
+    __builtin_amdgcn_sched_barrier(0);
+  };
+  // per-step scalars of this lane's output, loaded PD steps ahead (clamped past the end)
+  auto aux = [&](int q, float& s_, float& e_, float& f_) {
+    const size_t row = rb + tout_of(q < T ? q : T - 1);
+    s_ = j.src[row * N + jc];
+    e_ = j.E[row * N + jc];
+    f_ = j.sc[row];
+  };
+  auto read_rows = [&](int par, float (&y)[G::KA]) {
+    const float* P = Pbuf(par) + part * G::RPP + r8 * G::KA;
+    const float* R = Rbuf(par) + part * G::RPP + r8 * G::KA;
+#pragma unroll
+    for (int h = 0; h <= G::RH; ++h) {
+      const float* src = h < G::RH ? P + h * NP : R;
+      float x[G::KA];
+      if constexpr (G::KA % 4 == 0) {
+#pragma unroll
+        for (int k4 = 0; k4 < G::KA / 4; ++k4) {
+          const float4 v = *reinterpret_cast<const float4*>(src + 4 * k4);
+          x[4 * k4] = v.x; x[4 * k4 + 1] = v.y; x[4 * k4 + 2] = v.z; x[4 * k4 + 3] = v.w;
+        }
+      } else {
+#pragma unroll
+        for (int k2 = 0; k2 < G::KA / 2; ++k2) {
+          const float2 v = *reinterpret_cast<const float2*>(src + 2 * k2);
+          x[2 * k2] = v.x; x[2 * k2 + 1] = v.y;
+        }
+      }
+#pragma unroll
+      for (int k = 0; k < G::KA; ++k) y[k] = h == 0 ? x[k] : y[k] + x[k];
+    }
+  };
+  // P row t (the sum of the partials, no R) -> HBM
+  auto publish_row = [&](int par, int t) {
+#pragma unroll
+    for (int kq = 0; kq < (G::KA + 7) / 8; ++kq) {
+      const int k = (l & 7) + 8 * kq;
+      if (k < G::KA) {
+        const int off = part * G::RPP + r8 * G::KA + k;
+        const int i = part * G::RPP + r8 + 8 * k;
+        const float* P = Pbuf(par) + off;
+        float u = P[0];
+#pragma unroll
+        for (int h = 1; h < G::RH; ++h) u += P[h * NP];
+        if (i < N) j.out[(rb + t) * N + i] = u;
+      }
+    }
+  };
+
+  float4 raw[PD][G::NV];
+  float rS[PD], rE[PD], rF[PD];
+  if (T > 1) {
+#pragma unroll
+    for (int s = 0; s < PD; ++s) {
+      prefetch(1 + s, raw[s]);
+      aux(1 + s, rS[s], rE[s], rF[s]);
+    }
+  }
+  // step 0: W_{T-1} = S_{T-1};  Z_0 = R_0 (P_0 = 0)
+  {
+    float s0, e0, f0;
+    aux(0, s0, e0, f0);
+    s0 = jok ? s0 : 0.f;
+    if (CH == 0) {
+      if (writer) {
+        xbuf[jo] = jok ? e0 * s0 : 0.f;
+        if (jok) j.out[(rb + T - 1) * N + jo] = s0;
+      }
+    } else if (writer) {
+      Pbuf(0)[part * NP + perm(jo)] = 0.f;
+      if (part == 0) Rbuf(0)[perm(jo)] = s0;
+    }
+  }
+  lds_barrier();
+
+  auto step = [&](int q, float4 (&rw)[G::NV], float& rs, float& re, float& rf) {
+    const int t = tout_of(q);
+    if (CH == 0) {
+      const float* prev = xbuf + ((q - 1) & 1) * NP;
+      float* cur = xbuf + (q & 1) * NP;
+      float wv[G::MB][4];
+#pragma unroll
+      for (int m = 0; m < G::MB; ++m) {
+        const float4 x = *reinterpret_cast<const float4*>(prev + 4 * ((l & 7) + 8 * m));
+        wv[m][0] = x.x; wv[m][1] = x.y; wv[m][2] = x.z; wv[m][3] = x.w;
+      }
+      float z[G::KB];
+#pragma unroll
+      for (int k = 0; k < G::KB; ++k) {
+        float s0 = 0.f, s1 = 0.f;
+#pragma unroll
+        for (int m = 0; m < G::MB; ++m) {
+          const float4 A = rw[k * G::MB + m];
+          s0 = fmaf(__expf(A.x), wv[m][0], s0);
+          s1 = fmaf(__expf(A.y), wv[m][1], s1);
+          s0 = fmaf(__expf(A.z), wv[m][2], s0);
+          s1 = fmaf(__expf(A.w), wv[m][3], s1);
+        }
+        z[k] = s0 + s1;
+      }
+      prefetch(q + PD, rw);
+      const float zz = quadlanes_transpose_sum<G::KB>(z, l);
+      const float v = (jok ? rs : 0.f) + rf * zz;   // W_t = S_t + F_t (A_t (E W)_{t+1})
+      if (writer) {
+        cur[jo] = jok ? re * v : 0.f;
+        if (jok) j.out[(rb + t) * N + jo] = v;
+      }
+    } else {
+      const int pp = (q - 1) & 1, cp = q & 1;
+      float y[G::KA];
+      read_rows(pp, y);   // Z_{t-1} = R + sum of the P partials
+      float acc[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int k = 0; k < G::KA; ++k) {
+        const float4 A = rw[k];
+        acc[0] = fmaf(y[k], __expf(A.x), acc[0]);
+        acc[1] = fmaf(y[k], __expf(A.y), acc[1]);
+        acc[2] = fmaf(y[k], __expf(A.z), acc[2]);
+        acc[3] = fmaf(y[k], __expf(A.w), acc[3]);
+      }
+      prefetch(q + PD, rw);
+      const float z = rowlanes_transpose_sum<8>(acc);
+      const float pr = rf * ((jok ? re : 0.f) * z);   // this row part's share of P_t
+      if (writer) {
+        Pbuf(cp)[part * NP + perm(jo)] = pr;
+        if (part == 0) Rbuf(cp)[perm(jo)] = jok ? rs : 0.f;
+      }
+      if (rowout) publish_row(pp, q - 1);
+    }
+    aux(q + PD, rs, re, rf);
+    lds_barrier();
+  };
+  int q0 = 1;
+  for (; q0 + PD <= T; q0 += PD) {
+#pragma unroll
+    for (int s = 0; s < PD; ++s) step(q0 + s, raw[s], rS[s], rE[s], rF[s]);
+  }
+#pragma unroll
+  for (int s = 0; s < PD; ++s)
+    if (q0 + s < T) step(q0 + s, raw[s], rS[s], rE[s], rF[s]);
+  if (CH == 1 && rowout) publish_row((T - 1) & 1, T - 1);
+}
+
+template <int NP, bool VEC>
+__global__ void __launch_bounds__(512) tv_adjoint_kernel(TvAdjArgs aw, TvAdjArgs az) {
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  const int b = blockIdx.x >> 1;
+  if (blockIdx.x & 1) tv_adj_chain<NP, 1, VEC>(az, lds, b);
+  else tv_adj_chain<NP, 0, VEC>(aw, lds, b);
+}
+
 // E = exp(lo - M) per (b,t) row (zero-padded to NP), M = the row max (0 for an all -inf row).
 // One wave per row, grid-stride.
 template <int NP>
@@ -744,6 +959,34 @@ HMM355_API int hmm355_tv_viterbi_f32(const float* log_obs, const float* log_A, l
     case 64: e = launch_tv_vit<64>(ta, va, vec, st); break;
     case 128: e = launch_tv_vit<128>(ta, va, vec, st); break;
     default: e = launch_tv_vit<256>(ta, va, vec, st); break;
+  }
+  return e == hipSuccess ? HMM355_OK : (int)e;
+}
+
+HMM355_API int hmm355_tv_fb_adjoint_f32(const float* E, const float* log_A, long long a_bstride, long long a_tstride,
+                                        const float* src_w, const float* scale_w, const float* src_z,
+                                        const float* scale_z, int B, int T, int N, float* W, float* P, void* stream) {
+  if (B < 0 || N < 0 || a_bstride < 0 || a_tstride < 0) return HMM355_E_ARG;
+  if (N < 1 || N > 256) return HMM355_E_STATES;
+  if (T < 1) return HMM355_E_SHAPE;
+  if (B == 0) return HMM355_OK;
+  if (!E || !log_A || !src_w || !scale_w || !src_z || !scale_z || !W || !P) return HMM355_E_ARG;
+  if ((size_t)B * T > (size_t)1 << 40 || B > (1 << 30)) return HMM355_E_SHAPE;
+  TvAdjArgs aw{log_A, a_bstride, a_tstride, E, src_w, scale_w, W, B, T, N};
+  TvAdjArgs az{log_A, a_bstride, a_tstride, E, src_z, scale_z, P, B, T, N};
+  const bool vec = tv_vec_ok(log_A, a_bstride, a_tstride, N);
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  hipError_t e = hipSuccess;
+  auto go = [&](auto kern) {
+    e = allow_lds(kern, kExclusiveLds);
+    if (e != hipSuccess) return;
+    hipLaunchKernelGGL(kern, dim3(2 * B), dim3(512), kExclusiveLds, st, aw, az);
+    e = hipGetLastError();
+  };
+  switch (pad_states(N)) {
+    case 64: vec ? go(tv_adjoint_kernel<64, true>) : go(tv_adjoint_kernel<64, false>); break;
+    case 128: vec ? go(tv_adjoint_kernel<128, true>) : go(tv_adjoint_kernel<128, false>); break;
+    default: vec ? go(tv_adjoint_kernel<256, true>) : go(tv_adjoint_kernel<256, false>); break;
   }
   return e == hipSuccess ? HMM355_OK : (int)e;
 }

@@ -188,9 +188,10 @@ class NeuralHMM(nn.Module):
         log_A = self._log_transitions(B, T, context)
         log_init = self._log_initial()
         mask = ops.FB_POSTERIOR | ops.FB_FORWARD | ops.FB_BACKWARD
-        post, fwd, bwd, _, _ = ops.tv_forward_backward(log_obs.detach(), log_A.detach(), log_init.detach(), mask)
         if needs_grad(log_obs, log_A, log_init):
-            post, fwd, bwd = tv_forward_backward_with_grad(log_obs, log_A, log_init, (post, fwd, bwd))
+            # differentiable outputs: the analytic adjoint on csrc/tv.hip (autograd.TvForwardBackwardFn)
+            return tv_forward_backward_with_grad(log_obs, log_A, log_init, mask)
+        post, fwd, bwd, _, _ = ops.tv_forward_backward(log_obs, log_A, log_init, mask)
         return post, fwd, bwd
 
     def viterbi_decode(self, observations: torch.Tensor,

@@ -261,3 +261,73 @@ def test_neural_hmm_training_step():
     for name, p in m.named_parameters():
         if "observation_model.logvar_net" in name or "mean_net" in name or "network" in name or "initial" in name:
             assert p.grad is not None and torch.isfinite(p.grad).all(), name
+
+
+# ------------------------------------------- gradients through the forward-backward outputs
+def _fp64_tv_outputs(lo, lA, l0):
+    """neural.py:391-401 in float64 with autograd (list-based, no in-place writes): posterior,
+    forward = exp(log_forward), backward = exp(log_backward)."""
+    B, T, N = lo.shape
+    A = lA if lA.dim() == 4 else lA.expand(B, T, N, N)
+    la = [l0 + lo[:, 0]]
+    for s in range(1, T):
+        la.append(torch.logsumexp(la[-1].unsqueeze(-1) + A[:, s - 1], dim=1) + lo[:, s])
+    lb = [torch.zeros(B, N, dtype=lo.dtype)]
+    for s in range(T - 2, -1, -1):
+        lb.insert(0, torch.logsumexp(A[:, s] + lo[:, s + 1].unsqueeze(1) + lb[0].unsqueeze(1), dim=-1))
+    la, lb = torch.stack(la, 1), torch.stack(lb, 1)
+    lp = la + lb
+    lp = lp - torch.logsumexp(lp, dim=-1, keepdim=True)
+    return torch.exp(lp), torch.exp(la), torch.exp(lb)
+
+
+@pytest.mark.parametrize("which", ["post", "all"])
+@pytest.mark.parametrize("B,T,N,static", [(2, 12, 5, False), (2, 30, 64, False), (1, 20, 100, True),
+                                          (2, 8, 128, False), (1, 9, 200, False), (2, 1, 7, False),
+                                          (2, 17, 33, True)])
+def test_tv_output_gradients_vs_fp64_autograd(which, B, T, N, static):
+    """NeuralHMM trains through its posteriors (and forward / backward) in the reference
+    (neural.py:355-461, plain autograd over the loops).  The analytic adjoint on
+    hmm355_tv_fb_adjoint_f32 against fp64 autograd through those loops, for a random linear loss
+    on the outputs: every gradient within 1e-4 of its tensor's largest entry."""
+    lo, lA, l0 = _random_case(B, T, N, 7 * T + N + B, static, spread=1.0)
+    lo = lo + np.float32(40.0)   # O(1) log-emissions: forward / backward stay representable
+    rng = np.random.default_rng(N + T)
+    gw = [rng.standard_normal((B, T, N)) for _ in range(3)]
+    ref_in = [torch.from_numpy(v).double().requires_grad_(True) for v in (lo, lA, l0)]
+    outs = _fp64_tv_outputs(*ref_in)
+    use = (0,) if which == "post" else (0, 1, 2)
+    sum(((outs[k] * torch.from_numpy(gw[k])).sum() for k in use)).backward()
+    from pytorch_hmm_amd import ops as o
+    from pytorch_hmm_amd.autograd import TvForwardBackwardFn
+    mask = o.FB_POSTERIOR if which == "post" else o.FB_POSTERIOR | o.FB_FORWARD | o.FB_BACKWARD
+    a, b_, c = (t(v).requires_grad_(True) for v in (lo, lA, l0))
+    got = TvForwardBackwardFn.apply(a, b_, c, mask)
+    np.testing.assert_allclose(got[0].detach().cpu().numpy(), outs[0].detach().numpy(), atol=2e-5)
+    sum(((got[i] * t(gw[k])).sum() for i, k in enumerate(use))).backward()
+    for name, g_, r_ in (("log_obs", a.grad, ref_in[0].grad), ("log_A", b_.grad, ref_in[1].grad),
+                         ("log_p0", c.grad, ref_in[2].grad)):
+        g_ = g_.cpu().numpy().astype(np.float64)
+        r_ = r_.numpy() if r_ is not None else np.zeros_like(g_)   # T = 1: no matrix is used
+        assert g_.shape == r_.shape, name
+        err, scale = np.abs(g_ - r_).max(), max(np.abs(r_).max(), 1e-30)
+        assert err <= 1e-4 * scale, (name, err, scale)
+
+
+def test_neural_hmm_trains_through_posteriors():
+    """NeuralHMM.forward's posteriors are differentiable into both networks and the initial
+    logits (the reference's natural training use); the gradient w.r.t. the networks' outputs
+    equals fp64 autograd through the reference loops on the same outputs."""
+    from pytorch_hmm_amd.neural import NeuralHMM
+    torch.manual_seed(0)
+    m = NeuralHMM(num_states=6, observation_dim=8, context_dim=5, hidden_dim=32).to(DEV).train()
+    x, ctx = torch.randn(2, 20, 8, device=DEV), torch.randn(2, 20, 5, device=DEV)
+    target = torch.randint(0, 6, (2, 20), device=DEV)
+    post, fwd, bwd = m(x, ctx)
+    loss = torch.nn.functional.cross_entropy(post.reshape(-1, 6), target.reshape(-1))
+    loss.backward()
+    for name, p in m.named_parameters():
+        if "observation_model" in name or "transition_model" in name or "initial" in name:
+            if p.requires_grad and ("net" in name or "network" in name or "initial" in name):
+                assert p.grad is not None and torch.isfinite(p.grad).all(), name
+    assert float(m.initial_logits.grad.abs().sum()) > 0
