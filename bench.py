@@ -111,6 +111,30 @@ def profiled_traffic(op, B, T, N, transition):
     return None, None
 
 
+def profiled_kernel_traffic(kernel, desc):
+    """HBM bytes per launch of `kernel` (a torch.profiler kernel name) from the committed
+    rocprofv3 PMC summary of the same layer workload (tools/gpu_prof.sh --workload ...;
+    FETCH_SIZE x 2 + WRITE_SIZE), or (None, None)."""
+    import glob
+    import re
+    m = re.search(r"hmm355::(\w+)(<[^>]*>)?", kernel or "")
+    if not m:
+        return None, None
+    short = (m.group(1) + (m.group(2) or "")).replace(" ", "")
+    for f in sorted(glob.glob(os.path.join(HERE, "profiles", "*_summary.json")), reverse=True):
+        try:
+            d = json.load(open(f))
+        except (OSError, ValueError):
+            continue
+        cfg = d.get("bench_config") or {}
+        if any(cfg.get(k) != desc.get(k) for k in ("workload", "batch_per_gpu", "seq_len", "num_states")):
+            continue
+        v = (d.get("traffic") or {}).get(short, {}).get("hbm_bytes_per_launch")
+        if v:
+            return float(v), os.path.relpath(f, HERE)
+    return None, None
+
+
 def cpu_baseline(B, T, N, budget, P):
     """Time the oracle (reference op sequence on torch-CPU) on the NS workload (transition
     matrix P), repeated until `budget` seconds of CPU work are spent (at least one FB+Viterbi
@@ -362,6 +386,8 @@ def layer_workload(args, rank, world, dev):
             kroof = {"note": f"torch.profiler unavailable: {type(exc).__name__}"}
     if kroof is not None and "frac" in kroof:
         roof = kroof
+        if roof.get("bound") == "hbm":
+            roof["traffic"], roof["traffic_source"] = profiled_kernel_traffic(roof.get("kernel"), desc)
     elif flops is not None:
         achieved = flops / (step_ms * 1e-3) / 1e12
         roof = {"bound": "valu", "kernel": dom, "achieved": achieved, "peak": VALU_PEAK_TFLOPS, "unit": "TFLOP/s",

@@ -46,9 +46,16 @@ def build(force=False, verbose=False, defines=(), out=None):
     objdir = os.path.join(os.path.dirname(lib), "obj", tag)
     os.makedirs(objdir, exist_ok=True)
 
+    headers = [d for d in deps if not d.endswith(".hip")]
+    hdr_time = max(os.path.getmtime(d) for d in headers if os.path.exists(d))
+
     def compile_one(s):
         obj = os.path.join(objdir, s.replace(".hip", ".o"))
-        cmd = [hipcc, *FLAGS, *["-D" + d for d in defines], "-c", os.path.join(CSRC, s), "-o", obj]
+        src = os.path.join(CSRC, s)
+        # an object newer than its source and every header is reused (per-object staleness)
+        if not force and os.path.exists(obj) and os.path.getmtime(obj) >= max(os.path.getmtime(src), hdr_time):
+            return obj
+        cmd = [hipcc, *FLAGS, *["-D" + d for d in defines], "-c", src, "-o", obj]
         if verbose:
             print(" ".join(cmd), flush=True)
         subprocess.run(cmd, check=True)

@@ -10,7 +10,7 @@ HMM355_API const char* hmm355_strerror(int code) {
     case HMM355_E_STATES: return "number of states outside [1, 256]";
     case HMM355_E_SHAPE: return "invalid shape (T < 1 or size overflow)";
     case HMM355_E_WORKSPACE: return "workspace too small";
-    case HMM355_E_DURATION: return "max_duration outside [1, 255]";
+    case HMM355_E_DURATION: return "HSMM max_duration outside [1, 127] (or above 63 with more than 64 states)";
     default: break;
   }
   if (code > 0) return hipGetErrorString(static_cast<hipError_t>(code));

@@ -3,6 +3,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <type_traits>
+
 #include "../../include/hmm355.h"
 
 #define HMM355_API extern "C" __attribute__((visibility("default")))
@@ -33,6 +35,15 @@ __device__ __forceinline__ unsigned long long stamp() {
 template <typename T>
 __device__ __forceinline__ void keep(T& v) { asm volatile("" : "+v"(v)); }
 constexpr int kAbl = HMM355_ABL;
+
+// compile-time loop: f(integral_constant<int, J>) for J in [B, E)
+template <int J, int E, typename F>
+__device__ __forceinline__ void static_for(F&& f) {
+  if constexpr (J < E) {
+    f(std::integral_constant<int, J>{});
+    static_for<J + 1, E>(f);
+  }
+}
 
 // ---- DPP: row_newbcast:N — every lane of a 16-lane row receives lane N of that row. ----
 template <int N>

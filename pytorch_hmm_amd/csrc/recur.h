@@ -78,6 +78,13 @@ __device__ __forceinline__ float wave_max_bcast(float x) {
   return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, x), 63));
 }
 
+// v_writelane_b32: lane LANE of dst takes the (wave-uniform) value v; the lane is an inline
+// constant (no s_mov: a single wave issues one instruction per issue cycle whatever its type).
+template <int LANE>
+__device__ __forceinline__ void writelane_c(float& dst, float v) {
+  asm("v_writelane_b32 %0, %1, %2" : "+v"(dst) : "s"(v), "i"(LANE));
+}
+
 // ---- one-instruction shifted window terms (DPP on src0; a lane whose DPP source falls off
 // the 64-lane wave is disabled and keeps the destination's previous value)
 #define HMM355_DPP_OP(name, op, ctrl)                                                         \
@@ -1047,13 +1054,18 @@ __device__ __forceinline__ void band_chain(const RecArgs& a, float* lds, int b, 
 
   // UA: uniform floor (alpha), a compile-time branch: a runtime one splits every unrolled
   // step into basic blocks whose joins wait for all outstanding LDS reads
-  auto step = [&](int q, int jj, bool last_in_block, auto UA) {
-    float* row = lds + C::OFF_RING + ((q - 1) & (C::RING - 1)) * NP;
+  // Per-step LDS addresses come from per-block bases (row / emission slots of step jj are
+  // base + jj * NP: immediate offsets), and the step's normaliser c (FB) / floor maximum M
+  // (fused Viterbi psi) goes into lane jj of `blk` by v_writelane, stored once per block
+  // (lanes < 16, after the last step): no per-step address arithmetic or scalar-to-vector
+  // moves on the chain.
+  auto step = [&](int q, int jj, bool last_in_block, auto UA, float* row, const float* enext, float& blk,
+                  auto wlane) {
     st(row + NB * l, y);  // row q-1: flushed by the helpers, window source in LDS mode
     float eo[NB];
 #pragma unroll
     for (int j = 0; j < NB; ++j) eo[j] = en[j];
-    if (!last_in_block) ld(erow(q + 1 - EL), en);
+    if (!last_in_block) ld(enext, en);
     float acc[NB], src[NB];
     float cs = 0.f, scale = 1.f;
     if (KIND == kFbBeta) {  // the product input is y = v * e_{q-1} (hmm.py:113-115)
@@ -1086,13 +1098,13 @@ __device__ __forceinline__ void band_chain(const RecArgs& a, float* lds, int b, 
       for (int j = 0; j < NB; ++j) { src[j] = y[j]; g = fmaxf(g, y[j] + fl[j]); }
       const float M = wave_max_bcast(g);
       // fused psi: M_q = max_i fl(delta_{q-1,i} + r_i) is also psi row q's floor maximum
-      if constexpr (FUSE) lds[C::OFF_SC + 64 * ((q - 1) & (C::RING - 1)) + l] = M;
+      if constexpr (FUSE) wlane(blk, M);
 #pragma unroll
       for (int j = 0; j < NB; ++j) acc[j] = M;
     }
     if (FB) {
       scale = __builtin_amdgcn_rcpf(cs);
-      lds[C::OFF_SC + 64 * ((q - 1) & (C::RING - 1)) + l] = cs;  // c_{q-1}: one conflict-free store
+      wlane(blk, cs);  // c_{q-1}
     }
     if constexpr (TW > 0) {
 #pragma unroll
@@ -1126,11 +1138,32 @@ __device__ __forceinline__ void band_chain(const RecArgs& a, float* lds, int b, 
       const int q0 = kb * 16 < 1 ? 1 : kb * 16;
       const int q1 = (kb + 1) * 16 < T ? (kb + 1) * 16 : T;
       if (q0 < q1) ld(erow(q0 - EL), en);
+      // step jj of this block writes row 16kb + jj - 1: slot (16kb & 63) + jj - 1 for jj >= 1
+      // (no wrap inside a block), slot (16kb - 1) & 63 for jj = 0; it loads the emission row
+      // of step 16kb + jj + 1 - EL, slot (kb % 3) * 16 + jj + 1 - EL of the staging ring
+      float* rbase = lds + C::OFF_RING + ((16 * kb) & (C::RING - 1)) * NP;
+      float* rwrap = lds + C::OFF_RING + ((16 * kb - 1) & (C::RING - 1)) * NP;
+      const float* ebase = lds + C::OFF_EMIS + ((kb % 3) * 16 + 1 - EL) * NP + NB * l;
+      float blk = 0.f;
       if (q0 == kb * 16 && q1 == kb * 16 + 16) {
-#pragma unroll
-        for (int jj = 0; jj < 16; ++jj) step(kb * 16 + jj, jj, jj == 15, UA);
+        static_for<0, 16>([&](auto JJ) {
+          constexpr int jj = decltype(JJ)::value;
+          step(kb * 16 + jj, jj, jj == 15, UA, jj == 0 ? rwrap : rbase + (jj - 1) * NP, ebase + jj * NP, blk,
+               [](float& d, float v) { writelane_c<jj>(d, v); });
+        });
+        // the block's normalisers / floor maxima: lane jj -> row 16kb + jj - 1 (entry 0 of its
+        // 64-float slot, where rec_ls_scan / the psi waves / fbpair's scan read it)
+        if constexpr (FB || FUSE) {
+          if (l < 16) lds[C::OFF_SC + 64 * ((16 * kb + l - 1) & (C::RING - 1))] = blk;
+        }
       } else {
-        for (int q = q0; q < q1; ++q) step(q, q - kb * 16, q + 1 == q1, UA);
+        // first and last (partial) blocks: one store per step, as it is computed
+        for (int q = q0; q < q1; ++q) {
+          const int jj = q - kb * 16;
+          float* sc = lds + C::OFF_SC + 64 * ((q - 1) & (C::RING - 1));
+          step(q, jj, q + 1 == q1, UA, jj == 0 ? rwrap : rbase + (jj - 1) * NP, ebase + jj * NP, blk,
+               [sc](float&, float v) { *sc = v; });
+        }
       }
       if (!(kAbl & 16384)) lds_barrier();  // B_{kb+1}: block kb+1 staged by the helpers, rows of block kb-1 written
     }
@@ -1267,7 +1300,7 @@ __device__ __forceinline__ void rec_band(const RecArgs& a, float* lds, int b, co
             const float4 v4 = *reinterpret_cast<const float4*>(drow + NB * l);
             yv[0] = v4.x; yv[1] = v4.y; yv[2] = v4.z; yv[3] = v4.w;
           }
-          const float M = lds[C::OFF_SC + 64 * rho + l];
+          const float M = lds[C::OFF_SC + 64 * rho];  // the chain's floor maximum of row rho (broadcast read)
 #pragma unroll
           for (int j = 0; j < NB; ++j)
 #pragma unroll

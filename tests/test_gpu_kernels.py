@@ -167,7 +167,8 @@ def test_hsmm_bitexact_given_lp(name):
     assert np.array_equal(scores.cpu().numpy(), g["scores"])
 
 
-@pytest.mark.parametrize("seed,T,S,Dm", [(1, 60, 6, 9), (2, 45, 4, 20), (3, 80, 9, 7), (4, 130, 12, 33)])
+@pytest.mark.parametrize("seed,T,S,Dm", [(1, 60, 6, 9), (2, 45, 4, 20), (3, 80, 9, 7), (4, 130, 12, 33),
+                                         (5, 150, 90, 50), (6, 100, 30, 110)])
 def test_hsmm_ties_vs_c_oracle(seed, T, S, Dm):
     """Coarse values (many equal totals): the first-candidate rule and the backtrace's
     re-resolution of earlier candidates that round to the same total."""
@@ -175,15 +176,23 @@ def test_hsmm_ties_vs_c_oracle(seed, T, S, Dm):
     lp = np.round(-(rng.random((2, T, S)) * 8 + 4), 1).astype(np.float32)
     dur = np.round(np.log(rng.random((S, Dm)) + 1e-3), 1).astype(np.float32)
     logT = np.round(np.log(rng.random((S, S)) + 1e-3), 1).astype(np.float32)
-    cs, csc = O.c_hsmm(lp, dur, logT, literal=True)
+    # the literal 5-deep loop where it is cheap; the reorganised C form (proven equal to it in
+    # tests/test_oracle.py) for the large geometries
+    cs, csc = O.c_hsmm(lp, dur, logT, literal=S * Dm <= 400)
     o = ops()
     states, scores = o.hsmm_viterbi(t(lp), t(dur), t(logT))
     assert np.array_equal(states.cpu().numpy(), cs)
     assert np.array_equal(scores.cpu().numpy(), csc)
 
 
-@pytest.mark.parametrize("B,T,S,Dm", [(2, 150, 16, 12), (1, 300, 64, 40), (3, 70, 7, 63)])
-def test_hsmm_vs_c_oracle(B, T, S, Dm):
+# every kernel geometry (csrc/hsmm.hip hsmm_cfg): (16,4,64) S <= 64 / Dmax <= 63, (8,16,64)
+# Dmax <= 127, (4,16,128) S <= 128 / Dmax <= 63; for S <= 64 / Dmax <= 63 both the default 8-lane
+# (8,8,64) form and HMM355_HSMM_SUB=16's 16-lane one
+@pytest.mark.parametrize("sub", ["8", "16"])
+@pytest.mark.parametrize("B,T,S,Dm", [(2, 150, 16, 12), (1, 300, 64, 40), (3, 70, 7, 63), (2, 260, 40, 100),
+                                      (1, 200, 100, 50), (2, 180, 128, 63), (1, 90, 65, 63), (2, 130, 3, 127)])
+def test_hsmm_vs_c_oracle(B, T, S, Dm, sub, monkeypatch):
+    monkeypatch.setenv("HMM355_HSMM_SUB", sub)
     rng = np.random.default_rng(T + S + Dm)
     lp = (-(rng.random((B, T, S), dtype=np.float32) * 40 + 80)).astype(np.float32)
     dur = np.log(rng.random((S, Dm), dtype=np.float32) + np.float32(1e-8)).astype(np.float32)

@@ -96,5 +96,13 @@ def test_argument_rejection_before_launch(L):
     # HSMM: duration table out of range
     rc = L.hmm355_hsmm_viterbi_f32(fake, fake, fake, 1, 10, 4, 0, fake, fake, fake, 1 << 30, None)
     assert rc == d["HMM355_E_DURATION"]
+    rc = L.hmm355_hsmm_viterbi_f32(fake, fake, fake, 1, 10, 4, 128, fake, fake, fake, 1 << 30, None)
+    assert rc == d["HMM355_E_DURATION"]
+    rc = L.hmm355_hsmm_viterbi_f32(fake, fake, fake, 1, 10, 129, 8, fake, fake, fake, 1 << 30, None)
+    assert rc == d["HMM355_E_STATES"]
+    rc = L.hmm355_hsmm_viterbi_f32(fake, fake, fake, 1, 10, 65, 64, fake, fake, fake, 1 << 30, None)
+    assert rc == d["HMM355_E_DURATION"]   # S > 64 takes Dmax <= 63
+    assert L.hmm355_hsmm_workspace_bytes(2, 100, 64, 127) > 0 and L.hmm355_hsmm_workspace_bytes(2, 100, 128, 63) > 0
+    assert L.hmm355_hsmm_workspace_bytes(2, 100, 129, 8) == 0 and L.hmm355_hsmm_workspace_bytes(2, 100, 65, 64) == 0
     # B == 0 is a no-op success
     assert L.hmm355_viterbi_f32(None, 0, None, None, 0, 10, 8, None, None, None, None, 0, None) == 0

@@ -8,6 +8,7 @@ cd $GRAFT_REPO_ROOT
 TAG=${1:-r1}; shift
 ARGS="$@"
 export TMPDIR=/tmp
+export HMM355_BENCH_NO_KPROF=1   # no torch.profiler inside the rocprofv3 passes
 D=gpurun_out/prof_$TAG
 mkdir -p $D
 timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $D/trace -o run -- python3 bench.py --steps 20 --warmup 3 --cpu-seconds 0 $ARGS > $D/bench_trace.log 2>&1 &&
