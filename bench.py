@@ -515,6 +515,7 @@ class NsStep:
         self.out = [dict() for _ in range(self.nbuf)]
         self.graph = [dict() for _ in range(self.nbuf)]
         self.k = 0
+        self.timing = None  # {op: [(start, end) events]} while set: each op bracketed on its stream
         if self.cuda:
             s_fb = torch.cuda.Stream(dev)
             self.stream = {"fb": s_fb, "vit": s_fb if serial else torch.cuda.Stream(dev)}
@@ -560,10 +561,17 @@ class NsStep:
             if self.read_done[slot] is not None:
                 s_.wait_event(self.read_done[slot])
             with torch.cuda.stream(s_):
+                if self.timing is not None:
+                    e0 = torch.cuda.Event(enable_timing=True)
+                    e0.record(s_)
                 if self.use_graph:
                     self.graph[slot][n].replay()
                 else:
                     self.out[slot][n] = self.ops[n]()
+                if self.timing is not None:
+                    e1 = torch.cuda.Event(enable_timing=True)
+                    e1.record(s_)
+                    self.timing[n].append((e0, e1))
                 if self.gatherer is not None:
                     self.op_end[slot][n].record(s_)
         if self.gatherer is not None:
@@ -644,6 +652,10 @@ def main():
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
+    # per-op launch durations for the roofline: HIP events on each op's own stream around its
+    # graph replay, over the timed steps (an event pair costs the step ~1-2 us of queue work;
+    # the wall clock below is what `value` uses)
+    step.timing = {n: [] for n in step.names}
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
@@ -656,19 +668,7 @@ def main():
         tt = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         elapsed = float(tt.item())
-
-    # per-op launch durations for the roofline: the same ops, eagerly, HIP events on the
-    # stream each op's kernels run on
-    ev = {k: [] for k in step.names}
-    for _ in range(min(args.steps, 10)):
-        for n in step.names:
-            with torch.cuda.stream(step.stream[n]):
-                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-                e0.record()
-                step.ops[n]()
-                e1.record()
-                ev[n].append((e0, e1))
-    torch.cuda.synchronize(dev)
+    ev, step.timing = step.timing, None
     fb_ms = sum(a.elapsed_time(b) for a, b in ev["fb"]) / len(ev["fb"])
     vit_ms = sum(a.elapsed_time(b) for a, b in ev["vit"]) / len(ev["vit"])
     global_b = args.batch if args.strong else B * world

@@ -218,6 +218,11 @@ struct RecArgs {
 constexpr int kPsiChunk = 64;
 template <int NP>
 constexpr bool kVitFused = RC<NP>::NW >= 6;
+// threads of the Viterbi chain kernel: the fused banded chain runs 16 waves (rec_band: two
+// staging helpers and two psi waves on each of SIMDs 1..3); the dense chains use the first
+// RC<NP>::NW waves and the rest exit at once
+template <int NP>
+constexpr int kVitNT = kVitFused<NP> ? 1024 : RC<NP>::NT;
 
 template <int KIND>
 __device__ __forceinline__ int rec_tau(int q, int T) {
@@ -1071,19 +1076,21 @@ __device__ __forceinline__ void band_chain(const RecArgs& a, float* lds, int b, 
     if (KIND == kFbBeta) {  // the product input is y = v * e_{q-1} (hmm.py:113-115)
       float t = 0.f;
 #pragma unroll
-      for (int j = 0; j < NB; ++j) { src[j] = y[j] * eo[j]; t += src[j]; }
+      for (int j = 0; j < NB; ++j) { src[j] = y[j] * eo[j]; t = j == 0 ? src[j] : t + src[j]; }
       if (TW == 0) st(ybuf + ((q - 1) & 1) * NP + NB * l, src);
       cs = wave_sum_bcast(t);
+      // the floor term fl_j * c is folded into the end: y_j = fl_j + (window sum) / c, one fma
+      // after the reduction instead of a multiply before the window fmas and one after
 #pragma unroll
-      for (int j = 0; j < NB; ++j) acc[j] = fl[j] * cs;
+      for (int j = 0; j < NB; ++j) acc[j] = 0.f;
     } else if (KIND == kFbAlpha) {
       float t = 0.f;
 #pragma unroll
-      for (int j = 0; j < NB; ++j) { src[j] = y[j]; t += y[j]; }
+      for (int j = 0; j < NB; ++j) { src[j] = y[j]; t = j == 0 ? y[j] : t + y[j]; }
       cs = wave_sum_bcast(t);
       float sw;
       if constexpr (decltype(UA)::value) {
-        sw = afl0 * cs;
+        sw = 0.f;  // uniform floor: folded into the end as for beta, y = (afl0 + wsum / c) e
       } else {
         float tw = 0.f;
 #pragma unroll
@@ -1127,9 +1134,14 @@ __device__ __forceinline__ void band_chain(const RecArgs& a, float* lds, int b, 
 #pragma unroll
     for (int j = 0; j < NB; ++j) {
       // padded states: the staged emission is 0 (FB) / -inf (Viterbi) and the floors 0
-      if (KIND == kFbAlpha) y[j] = acc[j] * (scale * eo[j]);
-      else if (KIND == kFbBeta) y[j] = acc[j] * scale;
-      else y[j] = acc[j] + eo[j];
+      if (KIND == kFbAlpha) {
+        if constexpr (decltype(UA)::value) y[j] = fmaf(acc[j], scale, afl0) * eo[j];
+        else y[j] = acc[j] * (scale * eo[j]);
+      } else if (KIND == kFbBeta) {
+        y[j] = fmaf(acc[j], scale, fl[j]);
+      } else {
+        y[j] = acc[j] + eo[j];
+      }
     }
   };
 
@@ -1207,15 +1219,26 @@ __device__ __forceinline__ void rec_band(const RecArgs& a, float* lds, int b, co
   // wave 4, beside the chain on SIMD 0: measured alone, 3 helpers 259 us, 4 helpers 238 us,
   // the separate log pass 248 us (B=32, T=2000, N=128); 3 of the 8 virtual waves on wave 4
   // and 5 on waves 1..3 was slower (262 us).
-  constexpr int NH = (KIND == kVit && C::NW >= 8) ? 4 : 3;  // (NP = 64: a 4-wave workgroup)
-  constexpr int HV = (C::NW + NH - 1) / NH;  // virtual staging waves per helper
-  auto vw_of = [&](int w, int h) -> int { return (w - 1) + h * NH; };  // virtual staging wave h of helper w
-  constexpr bool FB = KIND != kVit;
-  // fused psi (kVitFused): helpers 1..3 also form the psi rows of the block they flush
+  // Round 3, fused-psi Viterbi (kVitFused, NP >= 128): the workgroup has 16 waves (kVitWideNT).
+  // With the chain's step down to ~95 ns its helpers had become the limit (one process,
+  // B=32 T=2000 N=128: Viterbi op 242 us; without the emission log 209, without the psi rows
+  // 195, neither 189; tools/ablate.py, profiles/r3g_ablate.log), so SIMDs 1..3 each carry
+  // TWO staging helpers (waves 1,2,3 and 9,10,11) and TWO psi waves (5,6,7 and 13,14,15), and
+  // nothing shares the chain's SIMD: waves 4, 8, 12 (w = 0 mod 4, the chain's SIMD) exit.
   constexpr bool FUSE = KIND == kVit && kVitFused<NP>;
+  constexpr bool WIDE = FUSE;
+  constexpr int NH = WIDE ? 6 : ((KIND == kVit && C::NW >= 8) ? 4 : 3);  // (NP = 64: a 4-wave workgroup)
+  constexpr int HV = (C::NW + NH - 1) / NH;  // virtual staging waves per helper
   const int tid = threadIdx.x;
   const int w = tid >> 6, l = tid & 63;
-  if (w > NH && !(FUSE && w >= 5 && w <= 7)) return;  // 5..7: psi-only waves (SIMDs 1..3)
+  // role of wave w: staging helper index hi (0 .. NH-1), psi wave index, or neither (exit)
+  const int grp = (w >> 3) * 3 + (w & 3) - 1;  // WIDE: waves 1,2,3 / 5,6,7 -> 0,1,2; 9,.. / 13,.. -> 3,4,5
+  const bool stager = WIDE ? ((w & 4) == 0 && (w & 3) != 0) : (w > 0 && w <= NH);
+  const bool psiw = WIDE && (w & 4) != 0 && (w & 3) != 0;
+  const int hi = WIDE ? grp : w - 1;
+  auto vw_of = [&](int h) -> int { return hi + h * NH; };  // virtual staging wave h of this helper
+  constexpr bool FB = KIND != kVit;
+  if (w != 0 && !stager && !psiw) return;  // ended waves take no part in s_barrier
   const int T = a.T, N = a.N;
   const int nblocks = (T + 15) / 16;
   double base = (KIND == kFbBeta && a.bscale) ? (double)a.bscale[b] : 0.0;
@@ -1224,11 +1247,11 @@ __device__ __forceinline__ void rec_band(const RecArgs& a, float* lds, int b, co
   // three register sets: the loads of block kb+3 are issued during block kb, so each has two
   // blocks (~3 us) to land before it is staged
   float er0[HV][5], er1[HV][5], er2[HV][5];
-  if (w > 0 && w <= NH) {
+  if (stager) {
     if (KIND == kVit) rec_logt_fill<NP>(lds, l);
 #pragma unroll
     for (int h = 0; h < HV; ++h) {
-      const int vw = vw_of(w, h);
+      const int vw = vw_of(h);
       if (vw < C::NW) {
         float er[5];
         rec_load<NP, KIND>(a, b, 0, vw, l, er);
@@ -1281,8 +1304,8 @@ __device__ __forceinline__ void rec_band(const RecArgs& a, float* lds, int b, co
     auto psi_rows = [&](int bk) {
       if constexpr (FUSE) {
         if (bk < 0 || (kAbl & 128)) return;
-        constexpr int NPW = 3, PR = (16 + NPW - 1) / NPW;
-        const int hw = w - 5;
+        constexpr int NPW = WIDE ? 6 : 3, PR = (16 + NPW - 1) / NPW;
+        const int hw = grp;
 #pragma unroll
         for (int m = 0; m < PR; ++m) {
           const int r = hw + NPW * m;
@@ -1350,7 +1373,7 @@ __device__ __forceinline__ void rec_band(const RecArgs& a, float* lds, int b, co
       if (!(kAbl & 32) && kb >= 2) lsv = rec_ls_scan<NP, KIND>(a, lds, b, kb - 2, base, w == 1);
 #pragma unroll
       for (int h = 0; h < HV; ++h) {
-        const int vw = vw_of(w, h);
+        const int vw = vw_of(h);
         if (vw < C::NW && !(kAbl & 32768)) {
           if (!(kAbl & 64)) {
             rec_stage<NP, KIND>(a, lds, kb + 1, vw, l, ernext[h]);
@@ -1362,7 +1385,7 @@ __device__ __forceinline__ void rec_band(const RecArgs& a, float* lds, int b, co
       if (!(kAbl & 16384)) lds_barrier();
     };
     if constexpr (FUSE) {
-      if (w > NH) {  // psi-only waves: one compact loop, same barrier count as the helpers
+      if (psiw) {  // psi-only waves: one compact loop, same barrier count as the helpers
         for (int kb = 0; kb < nblocks; ++kb) {
           psi_rows(kb - 2);
           if (!(kAbl & 16384)) lds_barrier();
@@ -1387,7 +1410,7 @@ __device__ __forceinline__ void rec_band(const RecArgs& a, float* lds, int b, co
     const float lsv1 = rec_ls_scan<NP, KIND>(a, lds, b, nblocks - 1, base, w == 1);
 #pragma unroll
     for (int h = 0; h < HV; ++h) {
-      const int vw = vw_of(w, h);
+      const int vw = vw_of(h);
       if (vw < C::NW) {
         if (nblocks >= 2) rec_flush<NP, KIND>(a, lds, b, nblocks - 2, l + 64 * vw, lsv2);
         rec_flush<NP, KIND>(a, lds, b, nblocks - 1, l + 64 * vw, lsv1);
@@ -1433,9 +1456,12 @@ __device__ __forceinline__ void rec_dispatch(const RecArgs& a, float* lds, int b
     case 16 * 3 - 1 + 2: rec_band<NP, KIND, 2, -1, 3>(a, lds, b, a.band); break;
     case 16 * 3 + 0 + 2: rec_band<NP, KIND, 2, 0, 3>(a, lds, b, a.band); break;
     default:
+      if (threadIdx.x >= RC<NP>::NT) return;  // (a wider Viterbi launch: waves beyond NW end here)
       // (diagnostic ablation bits: 1 << 25 the round-2 register-operand chain (NP <= 128),
       // 1 << 24 the DPP-broadcast chain)
-      if constexpr (!(kAbl & (3 << 24))) rec_run_rb<NP, KIND>(a, lds, b);
+      // (NP = 256 keeps the DPP-broadcast chain: 16 waves leave 128 VGPRs a lane, too few for
+      // the register-blocked slices)
+      if constexpr (NP <= 128 && !(kAbl & (3 << 24))) rec_run_rb<NP, KIND>(a, lds, b);
       else if constexpr (NP <= 128 && !(kAbl & (1 << 24))) rec_run_bc<NP, KIND>(a, lds, b);
       else rec_run<NP, KIND>(a, lds, b);
       break;

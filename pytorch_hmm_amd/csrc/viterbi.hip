@@ -34,7 +34,7 @@
 namespace hmm355 {
 
 template <int NP>
-__global__ void __launch_bounds__(RC<NP>::NT) vit_fwd_kernel(RecArgs ra) {
+__global__ void __launch_bounds__(kVitNT<NP>) vit_fwd_kernel(RecArgs ra) {
   extern __shared__ __attribute__((aligned(16))) float lds[];
   rec_dispatch<NP, kVit>(ra, lds, blockIdx.x);
 }
@@ -235,7 +235,7 @@ static hipError_t launch_vit(const VitArgs& va, bool prep, hipStream_t sm) {
   }
   RecArgs ra{va.obs, va.log_P, va.init, va.delta, nullptr, nullptr, va.B, va.T, va.N, va.obs_mode, va.N, va.band,
              nullptr, nullptr, va.psi};
-  hipLaunchKernelGGL(vit_fwd_kernel<NP>, dim3(va.B), dim3(RC<NP>::NT), kExclusiveLds, sm, ra);
+  hipLaunchKernelGGL(vit_fwd_kernel<NP>, dim3(va.B), dim3(kVitNT<NP>), kExclusiveLds, sm, ra);
   e = hipGetLastError();
   if (e != hipSuccess) return e;
   // banded psi stages the chunk's delta rows in LDS (dynamic, kChunk x NP floats)
