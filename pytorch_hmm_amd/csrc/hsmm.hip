@@ -342,10 +342,12 @@ __device__ __forceinline__ float hs_obs_sum_lds(const float* col, int d) {
   return r;
 }
 
-// R >= the longest duration; every lane owns the candidates d' = l + 1 + 64k, k < R/64
-template <int R>
+// R >= the longest duration; every lane owns the candidates d' = l + 1 + 64k, k < R/64, and
+// the predecessor states s' = l + 64k, k < SMAX/64
+template <int R, int SMAX>
 __global__ void __launch_bounds__(64) hsmm_backtrace_kernel(HsArgs a) {
   constexpr int K = R / 64;
+  constexpr int KS = (SMAX + 63) / 64;
   __shared__ float pcol[R];  // lp[tau - i][s1], i < Dm: the predecessor's candidate column
   __shared__ float ccol[R];  // lp[t - i][cs], i < cd: the current segment, newest first
   const int b = blockIdx.x, l = threadIdx.x;
@@ -380,13 +382,20 @@ __global__ void __launch_bounds__(64) hsmm_backtrace_kernel(HsArgs a) {
         if (pin) pcol[e] = pv;
         if (e < cd) ccol[e] = lp[(size_t)(t - e) * S + cs];
       }
-      float xo = -INFINITY;  // max over s' < ns, s' != cs of fl(Dm[tau][s'] + logT[s'][cs])
-      for (int sp = l; sp < ns; sp += 64) {
-        const float dm = Db[(size_t)tau * S + sp];
-        const float ltl = a.logT[(size_t)sp * S + cs];
-        if (sp != cs && dm != -INFINITY) xo = fmaxf(xo, dm + ltl);
+      // max over s' < ns, s' != cs of fl(Dm[tau][s'] + logT[s'][cs]) (loads in the same round trip)
+      float dm[KS], ltl[KS];
+#pragma unroll
+      for (int k = 0; k < KS; ++k) {
+        const int sp = l + 64 * k;
+        const bool ok = sp < ns;
+        dm[k] = ok ? Db[(size_t)tau * S + sp] : -INFINITY;
+        ltl[k] = ok ? a.logT[(size_t)sp * S + cs] : 0.f;
       }
       __syncthreads();
+      float xo = -INFINITY;
+#pragma unroll
+      for (int k = 0; k < KS; ++k)
+        if (l + 64 * k != cs && dm[k] != -INFINITY) xo = fmaxf(xo, dm[k] + ltl[k]);
       // first d' of s1 whose fl(delta + logT) equals M, and the best earlier total (xb)
       float dv[K];
       nd = 0;
@@ -470,7 +479,7 @@ static hipError_t launch_hsmm(const HsArgs& ha, hipStream_t st) {
   hipLaunchKernelGGL((hsmm_fwd_kernel<SUB, NJ, SMAX>), dim3(ha.B), dim3(G::NT), lds, st, ha);
   e = hipGetLastError();
   if (e != hipSuccess) return e;
-  hipLaunchKernelGGL(hsmm_backtrace_kernel<G::R>, dim3(ha.B), dim3(64), 0, st, ha);
+  hipLaunchKernelGGL((hsmm_backtrace_kernel<G::R, SMAX>), dim3(ha.B), dim3(64), 0, st, ha);
   return hipGetLastError();
 }
 
