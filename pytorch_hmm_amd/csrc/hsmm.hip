@@ -12,26 +12,34 @@
 //   g(x) = fl(fl(x + o) + u) is monotone: the literal max over candidates is g(M).  The
 //   literal strict-> argmax is the first candidate (s' asc, d' asc) whose g(x) equals g(M):
 //   the first candidate attaining M (p1) unless an EARLIER candidate rounds to the same
-//   final value — so the kernel stores p1 and xb = max over the candidates before p1, and
-//   the backtrace re-resolves exactly (rare) only for segments on the decoded path.
+//   final value — so the forward stores only M and Dm, and the backtrace finds p1 and
+//   xb = max over the candidates before p1 for the segments on the decoded path and
+//   re-resolves exactly there (rare).
 //   obs_sum is torch-CPU's order for a strided slice of length d: four accumulators over
 //   whole groups of 4, the tail folded into the first, then ((a0+a1)+a2)+a3.
 //
 // hsmm_fwd_kernel<SUB, NJ, SMAX>: one workgroup per sequence (SMAX * SUB threads), the segment
 //   END time t as the loop index (semimarkov.hip's layout): SUB lanes (a DPP group) per state;
 //   lane `sub` owns the start-time slots k = NJ*sub + j (mod R = SUB*NJ) of its state.  A live
-//   segment's torch-order obs_sum state (the four group accumulators, the pending group and
-//   the tail sum) and its predecessor score M stay in the slot's registers for the segment's
-//   life, so a step reads one lp row, writes delta's per-state maximum Dm for the predecessor
-//   phase, and meets at ONE barrier.  Per end time t it stores M[t][s] (the best
-//   fl(delta + logT) over predecessors ending at t, for segments starting at t+1), the first
-//   s' attaining it, and Dm[t][s].  Geometries: (16, 4, 64) for the config-5 class (S <= 64,
-//   Dmax <= 63), (8, 8, 64) the same with 8-lane groups, (8, 16, 64) for Dmax <= 127 and
-//   (4, 16, 128) for 65 <= S <= 128 with Dmax <= 63.
+//   segment's torch-order obs_sum state (the four group accumulators and the tail sum) and its
+//   predecessor score M stay in the slot's registers for the segment's life, so a step reads
+//   one lp row, writes delta's per-state maximum Dm for the predecessor phase, and meets at ONE
+//   barrier.  Slots j and j + NJ/2 run as one packed-fp32 pair (v_pk_add_f32: the obs_sum and
+//   delta adds of two segments per instruction; with NJ/2 a multiple of 4 both halves take the
+//   same accumulator update).  The branchy literal conditions are folded into the data: a slot
+//   not yet started has M = -inf, the slot starting at time 0 has M = 0 (fl(0 + o) == o), and
+//   durations beyond Dmax or padding states read -inf from the duration table.  Per end time t
+//   the kernel stores M[t][s] (the best fl(delta + logT) over predecessors ending at t, for
+//   segments starting at t+1) and Dm[t][s].  Geometries: (8, 8, 64) for the config-5 class
+//   (S <= 64, Dmax <= 63), (4, 16, 64) / (16, 4, 64) the same with 4- and 16-lane groups, (8, 16, 64) for Dmax <= 127 and (4, 16, 128) for 65 <= S <= 128 with
+//   Dmax <= 63.
 // hsmm_backtrace_kernel: one wave per sequence walks the segments (hsmm.py:331-352); for each
-//   segment it recomputes, bit-identically, the candidate deltas of the winning s' to find
-//   the first d' and xb (the best total of the earlier candidates), and re-resolves the rare
-//   case where an earlier candidate rounds to the same total.
+//   segment it finds the first predecessor state attaining M from the stored Dm row (the
+//   forward's own candidate values), recomputes, bit-identically, that state's candidate
+//   deltas to find the first d' and xb (the best total of the earlier candidates), and
+//   re-resolves the rare case where an earlier candidate rounds to the same total.  Two
+//   dependent global round trips per segment; the tables sit in LDS and the next segment's
+//   obs_sum is the one this segment's candidate search already formed.
 #include <stdlib.h>
 
 #include <type_traits>
@@ -44,6 +52,8 @@ constexpr int kHsL = 128;    // lp row ring (two 64-row chunks)
 constexpr int kHsSMax = 128; // states (the largest geometry below)
 constexpr int kHsDMax = 127; // durations (slot ring R = 128)
 
+typedef float hs_f2 __attribute__((ext_vector_type(2)));
+
 // Kernel geometry: SUB lanes per state (one DPP group), NJ start-time slots per lane, SMAX
 // states per workgroup.  R = SUB * NJ slots (a segment's duration is < R), NT threads.
 template <int SUB, int NJ, int SMAX>
@@ -52,7 +62,11 @@ struct HsG {
   static constexpr int NT = SMAX * SUB;
   static constexpr int NPRED = SMAX / SUB;   // predecessor states per lane
   static constexpr int PER = 64 * SMAX / NT; // lp values per thread per 64-row chunk
+  static constexpr int NP2 = NJ / 2;         // packed slot pairs (j, j + NJ/2)
+  static constexpr int DW = R + NJ + 1;      // duration-table row stride (odd: bank spread)
   static_assert(NJ % 4 == 0, "slot position (t - k) & 3 must be a compile-time constant");
+  static_assert((R & (R - 1)) == 0, "slot ring is a power of two");
+  static_assert(NPRED % 4 == 0, "predecessor scores are read as float4");
   static_assert(NT <= 1024, "one workgroup per sequence");
 };
 
@@ -61,7 +75,6 @@ struct HsArgs {
   const float* dur;     // (S,Dm)
   const float* logT;    // (S,S)
   float* Mg;            // (B,T,S): M[t][s], best predecessor total for segments starting at t+1
-  uint8_t* S1;          // (B,T,S): first s' attaining M[t][s]
   float* Dg;            // (B,T,S): Dm[t][s] = max_d delta[t][s][d]
   int* fin;             // (B,2): final (s, d)
   float* scores;        // (B)
@@ -69,12 +82,14 @@ struct HsArgs {
   int B, T, S, Dm;
 };
 
-template <int SMAX, int R>
+template <int SMAX, int DW, int NJ, int NT>
 struct HsLds {
+  float dmx[2][SMAX];    // Dm[t][s'] at q(s') = (s' % SUB) * NPRED + s' / SUB: a lane's
+                         // predecessors are contiguous
   float lpr[kHsL][SMAX];
-  float dur[SMAX][R + 1];
-  float dmx[2][SMAX];
+  float durx[SMAX][DW];  // durx[s][i] = dur[s][(i - NJ) mod R], -inf for d >= Dmax or s >= S
   int fd[SMAX];
+  float vfin[NJ][NT];    // the final step's slot values
 };
 
 // all-reduce over the SUB lanes of a state group (16: one DPP row; 8: half a row; 4: a quad)
@@ -104,26 +119,28 @@ __device__ __forceinline__ int grp_min_i(int v) {
 template <int SUB, int NJ, int SMAX>
 __global__ void __launch_bounds__((HsG<SUB, NJ, SMAX>::NT)) hsmm_fwd_kernel(HsArgs a) {
   using G = HsG<SUB, NJ, SMAX>;
-  constexpr int R = G::R, NT = G::NT;
+  constexpr int R = G::R, NT = G::NT, NP2 = G::NP2, NPRED = G::NPRED, DW = G::DW;
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  HsLds<SMAX, R>& L = *reinterpret_cast<HsLds<SMAX, R>*>(smem);
+  HsLds<SMAX, DW, NJ, NT>& L = *reinterpret_cast<HsLds<SMAX, DW, NJ, NT>*>(smem);
   const int b = blockIdx.x, tid = threadIdx.x;
   const int T = a.T, S = a.S, Dm = a.Dm;
   const int s = tid / SUB, sub = tid % SUB;
   const bool live = s < S;
+  const int q = (s % SUB) * NPRED + s / SUB;
   const float* lp = a.lp + (size_t)b * T * S;
 
-  for (int i = tid; i < SMAX * R; i += NT) {
-    const int r = i / R, d = i % R;
-    L.dur[r][d] = (r < S && d < Dm) ? a.dur[(size_t)r * Dm + d] : -INFINITY;
+  for (int i = tid; i < SMAX * DW; i += NT) {
+    const int r = i / DW, c = i % DW;
+    const int d = (c - NJ) & (R - 1);
+    L.durx[r][c] = (r < S && d < Dm) ? a.dur[(size_t)r * Dm + d] : -INFINITY;
   }
-  float lt[G::NPRED];  // log T[s'][s] for the lane's predecessor states s' = sub + SUB j (-inf: excluded)
+  hs_f2 lt2[NPRED / 2];  // log T[s'][s] for the lane's predecessors s' = sub + SUB j (-inf: excluded)
 #pragma unroll
-  for (int j = 0; j < G::NPRED; ++j) {
+  for (int j = 0; j < NPRED; ++j) {
     const int sp = sub + SUB * j;
     const bool ok = live && sp < S && sp != s;
     const float v = a.logT[ok ? (size_t)sp * S + s : 0];
-    lt[j] = ok ? v : -INFINITY;
+    lt2[j >> 1][j & 1] = ok ? v : -INFINITY;
   }
 
   float rc[G::PER];
@@ -151,127 +168,129 @@ __global__ void __launch_bounds__((HsG<SUB, NJ, SMAX>::NT)) hsmm_fwd_kernel(HsAr
 
   // torch-CPU order of sum(lp[st:st+d, s]) (a strided slice): four accumulators over the
   // whole groups of 4, the tail folded into the first, then ((a0+a1)+a2)+a3.  Per slot:
-  // G = completed-group sums, A0 = G0 + tail.  A group's four elements are the state's last
+  // Gs = completed-group sums, A0 = G0 + tail.  A group's four elements are the state's last
   // four lp values whatever the slot, so they come from one per-lane ring xr (x at time t in
   // xr[t & 3]) when the group closes: G_i += x_{t-3+i} (the same fp32 adds as accumulating
-  // each element into its own accumulator as it arrives).
-  float Gs[NJ][4], A0[NJ], mp[NJ], xr[4] = {0.f, 0.f, 0.f, 0.f};
+  // each element into its own accumulator as it arrives).  (The leading 0 + a0 of torch's
+  // sum is an identity here: a0 is never -0, every accumulator starting from +0.)
+  hs_f2 Gs[NP2][4], A0[NP2], mp[NP2];
 #pragma unroll
-  for (int j = 0; j < NJ; ++j) {
+  for (int p = 0; p < NP2; ++p) {
 #pragma unroll
-    for (int i = 0; i < 4; ++i) Gs[j][i] = 0.f;
-    A0[j] = 0.f;
-    mp[j] = -INFINITY;
+    for (int i = 0; i < 4; ++i) Gs[p][i] = hs_f2{0.f, 0.f};
+    A0[p] = hs_f2{0.f, 0.f};
+    mp[p] = hs_f2{-INFINITY, -INFINITY};  // not started: delta = -inf
   }
-  float Mlast = -INFINITY;
-  // delta of slot j's segment (duration d, start st) ending now, from its updated registers
-  auto slot_val = [&](int j, int d, int st, float u) -> float {
-    float o = 0.f + A0[j];
-    o = o + Gs[j][1];
-    o = o + Gs[j][2];
-    o = o + Gs[j][3];
-    // hsmm.py:269-274 (st == 0: no predecessor) / :304-314; mp == -inf (no predecessor path)
-    // gives (mp + o) + u == -inf since o is finite
-    const float val = st == 0 ? o + u : (mp[j] + o) + u;
-    return (live && d <= Dm && st >= 0) ? val : -INFINITY;
-  };
+  float xr[4] = {0.f, 0.f, 0.f, 0.f};
+  // M handed to the slot that starts next; 0 for the segment starting at t = 0, whose delta
+  // is o + u (hsmm.py:269-274): fl(fl(0 + o) + u) == fl(o + u)
+  float Mlast = 0.f;
+  int Afin = 0;
+  float mxfin = -INFINITY;
 
-  // One end time.  Lane `sub` owns slots k = NJ*sub + j, so the new element's position in its
-  // segment's group of four, (t - k) & 3 = (U - j) & 3 with U = t & 3 (NJ is a multiple of 4),
-  // is a compile-time constant of the unrolled copy: each slot runs only its own accumulator
-  // update.  Branch-free: every LDS read of the step is issued before its first use (a guarded
-  // read ends in its own s_waitcnt, which serialised the duration-table round trips).  Rows
-  // s >= S of the tables hold -inf / 0, so the unguarded reads are in range and inert.
+  // One end time t (U = t % NJ).  Lane `sub` owns slots k = NJ*sub + j, so the new element's
+  // position in its segment's group of four, (t - k) & 3 = (U - j) & 3 (NJ is a multiple of
+  // 4), is a compile-time constant of the unrolled copy, and the only slot that can start at
+  // t is j = U.  Every LDS read of the step is issued before its first use.
   auto end_step = [&](const int t, auto Uc) -> bool {
     constexpr int U = decltype(Uc)::value;
+    const int A = (t - NJ * sub) & (R - 1);  // slot j's age is (A - j) & (R - 1)
     const float x = L.lpr[t % kHsL][s];
-    xr[U] = x;
-    float du[NJ];
-    float mx = -INFINITY;
-    static_for<0, NJ>([&](auto Jc) {
-      constexpr int j = decltype(Jc)::value;
-      du[j] = L.dur[s][(t - (NJ * sub + j)) & (R - 1)];  // dur[s][d - 1], -inf for d > Dm
+    xr[U & 3] = x;
+    const float* drow = &L.durx[s][A + NJ];  // dur[s][age_j] = drow[-j]
+    hs_f2 du[NP2];
+    static_for<0, NP2>([&](auto Pc) {
+      constexpr int p = decltype(Pc)::value;
+      du[p] = hs_f2{drow[-p], drow[-(p + NP2)]};
     });
-    static_for<0, NJ>([&](auto Jc) {
-      constexpr int j = decltype(Jc)::value;
-      const int age = (t - (NJ * sub + j)) & (R - 1);
-      const int d = age + 1, st = t - age;
-      constexpr int pos = (U - j) & 3;  // == age & 3
-      if constexpr (pos == 0) {
-        const bool fresh = age == 0;
+    {
+      constexpr int pf = U % NP2, hf = U / NP2;
+      const bool fresh = A == U;
 #pragma unroll
-        for (int i = 0; i < 4; ++i) Gs[j][i] = fresh ? 0.f : Gs[j][i];
-        mp[j] = fresh ? Mlast : mp[j];
-        A0[j] = Gs[j][0] + x;
-      } else if constexpr (pos == 3) {
+      for (int i = 0; i < 4; ++i) Gs[pf][i][hf] = fresh ? 0.f : Gs[pf][i][hf];
+      mp[pf][hf] = fresh ? Mlast : mp[pf][hf];
+    }
+    const hs_f2 x2 = {x, x};
+    float mx = -INFINITY;
+    float vv[NJ];
+    static_for<0, NP2>([&](auto Pc) {
+      constexpr int p = decltype(Pc)::value;
+      constexpr int pa = (U - p + 4 * NJ) & 3, pb = (U - p - NP2 + 4 * NJ) & 3;
+      if constexpr (pa == pb) {
+        if constexpr (pa == 0) {
+          A0[p] = Gs[p][0] + x2;
+        } else if constexpr (pa == 3) {
 #pragma unroll
-        for (int i = 0; i < 4; ++i) Gs[j][i] = Gs[j][i] + xr[(U - 3 + i) & 3];
-        A0[j] = Gs[j][0];
+          for (int i = 0; i < 4; ++i) {
+            const float xe = xr[(U + 1 + i) & 3];
+            Gs[p][i] = Gs[p][i] + hs_f2{xe, xe};
+          }
+        } else {
+          A0[p] = A0[p] + x2;
+        }
       } else {
-        A0[j] = A0[j] + x;
+        static_for<0, 2>([&](auto Hc) {
+          constexpr int h = decltype(Hc)::value;
+          constexpr int ps = h ? pb : pa;
+          if constexpr (ps == 0) {
+            A0[p][h] = Gs[p][0][h] + x;
+          } else if constexpr (ps == 3) {
+#pragma unroll
+            for (int i = 0; i < 4; ++i) Gs[p][i][h] = Gs[p][i][h] + xr[(U + 1 + i) & 3];
+          } else {
+            A0[p][h] = A0[p][h] + x;
+          }
+        });
       }
-      mx = fmaxf(mx, slot_val(j, d, st, du[j]));
+      hs_f2 a0;
+      if constexpr (pa == 3 && pb == 3) {
+        a0 = Gs[p][0];  // the group just closed: empty tail
+      } else if constexpr (pa != 3 && pb != 3) {
+        a0 = A0[p];
+      } else {
+        a0 = hs_f2{pa == 3 ? Gs[p][0].x : A0[p].x, pb == 3 ? Gs[p][0].y : A0[p].y};
+      }
+      const hs_f2 o = ((a0 + Gs[p][1]) + Gs[p][2]) + Gs[p][3];
+      // hsmm.py:304-314: fl(fl(M + o) + u); mp == -inf (no predecessor path) gives -inf
+      const hs_f2 v = (mp[p] + o) + du[p];
+      vv[p] = v.x;
+      vv[p + NP2] = v.y;
+      mx = fmaxf(mx, fmaxf(v.x, v.y));
     });
     mx = grp_max<SUB>(mx);
     if (sub == 0) {
-      L.dmx[t & 1][s] = mx;  // -inf for the padding states s >= S (read unguarded below)
+      L.dmx[t & 1][q] = mx;  // -inf for the padding states s >= S
       if (live) a.Dg[((size_t)b * T + t) * S + s] = mx;
     }
     if (t == T - 1) {
-      // best over (s asc, d asc) of delta[T-1][s][d-1], strict > (hsmm.py:319-329)
-      int ld = 0x7fff;
+      // the final step's slot values go to LDS (a store cannot be hoisted into every step);
+      // the (s asc, d asc) selection runs after the loop
 #pragma unroll
-      for (int j = 0; j < NJ; ++j) {  // (recomputed here, once, rather than kept live every step)
-        const int age = (t - (NJ * sub + j)) & (R - 1);
-        const int d = age + 1;
-        if (slot_val(j, d, t - age, du[j]) == mx && d < ld) ld = d;
-      }
-      ld = grp_min_i<SUB>(ld);
-      if (live && sub == 0) L.fd[s] = ld;
-      __syncthreads();
-      if (tid < 64) {
-        float bv = -INFINITY;
-        int bi = 0x7fffffff;
-#pragma unroll
-        for (int k = 0; k < (SMAX + 63) / 64; ++k) {
-          const int ss = tid + 64 * k;
-          if (ss < S) argmax_combine(bv, bi, L.dmx[t & 1][ss], ss);
-        }
-        wave_argmax(bv, bi);
-        if (tid == 0) {
-          const bool any = bv != -INFINITY;
-          a.scores[b] = bv;
-          a.fin[2 * b] = any ? bi : 0;
-          a.fin[2 * b + 1] = any ? L.fd[bi] : 1;
-        }
-      }
+      for (int j = 0; j < NJ; ++j) L.vfin[j][tid] = vv[j];
+      Afin = A;
+      mxfin = mx;
       return false;
     }
     step_barrier();
-    // M[t][s] = max_{s' != s} fl(Dm[t][s'] + logT[s'][s]) and the first s' attaining it
+    // M[t][s] = max_{s' != s} fl(Dm[t][s'] + logT[s'][s]) (the first s' attaining it is
+    // recovered by the backtrace from the stored Dm row, for the path's segments only)
     {
+      const float4* dp = reinterpret_cast<const float4*>(&L.dmx[t & 1][sub * NPRED]);
+      float4 dq[NPRED / 4];
+#pragma unroll
+      for (int i = 0; i < NPRED / 4; ++i) dq[i] = dp[i];  // all reads first
       float lm = -INFINITY;
-      int ls = 0x7fff;
-      float dmv[G::NPRED];
 #pragma unroll
-      for (int j = 0; j < G::NPRED; ++j) dmv[j] = L.dmx[t & 1][sub + SUB * j];  // all reads first
-#pragma unroll
-      for (int j = 0; j < G::NPRED; ++j) {
-        const int sp = sub + SUB * j;
+      for (int i = 0; i < NPRED / 4; ++i) {
         // lt == -inf (excluded s') or dm == -inf: the sum is -inf (never +inf: no NaN)
-        const float c = dmv[j] + lt[j];
-        const bool gt = c > lm;
-        lm = gt ? c : lm;
-        ls = gt ? sp : ls;
+        const hs_f2 c0 = hs_f2{dq[i].x, dq[i].y} + lt2[2 * i];
+        const hs_f2 c1 = hs_f2{dq[i].z, dq[i].w} + lt2[2 * i + 1];
+        lm = fmaxf(lm, fmaxf(c0.x, c0.y));
+        lm = fmaxf(lm, fmaxf(c1.x, c1.y));
       }
       const float M = grp_max<SUB>(lm);
-      const int s1 = grp_min_i<SUB>((lm == M && M != -INFINITY) ? ls : 0x7fff);
       Mlast = M;
-      if (live && sub == 0) {
-        const size_t gi = ((size_t)b * T + t) * S + s;
-        a.Mg[gi] = M;
-        a.S1[gi] = (uint8_t)(M == -INFINITY ? 0 : s1);
-      }
+      if (live && sub == 0) a.Mg[((size_t)b * T + t) * S + s] = M;
     }
     if ((t + 2) % 64 == 0) {  // rows of chunk c = (t+2)/64 are first read at step t+2
       const int cidx = (t + 2) >> 6;
@@ -281,15 +300,40 @@ __global__ void __launch_bounds__((HsG<SUB, NJ, SMAX>::NT)) hsmm_fwd_kernel(HsAr
     }
     return true;
   };
-  using I0 = std::integral_constant<int, 0>;
-  using I1 = std::integral_constant<int, 1>;
-  using I2 = std::integral_constant<int, 2>;
-  using I3 = std::integral_constant<int, 3>;
-  for (int t = 0; t < T; t += 4) {
-    if (!end_step(t, I0{})) break;
-    if (!end_step(t + 1, I1{})) break;
-    if (!end_step(t + 2, I2{})) break;
-    if (!end_step(t + 3, I3{})) break;
+  bool go = true;
+  for (int t = 0; go; t += NJ)
+    static_for<0, NJ>([&](auto Uc) {
+      if (go) go = end_step(t + decltype(Uc)::value, Uc);
+    });
+  // best over (s asc, d asc) of delta[T-1][s][d-1], strict > (hsmm.py:319-329); each lane
+  // reads back only what it wrote
+  {
+    const int t = T - 1;
+    int ld = 0x7fff;
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+      const int d = ((Afin - j) & (R - 1)) + 1;
+      if (L.vfin[j][tid] == mxfin && d < ld) ld = d;
+    }
+    ld = grp_min_i<SUB>(ld);
+    if (live && sub == 0) L.fd[s] = ld;
+    __syncthreads();
+    if (tid < 64) {
+      float bv = -INFINITY;
+      int bi = 0x7fffffff;
+#pragma unroll
+      for (int k = 0; k < (SMAX + 63) / 64; ++k) {
+        const int ss = tid + 64 * k;
+        if (ss < S) argmax_combine(bv, bi, L.dmx[t & 1][(ss % SUB) * NPRED + ss / SUB], ss);
+      }
+      wave_argmax(bv, bi);
+      if (tid == 0) {
+        const bool any = bv != -INFINITY;
+        a.scores[b] = bv;
+        a.fin[2 * b] = any ? bi : 0;
+        a.fin[2 * b + 1] = any ? L.fd[bi] : 1;
+      }
+    }
   }
 }
 
@@ -342,35 +386,64 @@ __device__ __forceinline__ float hs_obs_sum_lds(const float* col, int d) {
   return r;
 }
 
+inline size_t hsmm_backtrace_lds(int S, int Dm, int R) { return (size_t)(S * Dm + S * S + R) * sizeof(float); }
+
 // R >= the longest duration; every lane owns the candidates d' = l + 1 + 64k, k < R/64, and
-// the predecessor states s' = l + 64k, k < SMAX/64
+// the predecessor states s' = l + 64k, k < SMAX/64.  LDS: dur (S, Dm), logT (S, S) and the
+// predecessor's candidate column lp[tau - e][s1], e < Dm.
 template <int R, int SMAX>
 __global__ void __launch_bounds__(64) hsmm_backtrace_kernel(HsArgs a) {
   constexpr int K = R / 64;
   constexpr int KS = (SMAX + 63) / 64;
-  __shared__ float pcol[R];  // lp[tau - i][s1], i < Dm: the predecessor's candidate column
-  __shared__ float ccol[R];  // lp[t - i][cs], i < cd: the current segment, newest first
+  extern __shared__ __attribute__((aligned(16))) char bsm[];
   const int b = blockIdx.x, l = threadIdx.x;
   const int T = a.T, S = a.S, Dm = a.Dm;
+  float* sdur = reinterpret_cast<float*>(bsm);
+  float* slt = sdur + S * Dm;
+  float* pcol = slt + S * S;
+  for (int i = l; i < S * Dm; i += 64) sdur[i] = a.dur[i];
+  for (int i = l; i < S * S; i += 64) slt[i] = a.logT[i];
   const float* lp = a.lp + (size_t)b * T * S;
   const float* Mb = a.Mg + (size_t)b * T * S;
   const float* Db = a.Dg + (size_t)b * T * S;
   int t = T - 1, cs = a.fin[2 * b], cd = a.fin[2 * b + 1];
+  float o = hs_obs_sum_global(lp, S, T - cd, cd, cs);  // the current segment's obs_sum
+  __syncthreads();
   while (t >= 0 && cd > 0) {
     int start = t - cd + 1;
     if (start < 0) start = 0;
     for (int u = start + l; u <= t; u += 64) a.states[(size_t)b * T + u] = cs;
     if (start == 0) break;
     const int tau = start - 1;  // end of the previous segment
-    const size_t gi = (size_t)tau * S + cs;
-    const float M = Mb[gi];
+    // round trip 1: M and the Dm row at tau
+    const float M = Mb[(size_t)tau * S + cs];
+    float dm[KS];
+#pragma unroll
+    for (int k = 0; k < KS; ++k) {
+      const int sp = l + 64 * k;
+      dm[k] = sp < S ? Db[(size_t)tau * S + sp] : -INFINITY;
+    }
     int ns = 0, nd = 0;  // literal: psi never written when no predecessor exists (hsmm.py:313)
+    float on = 0.f;
     if (M != -INFINITY) {
-      ns = a.S1[(size_t)b * T * S + gi];
-      const float lt = a.logT[(size_t)ns * S + cs];
+      // the first s' != cs attaining M: the forward's own candidate values fl(Dm + logT)
+      float cv[KS];
+      ns = -1;
+#pragma unroll
+      for (int k = 0; k < KS; ++k) {
+        const int sp = l + 64 * k;
+        cv[k] = (sp < S && sp != cs) ? dm[k] + slt[sp * S + cs] : -INFINITY;
+        const unsigned long long mask = __ballot(cv[k] == M);
+        if (ns < 0 && mask) ns = 64 * k + __ffsll((long long)mask) - 1;
+      }
+      if (ns < 0) ns = 0;  // unreachable: M is the maximum of these candidates
+      const float lt = slt[ns * S + cs];
+      float xo = -INFINITY;  // best total of the states before ns
+#pragma unroll
+      for (int k = 0; k < KS; ++k)
+        if (l + 64 * k < ns) xo = fmaxf(xo, cv[k]);
+      // round trip 2: ns's candidate column and its candidates' predecessor scores
       const int dlim = Dm < tau + 1 ? Dm : tau + 1;
-      // one round trip: both columns, the candidates' predecessor scores, the other states'
-      // best totals (xb)
       float pm[K];
 #pragma unroll
       for (int k = 0; k < K; ++k) {
@@ -380,35 +453,22 @@ __global__ void __launch_bounds__(64) hsmm_backtrace_kernel(HsArgs a) {
         const int pst = tau - e;  // candidate d' = e + 1 starts at tau - e
         pm[k] = (pin && pst >= 1) ? Mb[(size_t)(pst - 1) * S + ns] : 0.f;
         if (pin) pcol[e] = pv;
-        if (e < cd) ccol[e] = lp[(size_t)(t - e) * S + cs];
-      }
-      // max over s' < ns, s' != cs of fl(Dm[tau][s'] + logT[s'][cs]) (loads in the same round trip)
-      float dm[KS], ltl[KS];
-#pragma unroll
-      for (int k = 0; k < KS; ++k) {
-        const int sp = l + 64 * k;
-        const bool ok = sp < ns;
-        dm[k] = ok ? Db[(size_t)tau * S + sp] : -INFINITY;
-        ltl[k] = ok ? a.logT[(size_t)sp * S + cs] : 0.f;
       }
       __syncthreads();
-      float xo = -INFINITY;
-#pragma unroll
-      for (int k = 0; k < KS; ++k)
-        if (l + 64 * k != cs && dm[k] != -INFINITY) xo = fmaxf(xo, dm[k] + ltl[k]);
-      // first d' of s1 whose fl(delta + logT) equals M, and the best earlier total (xb)
-      float dv[K];
+      // first d' of ns whose fl(delta + logT) equals M, and the best earlier total (xb)
+      float dv[K], ov[K];
       nd = 0;
 #pragma unroll
       for (int k = 0; k < K; ++k) {
         const int e = l + 64 * k;
         dv[k] = -INFINITY;
+        ov[k] = 0.f;
         bool hit = false;
         if (e < dlim) {
-          const float o = hs_obs_sum_lds(pcol, e + 1);
-          const float u = a.dur[(size_t)ns * Dm + e];
+          ov[k] = hs_obs_sum_lds(pcol, e + 1);
+          const float u = sdur[ns * Dm + e];
           const int pst = tau - e;
-          dv[k] = pst == 0 ? o + u : (pm[k] == -INFINITY ? -INFINITY : (pm[k] + o) + u);
+          dv[k] = pst == 0 ? ov[k] + u : (pm[k] == -INFINITY ? -INFINITY : (pm[k] + ov[k]) + u);
           hit = dv[k] != -INFINITY && dv[k] + lt == M;
         }
         const unsigned long long mask = __ballot(hit);
@@ -420,8 +480,14 @@ __global__ void __launch_bounds__(64) hsmm_backtrace_kernel(HsArgs a) {
       for (int k = 0; k < K; ++k)
         if (l + 64 * k + 1 < nd && dv[k] != -INFINITY) xb = fmaxf(xb, dv[k] + lt);
       xb = wave_max(xb);
-      const float o = hs_obs_sum_lds(ccol, cd);
-      const float u = a.dur[(size_t)cs * Dm + cd - 1];
+      // the next segment's obs_sum is candidate nd's
+      {
+        float ok = ov[0];
+#pragma unroll
+        for (int k = 1; k < K; ++k) ok = (nd - 1) >> 6 == k ? ov[k] : ok;
+        on = __shfl(ok, (nd - 1) & 63);
+      }
+      const float u = sdur[cs * Dm + cd - 1];
       const float F = (M + o) + u;
       if (xb != -INFINITY && (xb + o) + u == F) {
         // rare: an earlier candidate rounds to the same total — the first one wins (hsmm.py:308)
@@ -434,7 +500,7 @@ __global__ void __launch_bounds__(64) hsmm_backtrace_kernel(HsArgs a) {
             const int sp = k / Dm, dp = k % Dm + 1;
             if (sp != cs && dp <= tau + 1) {
               const float c2 = hs_delta(a, lp, Mb, tau - dp + 1, sp, dp);
-              if (c2 != -INFINITY) h2 = ((c2 + a.logT[(size_t)sp * S + cs]) + o) + u == F;
+              if (c2 != -INFINITY) h2 = ((c2 + slt[sp * S + cs]) + o) + u == F;
             }
           }
           const unsigned long long m2 = __ballot(h2);
@@ -442,28 +508,31 @@ __global__ void __launch_bounds__(64) hsmm_backtrace_kernel(HsArgs a) {
         }
         ns = win / Dm;
         nd = win % Dm + 1;
+        on = hs_obs_sum_global(lp, S, tau - nd + 1, nd, ns);
       }
-      __syncthreads();  // the columns are restaged for the next segment
+      __syncthreads();  // the column is restaged for the next segment
     }
     t = start - 1;
     cs = ns;
     cd = nd;
+    o = on;
   }
 }
 
-// Geometries (S <= SMAX, Dmax < R): the config-5 class S <= 64, Dmax <= 63 takes the 8-lane
-// form unless HMM355_HSMM_SUB=16 asks for the 16-lane one.
-// The larger geometries run 512 threads (8 waves) so a lane has 256 VGPRs for its 16 slots.
-// (S <= 128 with 64 <= Dmax <= 127 would need 32 slots per lane: beyond the register file;
-// rejected.)
-enum HsCfg : int { kHs16x4 = 0, kHs8x8s64 = 1, kHs8x16 = 2, kHs4x16 = 3, kHsNone = -1 };
+// Geometries (S <= SMAX, Dmax < R).  The config-5 class S <= 64, Dmax <= 63 takes the
+// 8-lane form (512 threads, 8 slots per lane: 0.96 ms at config 5, vs 0.97 for 16 lanes and
+// 1.22 for 4 lanes with one wave per SIMD; profiles/r3l_c5_sub*.log) unless HMM355_HSMM_SUB=4
+// or =16 asks for another.  The larger geometries run 512 threads (8 waves) so a lane has 256 VGPRs
+// for its 16 slots.  (S <= 128 with 64 <= Dmax <= 127 would need 32 slots per lane: beyond
+// the register file; rejected.)
+enum HsCfg : int { kHs16x4 = 0, kHs8x8s64 = 1, kHs8x16 = 2, kHs4x16 = 3, kHs4x16s64 = 4, kHsNone = -1 };
 inline int hsmm_cfg(int S, int Dm) {
   if (S < 1 || Dm < 1) return kHsNone;
   if (S <= 64 && Dm < 64) {
-    // 8-lane groups, 512 threads: 1.48 vs 1.57 ms for the 16-lane form at config 5
-    // (profiles/r3f_c5_sub*.log); HMM355_HSMM_SUB=16 selects the 16-lane form
     const char* e = getenv("HMM355_HSMM_SUB");
-    return (e && e[0] == '1' && e[1] == '6') ? kHs16x4 : kHs8x8s64;
+    if (e && e[0] == '1' && e[1] == '6') return kHs16x4;
+    if (e && e[0] == '4') return kHs4x16s64;
+    return kHs8x8s64;
   }
   if (S <= 64 && Dm < 128) return kHs8x16;
   if (S <= 128 && Dm < 64) return kHs4x16;
@@ -473,13 +542,16 @@ inline int hsmm_cfg(int S, int Dm) {
 template <int SUB, int NJ, int SMAX>
 static hipError_t launch_hsmm(const HsArgs& ha, hipStream_t st) {
   using G = HsG<SUB, NJ, SMAX>;
-  const size_t lds = sizeof(HsLds<SMAX, G::R>);
+  const size_t lds = sizeof(HsLds<SMAX, G::DW, NJ, G::NT>);
   hipError_t e = allow_lds(hsmm_fwd_kernel<SUB, NJ, SMAX>, lds);
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL((hsmm_fwd_kernel<SUB, NJ, SMAX>), dim3(ha.B), dim3(G::NT), lds, st, ha);
   e = hipGetLastError();
   if (e != hipSuccess) return e;
-  hipLaunchKernelGGL((hsmm_backtrace_kernel<G::R, SMAX>), dim3(ha.B), dim3(64), 0, st, ha);
+  const size_t blds = hsmm_backtrace_lds(ha.S, ha.Dm, G::R);
+  e = allow_lds(hsmm_backtrace_kernel<G::R, SMAX>, blds);
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL((hsmm_backtrace_kernel<G::R, SMAX>), dim3(ha.B), dim3(64), blds, st, ha);
   return hipGetLastError();
 }
 
@@ -490,7 +562,7 @@ using namespace hmm355;
 HMM355_API size_t hmm355_hsmm_workspace_bytes(int B, int T, int S, int Dmax) {
   if (B < 0 || T < 1 || hsmm_cfg(S, Dmax) == kHsNone) return 0;
   const size_t n = (size_t)B * T * S;
-  return align_up(n * 4, 256) + align_up(n, 256) + align_up(n * 4, 256) + align_up((size_t)B * 8, 256);
+  return 2 * align_up(n * 4, 256) + align_up((size_t)B * 8, 256);
 }
 
 HMM355_API int hmm355_hsmm_viterbi_f32(const float* lp, const float* dur_lp, const float* log_T, int B, int T,
@@ -506,15 +578,15 @@ HMM355_API int hmm355_hsmm_viterbi_f32(const float* lp, const float* dur_lp, con
   const size_t n = (size_t)B * T * S;
   char* ws = static_cast<char*>(workspace);
   float* Mg = reinterpret_cast<float*>(ws);
-  uint8_t* S1 = reinterpret_cast<uint8_t*>(ws + align_up(n * 4, 256));
-  float* Dg = reinterpret_cast<float*>(ws + align_up(n * 4, 256) + align_up(n, 256));
-  int* fin = reinterpret_cast<int*>(ws + align_up(n * 4, 256) + align_up(n, 256) + align_up(n * 4, 256));
-  HsArgs ha{lp, dur_lp, log_T, Mg, S1, Dg, fin, scores, states, B, T, S, Dmax};
+  float* Dg = reinterpret_cast<float*>(ws + align_up(n * 4, 256));
+  int* fin = reinterpret_cast<int*>(ws + 2 * align_up(n * 4, 256));
+  HsArgs ha{lp, dur_lp, log_T, Mg, Dg, fin, scores, states, B, T, S, Dmax};
   hipStream_t st = static_cast<hipStream_t>(stream);
   hipError_t e;
   switch (hsmm_cfg(S, Dmax)) {
     case kHs16x4: e = launch_hsmm<16, 4, 64>(ha, st); break;
     case kHs8x8s64: e = launch_hsmm<8, 8, 64>(ha, st); break;
+    case kHs4x16s64: e = launch_hsmm<4, 16, 64>(ha, st); break;
     case kHs8x16: e = launch_hsmm<8, 16, 64>(ha, st); break;
     default: e = launch_hsmm<4, 16, 128>(ha, st); break;
   }

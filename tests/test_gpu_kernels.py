@@ -185,10 +185,10 @@ def test_hsmm_ties_vs_c_oracle(seed, T, S, Dm):
     assert np.array_equal(scores.cpu().numpy(), csc)
 
 
-# every kernel geometry (csrc/hsmm.hip hsmm_cfg): (16,4,64) S <= 64 / Dmax <= 63, (8,16,64)
-# Dmax <= 127, (4,16,128) S <= 128 / Dmax <= 63; for S <= 64 / Dmax <= 63 both the default 8-lane
-# (8,8,64) form and HMM355_HSMM_SUB=16's 16-lane one
-@pytest.mark.parametrize("sub", ["8", "16"])
+# every kernel geometry (csrc/hsmm.hip hsmm_cfg): (8,16,64) Dmax <= 127, (4,16,128)
+# S <= 128 / Dmax <= 63; for S <= 64 / Dmax <= 63 the default 8-lane (8,8,64) form and
+# HMM355_HSMM_SUB=4 / =16's (4,16,64) and (16,4,64) ones
+@pytest.mark.parametrize("sub", ["8", "4", "16"])
 @pytest.mark.parametrize("B,T,S,Dm", [(2, 150, 16, 12), (1, 300, 64, 40), (3, 70, 7, 63), (2, 260, 40, 100),
                                       (1, 200, 100, 50), (2, 180, 128, 63), (1, 90, 65, 63), (2, 130, 3, 127)])
 def test_hsmm_vs_c_oracle(B, T, S, Dm, sub, monkeypatch):
@@ -197,6 +197,27 @@ def test_hsmm_vs_c_oracle(B, T, S, Dm, sub, monkeypatch):
     lp = (-(rng.random((B, T, S), dtype=np.float32) * 40 + 80)).astype(np.float32)
     dur = np.log(rng.random((S, Dm), dtype=np.float32) + np.float32(1e-8)).astype(np.float32)
     logT = np.log(rng.random((S, S), dtype=np.float32) + np.float32(1e-8)).astype(np.float32)
+    cs, csc = O.c_hsmm(lp, dur, logT)
+    o = ops()
+    states, scores = o.hsmm_viterbi(t(lp), t(dur), t(logT))
+    assert np.array_equal(states.cpu().numpy(), cs)
+    assert np.array_equal(scores.cpu().numpy(), csc)
+
+
+@pytest.mark.parametrize("sub", ["8", "4", "16"])
+def test_hsmm_impossible_transitions_and_durations(sub, monkeypatch):
+    """-inf in the tables (a left-to-right transition matrix, durations below a minimum, a state
+    no segment may take): the kernel's folded conditions (M = -inf for slots not started, -inf
+    duration rows) against the C oracle."""
+    monkeypatch.setenv("HMM355_HSMM_SUB", sub)
+    rng = np.random.default_rng(5)
+    B, T, S, Dm = 3, 140, 12, 20
+    lp = (-(rng.random((B, T, S), dtype=np.float32) * 30 + 10)).astype(np.float32)
+    dur = np.log(rng.random((S, Dm), dtype=np.float32) + np.float32(1e-8)).astype(np.float32)
+    dur[:, :2] = -np.inf          # min_duration 3
+    dur[5, :] = -np.inf           # state 5 never holds a segment
+    logT = np.log(rng.random((S, S), dtype=np.float32) + np.float32(1e-8)).astype(np.float32)
+    logT[np.tril_indices(S, -1)] = -np.inf   # left to right
     cs, csc = O.c_hsmm(lp, dur, logT)
     o = ops()
     states, scores = o.hsmm_viterbi(t(lp), t(dur), t(logT))
