@@ -30,8 +30,8 @@
 //   not yet started has M = -inf, the slot starting at time 0 has M = 0 (fl(0 + o) == o), and
 //   durations beyond Dmax or padding states read -inf from the duration table.  Per end time t
 //   the kernel stores M[t][s] (the best fl(delta + logT) over predecessors ending at t, for
-//   segments starting at t+1) and Dm[t][s].  Geometries: (8, 8, 64) for the config-5 class
-//   (S <= 64, Dmax <= 63), (4, 16, 64) / (16, 4, 64) the same with 4- and 16-lane groups, (8, 16, 64) for Dmax <= 127 and (4, 16, 128) for 65 <= S <= 128 with
+//   segments starting at t+1) and Dm[t][s].  Geometries: (4, 16, 64) for the config-5 class
+//   (S <= 64, Dmax <= 63), (8, 8, 64) / (16, 4, 64) the same with 8- and 16-lane groups, (8, 16, 64) for Dmax <= 127 and (4, 16, 128) for 65 <= S <= 128 with
 //   Dmax <= 63.
 // hsmm_backtrace_kernel: one wave per sequence walks the segments (hsmm.py:331-352); for each
 //   segment it finds the first predecessor state attaining M from the stored Dm row (the
@@ -63,7 +63,7 @@ struct HsG {
   static constexpr int NPRED = SMAX / SUB;   // predecessor states per lane
   static constexpr int PER = 64 * SMAX / NT; // lp values per thread per 64-row chunk
   static constexpr int NP2 = NJ / 2;         // packed slot pairs (j, j + NJ/2)
-  static constexpr int DW = R + NJ + 1;      // duration-table row stride (odd: bank spread)
+  static constexpr int DW = R + NJ + 1;      // duration-pair table row stride
   static_assert(NJ % 4 == 0, "slot position (t - k) & 3 must be a compile-time constant");
   static_assert((R & (R - 1)) == 0, "slot ring is a power of two");
   static_assert(NPRED % 4 == 0, "predecessor scores are read as float4");
@@ -82,15 +82,19 @@ struct HsArgs {
   int B, T, S, Dm;
 };
 
-template <int SMAX, int DW, int NJ, int NT>
+template <int SMAX, int DW>
 struct HsLds {
-  float dmx[2][SMAX];    // Dm[t][s'] at q(s') = (s' % SUB) * NPRED + s' / SUB: a lane's
-                         // predecessors are contiguous
-  float lpr[kHsL][SMAX];
-  float durx[SMAX][DW];  // durx[s][i] = dur[s][(i - NJ) mod R], -inf for d >= Dmax or s >= S
+  float dmx[2][SMAX];      // Dm[t][s'] at q(s') = (s' % SUB) * NPRED + s' / SUB: a lane's
+                           // predecessors are contiguous
+  float lpr[kHsL][SMAX];   // lp row ring; after the last step, the final slot values
+  hs_f2 dpair[SMAX][DW];   // dpair[s][c] = {dur[s][(c - NJ) mod R], dur[s][(c - NJ - NJ/2) mod R]}
   int fd[SMAX];
-  float vfin[NJ][NT];    // the final step's slot values
 };
+
+constexpr int kHsOOB = 0x7FFFFFF0;  // a buffer offset past every record count: the store is dropped
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t hs_rsrc(const void* p, unsigned bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, (int)bytes, 0x00020000);
+}
 
 // all-reduce over the SUB lanes of a state group (16: one DPP row; 8: half a row; 4: a quad)
 template <int SUB>
@@ -121,19 +125,26 @@ __global__ void __launch_bounds__((HsG<SUB, NJ, SMAX>::NT)) hsmm_fwd_kernel(HsAr
   using G = HsG<SUB, NJ, SMAX>;
   constexpr int R = G::R, NT = G::NT, NP2 = G::NP2, NPRED = G::NPRED, DW = G::DW;
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  HsLds<SMAX, DW, NJ, NT>& L = *reinterpret_cast<HsLds<SMAX, DW, NJ, NT>*>(smem);
+  HsLds<SMAX, DW>& L = *reinterpret_cast<HsLds<SMAX, DW>*>(smem);
   const int b = blockIdx.x, tid = threadIdx.x;
   const int T = a.T, S = a.S, Dm = a.Dm;
   const int s = tid / SUB, sub = tid % SUB;
   const bool live = s < S;
   const int q = (s % SUB) * NPRED + s / SUB;
   const float* lp = a.lp + (size_t)b * T * S;
+  // Dm / M rows: one lane per state stores (buffer offsets past the records drop the rest)
+  const __amdgpu_buffer_rsrc_t dg_r = hs_rsrc(a.Dg + (size_t)b * T * S, (unsigned)T * S * 4u);
+  const __amdgpu_buffer_rsrc_t mg_r = hs_rsrc(a.Mg + (size_t)b * T * S, (unsigned)T * S * 4u);
+  const int st_off = (live && sub == 0) ? s * 4 : kHsOOB;
 
+  auto dur_at = [&](int r, int age) -> float {  // -inf beyond Dmax and for padding states
+    return (r < S && age < Dm) ? a.dur[(size_t)r * Dm + age] : -INFINITY;
+  };
   for (int i = tid; i < SMAX * DW; i += NT) {
     const int r = i / DW, c = i % DW;
-    const int d = (c - NJ) & (R - 1);
-    L.durx[r][c] = (r < S && d < Dm) ? a.dur[(size_t)r * Dm + d] : -INFINITY;
+    L.dpair[r][c] = hs_f2{dur_at(r, (c - NJ) & (R - 1)), dur_at(r, (c - NJ - NP2) & (R - 1))};
   }
+  const float u0 = dur_at(s, 0), u1 = dur_at(s, 1);  // duration terms of d = 1, 2
   hs_f2 lt2[NPRED / 2];  // log T[s'][s] for the lane's predecessors s' = sub + SUB j (-inf: excluded)
 #pragma unroll
   for (int j = 0; j < NPRED; ++j) {
@@ -181,50 +192,76 @@ __global__ void __launch_bounds__((HsG<SUB, NJ, SMAX>::NT)) hsmm_fwd_kernel(HsAr
     A0[p] = hs_f2{0.f, 0.f};
     mp[p] = hs_f2{-INFINITY, -INFINITY};  // not started: delta = -inf
   }
-  float xr[4] = {0.f, 0.f, 0.f, 0.f};
-  // M handed to the slot that starts next; 0 for the segment starting at t = 0, whose delta
-  // is o + u (hsmm.py:269-274): fl(fl(0 + o) + u) == fl(o + u)
-  float Mlast = 0.f;
-  int Afin = 0;
-  float mxfin = -INFINITY;
-
-  // One end time t (U = t % NJ).  Lane `sub` owns slots k = NJ*sub + j, so the new element's
-  // position in its segment's group of four, (t - k) & 3 = (U - j) & 3 (NJ is a multiple of
-  // 4), is a compile-time constant of the unrolled copy, and the only slot that can start at
-  // t is j = U.  Every LDS read of the step is issued before its first use.
-  auto end_step = [&](const int t, auto Uc) -> bool {
-    constexpr int U = decltype(Uc)::value;
-    const int A = (t - NJ * sub) & (R - 1);  // slot j's age is (A - j) & (R - 1)
-    const float x = L.lpr[t % kHsL][s];
-    xr[U & 3] = x;
-    const float* drow = &L.durx[s][A + NJ];  // dur[s][age_j] = drow[-j]
-    hs_f2 du[NP2];
-    static_for<0, NP2>([&](auto Pc) {
-      constexpr int p = decltype(Pc)::value;
-      du[p] = hs_f2{drow[-p], drow[-(p + NP2)]};
-    });
-    {
-      constexpr int pf = U % NP2, hf = U / NP2;
-      const bool fresh = A == U;
+  hs_f2 xr[4] = {};
+  float xcur = 0.f, xnext = 0.f;  // lp[t][s], lp[t+1][s]
+  float mxc = -INFINITY, mxn = -INFINITY;  // best delta of the segments of age >= 2 at t, t+1
+  float v1c = -INFINITY;   // delta of the segment that started at t-1 (d = 2), ending at t
+  float vv[NJ];            // phase B's slot values (the final step's selection)
+  bool age1 = false;       // this lane owns the slot of age 1 (started at t-1) at phase B's t
+  int Af = 0;
+  // phase B's LDS operands, read a step ahead into the buffer of t's parity (NJ is even, so
+  // the parity is a compile-time constant of every unrolled copy)
+  float xq[2] = {0.f, 0.f};
+  hs_f2 duq[2][NP2];
+  auto prefetch = [&](const int t, auto Bc) {
+    constexpr int B2 = decltype(Bc)::value;
+    const int A = (t - NJ * sub) & (R - 1);
+    xq[B2] = L.lpr[t % kHsL][s];
+    const hs_f2* drow = &L.dpair[s][A + NJ];  // {dur[age_p], dur[age_{p+NP2}]} = drow[-p]
 #pragma unroll
-      for (int i = 0; i < 4; ++i) Gs[pf][i][hf] = fresh ? 0.f : Gs[pf][i][hf];
-      mp[pf][hf] = fresh ? Mlast : mp[pf][hf];
+    for (int p = 0; p < NP2; ++p) duq[B2][p] = drow[-p];
+  };
+
+  // Phase B for end time t (U = t % NJ): every segment of age >= 2 ending at t takes lp[t]
+  // into its sums; mxn = their best delta.  It does not depend on M[t-1] or M[t-2], so it
+  // runs in the shadow of the predecessor phase of t-1: `mid1` (its predecessor scores)
+  // and `mid2` (the group reduction, M, Dm[t-1]'s store) run between pairs of slots, fenced
+  // so that the in-order issue fills their LDS and DPP latencies with slot work.
+  // Lane `sub` owns slots k = NJ*sub + j, so the new element's position in its segment's
+  // group of four, (t - k) & 3 = (U - j) & 3, is a compile-time constant of the unrolled
+  // copy; the slot of age 0 at t is j = U (iff A == U) and the one of age 1 is j = U - 1 mod NJ.
+  auto phase_b = [&](const int t, auto Uc, auto&& mid1, auto&& mid2) {
+    constexpr int U = decltype(Uc)::value;
+    constexpr int J1 = (U + NJ - 1) % NJ;
+    const int A = (t - NJ * sub) & (R - 1);
+    const float x = xq[U & 1];
+    age1 = ((A - J1) & (R - 1)) == 1;
+    {
+      // the segment that started at t-1: sums restart from lp[t-1] (its M is set by the
+      // predecessor phase of t-1, before its first use at t+1)
+      constexpr int p1 = J1 % NP2, h1 = J1 / NP2;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) Gs[p1][i][h1] = age1 ? 0.f : Gs[p1][i][h1];
+      A0[p1][h1] = age1 ? xcur : A0[p1][h1];
     }
+    xnext = x;
     const hs_f2 x2 = {x, x};
+    xr[U & 3] = x2;
     float mx = -INFINITY;
-    float vv[NJ];
     static_for<0, NP2>([&](auto Pc) {
       constexpr int p = decltype(Pc)::value;
+      if constexpr (p == NP2 / 2) {
+        __builtin_amdgcn_sched_barrier(0);
+        mid1();
+        __builtin_amdgcn_sched_barrier(0);
+      }
+      if constexpr (p == (3 * NP2) / 4) {
+        __builtin_amdgcn_sched_barrier(0);
+        mid2();
+        __builtin_amdgcn_sched_barrier(0);
+      }
+      if constexpr (kAbl & (1 << 21)) {  // ablation: no slot work (timing only)
+        vv[p] = vv[p + NP2] = x;
+        mx = fmaxf(mx, x);
+        return;
+      }
       constexpr int pa = (U - p + 4 * NJ) & 3, pb = (U - p - NP2 + 4 * NJ) & 3;
       if constexpr (pa == pb) {
         if constexpr (pa == 0) {
           A0[p] = Gs[p][0] + x2;
         } else if constexpr (pa == 3) {
 #pragma unroll
-          for (int i = 0; i < 4; ++i) {
-            const float xe = xr[(U + 1 + i) & 3];
-            Gs[p][i] = Gs[p][i] + hs_f2{xe, xe};
-          }
+          for (int i = 0; i < 4; ++i) Gs[p][i] = Gs[p][i] + xr[(U + 1 + i) & 3];
         } else {
           A0[p] = A0[p] + x2;
         }
@@ -236,7 +273,7 @@ __global__ void __launch_bounds__((HsG<SUB, NJ, SMAX>::NT)) hsmm_fwd_kernel(HsAr
             A0[p][h] = Gs[p][0][h] + x;
           } else if constexpr (ps == 3) {
 #pragma unroll
-            for (int i = 0; i < 4; ++i) Gs[p][i][h] = Gs[p][i][h] + xr[(U + 1 + i) & 3];
+            for (int i = 0; i < 4; ++i) Gs[p][i][h] = Gs[p][i][h] + xr[(U + 1 + i) & 3][0];
           } else {
             A0[p][h] = A0[p][h] + x;
           }
@@ -252,69 +289,107 @@ __global__ void __launch_bounds__((HsG<SUB, NJ, SMAX>::NT)) hsmm_fwd_kernel(HsAr
       }
       const hs_f2 o = ((a0 + Gs[p][1]) + Gs[p][2]) + Gs[p][3];
       // hsmm.py:304-314: fl(fl(M + o) + u); mp == -inf (no predecessor path) gives -inf
-      const hs_f2 v = (mp[p] + o) + du[p];
+      hs_f2 v = (mp[p] + o) + duq[U & 1][p];
+      if constexpr (p == U % NP2) v[U / NP2] = A == U ? -INFINITY : v[U / NP2];  // age 0
+      if constexpr (p == J1 % NP2) v[J1 / NP2] = age1 ? -INFINITY : v[J1 / NP2];  // age 1
       vv[p] = v.x;
       vv[p + NP2] = v.y;
       mx = fmaxf(mx, fmaxf(v.x, v.y));
     });
-    mx = grp_max<SUB>(mx);
-    if (sub == 0) {
-      L.dmx[t & 1][q] = mx;  // -inf for the padding states s >= S
-      if (live) a.Dg[((size_t)b * T + t) * S + s] = mx;
-    }
-    if (t == T - 1) {
-      // the final step's slot values go to LDS (a store cannot be hoisted into every step);
-      // the (s asc, d asc) selection runs after the loop
-#pragma unroll
-      for (int j = 0; j < NJ; ++j) L.vfin[j][tid] = vv[j];
-      Afin = A;
-      mxfin = mx;
-      return false;
-    }
-    step_barrier();
-    // M[t][s] = max_{s' != s} fl(Dm[t][s'] + logT[s'][s]) (the first s' attaining it is
-    // recovered by the backtrace from the stored Dm row, for the path's segments only)
-    {
-      const float4* dp = reinterpret_cast<const float4*>(&L.dmx[t & 1][sub * NPRED]);
-      float4 dq[NPRED / 4];
-#pragma unroll
-      for (int i = 0; i < NPRED / 4; ++i) dq[i] = dp[i];  // all reads first
-      float lm = -INFINITY;
-#pragma unroll
-      for (int i = 0; i < NPRED / 4; ++i) {
-        // lt == -inf (excluded s') or dm == -inf: the sum is -inf (never +inf: no NaN)
-        const hs_f2 c0 = hs_f2{dq[i].x, dq[i].y} + lt2[2 * i];
-        const hs_f2 c1 = hs_f2{dq[i].z, dq[i].w} + lt2[2 * i + 1];
-        lm = fmaxf(lm, fmaxf(c0.x, c0.y));
-        lm = fmaxf(lm, fmaxf(c1.x, c1.y));
-      }
-      const float M = grp_max<SUB>(lm);
-      Mlast = M;
-      if (live && sub == 0) a.Mg[((size_t)b * T + t) * S + s] = M;
-    }
-    if ((t + 2) % 64 == 0) {  // rows of chunk c = (t+2)/64 are first read at step t+2
-      const int cidx = (t + 2) >> 6;
-      chunk_store(cidx);
-      if ((cidx + 1) * 64 < T) chunk_load(cidx + 1);
-      __syncthreads();
-    }
-    return true;
+    mxn = grp_max<SUB>(mx);
+    Af = A;
   };
-  bool go = true;
-  for (int t = 0; go; t += NJ)
+
+  // The predecessor phase of end time t: M[t-1] (0 at t = 0: the segment starting at 0 is
+  // o + u, hsmm.py:269-274), then the segments of age 0 and 1 (their deltas
+  // fl(fl(M + o) + dur) are the same in every lane of the group) and Dm[t].
+  float M = 0.f, v0 = -INFINITY, dmt = -INFINITY, lm = -INFINITY;
+  auto chain1 = [&](const float4 (&dq)[NPRED / 4]) {
+    // M[t-1][s] = max_{s' != s} fl(Dm[t-1][s'] + logT[s'][s]) (the first s' attaining it is
+    // recovered by the backtrace from the stored Dm row, for the path's segments only)
+    lm = -INFINITY;
+    if constexpr (kAbl & (1 << 20)) {  // ablation: no predecessor scores (timing only)
+      lm = lt2[0][0];
+      return;
+    }
+#pragma unroll
+    for (int i = 0; i < NPRED / 4; ++i) {
+      // lt == -inf (excluded s') or dm == -inf: the sum is -inf (never +inf: no NaN)
+      const hs_f2 c0 = hs_f2{dq[i].x, dq[i].y} + lt2[2 * i];
+      const hs_f2 c1 = hs_f2{dq[i].z, dq[i].w} + lt2[2 * i + 1];
+      lm = fmaxf(lm, fmaxf(c0.x, c0.y));
+      lm = fmaxf(lm, fmaxf(c1.x, c1.y));
+    }
+  };
+  auto chain2 = [&](const int t) {
+    M = t > 0 ? grp_max<SUB>(lm) : 0.f;  // (t = 0 read an unwritten row: discarded)
+    __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, M), mg_r, t > 0 ? st_off : kHsOOB,
+                                          (t - 1) * S * 4, 0);
+    v0 = (M + xcur) + u0;
+    dmt = fmaxf(fmaxf(mxc, v1c), v0);
+    L.dmx[t & 1][q] = dmt;  // every lane of the group: the same value; -inf for padding states
+    __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, dmt), dg_r, st_off, t * S * 4, 0);
+  };
+  auto read_dq = [&](const int t, float4 (&dq)[NPRED / 4]) {
+    if constexpr (kAbl & (1 << 20)) return;
+    const float4* dp = reinterpret_cast<const float4*>(&L.dmx[(t - 1) & 1][sub * NPRED]);
+#pragma unroll
+    for (int i = 0; i < NPRED / 4; ++i) dq[i] = dp[i];
+  };
+
+  prefetch(0, std::integral_constant<int, 0>{});
+  phase_b(0, std::integral_constant<int, 0>{}, [] {}, [] {});
+  xcur = xnext;
+  mxc = mxn;
+  if (T > 1) prefetch(1, std::integral_constant<int, 1>{});
+  // End times t < T-1: barrier, the LDS reads (predecessor scores, t+2's operands), phase B
+  // of t+1 with the predecessor phase of t between its slot pairs.  One basic block.
+  bool go = T > 1;
+  for (int t0 = 0; go; t0 += NJ)
     static_for<0, NJ>([&](auto Uc) {
-      if (go) go = end_step(t + decltype(Uc)::value, Uc);
+      constexpr int U = decltype(Uc)::value;
+      const int t = t0 + U;
+      if (!go) return;
+      step_barrier();
+      float4 dq[NPRED / 4];
+      read_dq(t, dq);
+      prefetch(t + 2, std::integral_constant<int, U & 1>{});  // in range past T-1: unused
+      phase_b(t + 1, std::integral_constant<int, (U + 1) % NJ>{}, [&] { chain1(dq); }, [&] { chain2(t); });
+      {
+        // the segment that started at t takes M (its slot is j = U, age 1 at t+1)
+        constexpr int pf = U % NP2, hf = U / NP2;
+        mp[pf][hf] = age1 ? M : mp[pf][hf];
+      }
+      v1c = (M + (xcur + xnext)) + u1;  // d = 2 at t+1: torch's sum of two elements
+      xcur = xnext;
+      mxc = mxn;
+      if (t + 2 >= T) {
+        go = false;
+        return;
+      }
+      if ((t + 3) % 64 == 0) {  // rows of chunk c = (t+3)/64 are first read by the prefetch
+        const int cidx = (t + 3) >> 6;  // at t+1, behind the barrier of t+1
+        chunk_store(cidx);
+        if ((cidx + 1) * 64 < T) chunk_load(cidx + 1);
+      }
     });
-  // best over (s asc, d asc) of delta[T-1][s][d-1], strict > (hsmm.py:319-329); each lane
-  // reads back only what it wrote
+  // the last end time: its predecessor phase, then the best over (s asc, d asc) of
+  // delta[T-1][s][d-1], strict > (hsmm.py:319-329): d = 1 and d = 2 (ages 0 and 1) first
   {
     const int t = T - 1;
+    step_barrier();
+    float4 dq[NPRED / 4];
+    read_dq(t, dq);
+    chain1(dq);
+    chain2(t);
     int ld = 0x7fff;
 #pragma unroll
     for (int j = 0; j < NJ; ++j) {
-      const int d = ((Afin - j) & (R - 1)) + 1;
-      if (L.vfin[j][tid] == mxfin && d < ld) ld = d;
+      const int d = ((Af - j) & (R - 1)) + 1;
+      if (vv[j] == dmt && d < ld) ld = d;
     }
+    if (v1c == dmt) ld = 2;
+    if (v0 == dmt) ld = 1;
     ld = grp_min_i<SUB>(ld);
     if (live && sub == 0) L.fd[s] = ld;
     __syncthreads();
@@ -356,16 +431,6 @@ __device__ float hs_obs_sum_global(const float* lp, int S, int t0, int d, int s)
   return r;
 }
 
-// delta of the segment (start st0, state s, duration d), exactly as the forward forms it
-__device__ float hs_delta(const HsArgs& a, const float* lp, const float* Mb, int st0, int s, int d) {
-  if (st0 < 0) return -INFINITY;
-  const float o = hs_obs_sum_global(lp, a.S, st0, d, s);
-  const float u = a.dur[(size_t)s * a.Dm + d - 1];
-  if (st0 == 0) return o + u;
-  const float m = Mb[(size_t)(st0 - 1) * a.S + s];
-  return m == -INFINITY ? -INFINITY : (m + o) + u;
-}
-
 // torch-order sum of the d elements col[d-1-e], e = 0..d-1 (a segment's column in time
 // order, staged newest-first in LDS)
 __device__ __forceinline__ float hs_obs_sum_lds(const float* col, int d) {
@@ -386,11 +451,13 @@ __device__ __forceinline__ float hs_obs_sum_lds(const float* col, int d) {
   return r;
 }
 
-inline size_t hsmm_backtrace_lds(int S, int Dm, int R) { return (size_t)(S * Dm + S * S + R) * sizeof(float); }
+inline size_t hsmm_backtrace_lds(int S, int Dm, int R) {
+  return (size_t)(S * Dm + S * S + R + 2 * 64 * Dm) * sizeof(float);
+}
 
 // R >= the longest duration; every lane owns the candidates d' = l + 1 + 64k, k < R/64, and
-// the predecessor states s' = l + 64k, k < SMAX/64.  LDS: dur (S, Dm), logT (S, S) and the
-// predecessor's candidate column lp[tau - e][s1], e < Dm.
+// the predecessor states s' = l + 64k, k < SMAX/64.  LDS: dur (S, Dm), logT (S, S), the
+// predecessor's candidate column lp[tau - e][s1], e < Dm, and the rare path's columns.
 template <int R, int SMAX>
 __global__ void __launch_bounds__(64) hsmm_backtrace_kernel(HsArgs a) {
   constexpr int K = R / 64;
@@ -401,6 +468,8 @@ __global__ void __launch_bounds__(64) hsmm_backtrace_kernel(HsArgs a) {
   float* sdur = reinterpret_cast<float*>(bsm);
   float* slt = sdur + S * Dm;
   float* pcol = slt + S * S;
+  float* rcol = pcol + R;       // rare path: lp[tau - e][s'], (e, s' mod 64)
+  float* rmc = rcol + 64 * Dm;  //            M[tau - e - 1][s']
   for (int i = l; i < S * Dm; i += 64) sdur[i] = a.dur[i];
   for (int i = l; i < S * S; i += 64) slt[i] = a.logT[i];
   const float* lp = a.lp + (size_t)b * T * S;
@@ -490,21 +559,69 @@ __global__ void __launch_bounds__(64) hsmm_backtrace_kernel(HsArgs a) {
       const float u = sdur[cs * Dm + cd - 1];
       const float F = (M + o) + u;
       if (xb != -INFINITY && (xb + o) + u == F) {
-        // rare: an earlier candidate rounds to the same total — the first one wins (hsmm.py:308)
-        const int p1 = ns * Dm + (nd - 1);
-        int win = p1;
-        for (int base = 0; base < p1; base += 64) {
-          const int k = base + l;
-          bool h2 = false;
-          if (k < p1) {
-            const int sp = k / Dm, dp = k % Dm + 1;
-            if (sp != cs && dp <= tau + 1) {
-              const float c2 = hs_delta(a, lp, Mb, tau - dp + 1, sp, dp);
-              if (c2 != -INFINITY) h2 = ((c2 + slt[sp * S + cs]) + o) + u == F;
+        // rare: an earlier candidate rounds to the same total — the first one wins
+        // (hsmm.py:308).  Lane l takes the predecessor state s' = l + 64k: both columns
+        // (lp and M, d' <= dlim) are staged for 64 states at once, each lane walks its own
+        // d' ascending, and the lowest state with a hit wins.
+        int win = ns * Dm + (nd - 1);  // p1 when no earlier candidate hits
+        for (int k = 0; 64 * k <= ns; ++k) {
+          const int sp = l + 64 * k;
+          const bool in = sp < S;
+          for (int e0 = 0; e0 < dlim; e0 += 16) {  // 16 loads of each column in flight
+            float cv2[16], mv2[16];
+#pragma unroll
+            for (int j = 0; j < 16; ++j) {
+              const int e = e0 + j;
+              const bool ok = in && e < dlim;
+              cv2[j] = ok ? lp[(size_t)(tau - e) * S + sp] : 0.f;
+              mv2[j] = (ok && tau - e >= 1) ? Mb[(size_t)(tau - e - 1) * S + sp] : 0.f;
+            }
+#pragma unroll
+            for (int j = 0; j < 16; ++j) {
+              if (e0 + j < dlim) {
+                rcol[(e0 + j) * 64 + l] = cv2[j];
+                rmc[(e0 + j) * 64 + l] = mv2[j];
+              }
             }
           }
-          const unsigned long long m2 = __ballot(h2);
-          if (m2) { win = base + __ffsll((long long)m2) - 1; break; }
+          __syncthreads();
+          int first = 0;
+          if (in && sp <= ns && sp != cs) {
+            const int lim = sp == ns ? nd - 1 : dlim;
+            const float ltc = slt[sp * S + cs];
+            for (int dp = 1; dp <= lim; ++dp) {
+              // delta of (s', d'), exactly as the forward forms it: torch-order sum of the
+              // d' elements rcol[e][l], e = d'-1 .. 0 (time order)
+              float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
+              const int m = dp & ~3;
+              int i = 0;
+              for (; i < m; i += 4) {
+                a0 += rcol[(dp - 1 - i) * 64 + l];
+                a1 += rcol[(dp - 2 - i) * 64 + l];
+                a2 += rcol[(dp - 3 - i) * 64 + l];
+                a3 += rcol[(dp - 4 - i) * 64 + l];
+              }
+              for (; i < dp; ++i) a0 += rcol[(dp - 1 - i) * 64 + l];
+              float oc = 0.f + a0;
+              oc = oc + a1;
+              oc = oc + a2;
+              oc = oc + a3;
+              const float uc = sdur[sp * Dm + dp - 1];
+              const float mc = rmc[(dp - 1) * 64 + l];
+              const float dlt = tau - dp + 1 == 0 ? oc + uc : (mc == -INFINITY ? -INFINITY : (mc + oc) + uc);
+              if (dlt != -INFINITY && ((dlt + ltc) + o) + u == F) {
+                first = dp;
+                break;
+              }
+            }
+          }
+          const unsigned long long m2 = __ballot(first > 0);
+          if (m2) {
+            const int ln = __ffsll((long long)m2) - 1;
+            win = (ln + 64 * k) * Dm + __shfl(first, ln) - 1;
+            break;
+          }
+          __syncthreads();  // the columns are restaged for the next 64 states
         }
         ns = win / Dm;
         nd = win % Dm + 1;
@@ -520,9 +637,9 @@ __global__ void __launch_bounds__(64) hsmm_backtrace_kernel(HsArgs a) {
 }
 
 // Geometries (S <= SMAX, Dmax < R).  The config-5 class S <= 64, Dmax <= 63 takes the
-// 8-lane form (512 threads, 8 slots per lane: 0.96 ms at config 5, vs 0.97 for 16 lanes and
-// 1.22 for 4 lanes with one wave per SIMD; profiles/r3l_c5_sub*.log) unless HMM355_HSMM_SUB=4
-// or =16 asks for another.  The larger geometries run 512 threads (8 waves) so a lane has 256 VGPRs
+// 4-lane form (256 threads: one wave per SIMD, 16 slots per lane; 0.81 ms at config 5 vs 0.83
+// for 8 lanes and 1.00 for 16, profiles/r3q_c5_sub*.log) unless HMM355_HSMM_SUB=8 or =16
+// asks for another.  The larger geometries run 512 threads (8 waves) so a lane has 256 VGPRs
 // for its 16 slots.  (S <= 128 with 64 <= Dmax <= 127 would need 32 slots per lane: beyond
 // the register file; rejected.)
 enum HsCfg : int { kHs16x4 = 0, kHs8x8s64 = 1, kHs8x16 = 2, kHs4x16 = 3, kHs4x16s64 = 4, kHsNone = -1 };
@@ -531,8 +648,8 @@ inline int hsmm_cfg(int S, int Dm) {
   if (S <= 64 && Dm < 64) {
     const char* e = getenv("HMM355_HSMM_SUB");
     if (e && e[0] == '1' && e[1] == '6') return kHs16x4;
-    if (e && e[0] == '4') return kHs4x16s64;
-    return kHs8x8s64;
+    if (e && e[0] == '8') return kHs8x8s64;
+    return kHs4x16s64;
   }
   if (S <= 64 && Dm < 128) return kHs8x16;
   if (S <= 128 && Dm < 64) return kHs4x16;
@@ -542,13 +659,14 @@ inline int hsmm_cfg(int S, int Dm) {
 template <int SUB, int NJ, int SMAX>
 static hipError_t launch_hsmm(const HsArgs& ha, hipStream_t st) {
   using G = HsG<SUB, NJ, SMAX>;
-  const size_t lds = sizeof(HsLds<SMAX, G::DW, NJ, G::NT>);
+  const size_t lds = sizeof(HsLds<SMAX, G::DW>);
   hipError_t e = allow_lds(hsmm_fwd_kernel<SUB, NJ, SMAX>, lds);
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL((hsmm_fwd_kernel<SUB, NJ, SMAX>), dim3(ha.B), dim3(G::NT), lds, st, ha);
   e = hipGetLastError();
   if (e != hipSuccess) return e;
   const size_t blds = hsmm_backtrace_lds(ha.S, ha.Dm, G::R);
+  if constexpr (kAbl & (1 << 22)) return hipSuccess;  // ablation: forward only (timing)
   e = allow_lds(hsmm_backtrace_kernel<G::R, SMAX>, blds);
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL((hsmm_backtrace_kernel<G::R, SMAX>), dim3(ha.B), dim3(64), blds, st, ha);
