@@ -42,6 +42,8 @@
 //   obs_sum is the one this segment's candidate search already formed.
 #include <stdlib.h>
 
+#include <algorithm>
+
 #include <type_traits>
 
 #include "common.h"
@@ -140,9 +142,19 @@ __global__ void __launch_bounds__((HsG<SUB, NJ, SMAX>::NT)) hsmm_fwd_kernel(HsAr
   auto dur_at = [&](int r, int age) -> float {  // -inf beyond Dmax and for padding states
     return (r < S && age < Dm) ? a.dur[(size_t)r * Dm + age] : -INFINITY;
   };
-  for (int i = tid; i < SMAX * DW; i += NT) {
-    const int r = i / DW, c = i % DW;
-    L.dpair[r][c] = hs_f2{dur_at(r, (c - NJ) & (R - 1)), dur_at(r, (c - NJ - NP2) & (R - 1))};
+  for (int i0 = 0; i0 < SMAX * DW; i0 += 8 * NT) {  // 8 entries per thread in flight
+    hs_f2 v[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const int i = i0 + k * NT + tid, r = i / DW, c = i % DW;
+      v[k] = i < SMAX * DW ? hs_f2{dur_at(r, (c - NJ) & (R - 1)), dur_at(r, (c - NJ - NP2) & (R - 1))}
+                           : hs_f2{0.f, 0.f};
+    }
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const int i = i0 + k * NT + tid;
+      if (i < SMAX * DW) L.dpair[i / DW][i % DW] = v[k];
+    }
   }
   const float u0 = dur_at(s, 0), u1 = dur_at(s, 1);  // duration terms of d = 1, 2
   hs_f2 lt2[NPRED / 2];  // log T[s'][s] for the lane's predecessors s' = sub + SUB j (-inf: excluded)
@@ -412,25 +424,6 @@ __global__ void __launch_bounds__((HsG<SUB, NJ, SMAX>::NT)) hsmm_fwd_kernel(HsAr
   }
 }
 
-// torch-order sum of lp[t0 .. t0+d-1][s] from global memory
-__device__ float hs_obs_sum_global(const float* lp, int S, int t0, int d, int s) {
-  float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
-  const int m = d & ~3;
-  int i = 0;
-  for (; i < m; i += 4) {
-    a0 += lp[(size_t)(t0 + i) * S + s];
-    a1 += lp[(size_t)(t0 + i + 1) * S + s];
-    a2 += lp[(size_t)(t0 + i + 2) * S + s];
-    a3 += lp[(size_t)(t0 + i + 3) * S + s];
-  }
-  for (; i < d; ++i) a0 += lp[(size_t)(t0 + i) * S + s];
-  float r = 0.f + a0;
-  r = r + a1;
-  r = r + a2;
-  r = r + a3;
-  return r;
-}
-
 // torch-order sum of the d elements col[d-1-e], e = 0..d-1 (a segment's column in time
 // order, staged newest-first in LDS)
 __device__ __forceinline__ float hs_obs_sum_lds(const float* col, int d) {
@@ -451,38 +444,107 @@ __device__ __forceinline__ float hs_obs_sum_lds(const float* col, int d) {
   return r;
 }
 
-inline size_t hsmm_backtrace_lds(int S, int Dm, int R) {
+// The segment walker of the backtrace (hsmm.py:331-352), one wave.  R >= the longest
+// duration; every lane owns the candidates d' = l + 1 + 64k, k < R/64, and the predecessor
+// states s' = l + 64k, k < SMAX/64.  LDS: dur (S, Dm), logT (S, S), the predecessor's
+// candidate column lp[tau - e][s1], e < Dm, and the tie path's columns.
+struct HsWalk {
+  const float* lp;  // this sequence's (T, S) rows
+  const float* Mb;
+  const float* Db;
+  float* sdur;
+  float* slt;
+  float* pcol;
+  float* rcol;  // tie path: lp[tau - e][s'], (e, s' mod 64)
+  float* rmc;   //           M[tau - e - 1][s']
+  int T, S, Dm;
+};
+
+// torch-order sum of lp[t0 .. t0+d-1][s] by one wave (d <= 128): the column is staged in
+// `scratch` with all its loads in flight, then summed from LDS (a loop over global loads
+// waits for each group of four in turn)
+__device__ float hs_obs_sum_wave(const float* lp, int S, int t0, int d, int s, float* scratch, int l) {
+  float v[2];
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    const int e = l + 64 * k;
+    v[k] = e < d ? lp[(size_t)(t0 + d - 1 - e) * S + s] : 0.f;
+  }
+#pragma unroll
+  for (int k = 0; k < 2; ++k)
+    if (l + 64 * k < d) scratch[l + 64 * k] = v[k];
+  __syncthreads();
+  const float r = hs_obs_sum_lds(scratch, d);
+  __syncthreads();
+  return r;
+}
+
+__host__ __device__ inline size_t align16(size_t x) { return (x + 15) & ~(size_t)15; }
+__host__ __device__ inline size_t hsmm_walk_lds(int S, int Dm, int R) {
   return (size_t)(S * Dm + S * S + R + 2 * 64 * Dm) * sizeof(float);
 }
 
-// R >= the longest duration; every lane owns the candidates d' = l + 1 + 64k, k < R/64, and
-// the predecessor states s' = l + 64k, k < SMAX/64.  LDS: dur (S, Dm), logT (S, S), the
-// predecessor's candidate column lp[tau - e][s1], e < Dm, and the rare path's columns.
-template <int R, int SMAX>
-__global__ void __launch_bounds__(64) hsmm_backtrace_kernel(HsArgs a) {
+// global -> LDS copy by one wave, 16 loads per lane in flight (a plain strided loop waits
+// for each load before the next: one round trip per 64 values)
+__device__ __forceinline__ void hs_copy_lds(float* dst, const float* src, int n, int l) {
+  for (int i0 = 0; i0 < n; i0 += 64 * 16) {
+    float v[16];
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+      const int i = i0 + 64 * k + l;
+      v[k] = i < n ? src[i] : 0.f;
+    }
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+      const int i = i0 + 64 * k + l;
+      if (i < n) dst[i] = v[k];
+    }
+  }
+}
+
+// tables into LDS (the caller's barrier publishes them)
+template <int R>
+__device__ HsWalk hs_walk_init(const HsArgs& a, char* bsm, int b, int l) {
+  HsWalk w;
+  w.T = a.T;
+  w.S = a.S;
+  w.Dm = a.Dm;
+  const size_t off = (size_t)b * a.T * a.S;
+  w.lp = a.lp + off;
+  w.Mb = a.Mg + off;
+  w.Db = a.Dg + off;
+  w.sdur = reinterpret_cast<float*>(bsm);
+  w.slt = w.sdur + a.S * a.Dm;
+  w.pcol = w.slt + a.S * a.S;
+  w.rcol = w.pcol + R;
+  w.rmc = w.rcol + 64 * a.Dm;
+  hs_copy_lds(w.sdur, a.dur, a.S * a.Dm, l);
+  hs_copy_lds(w.slt, a.logT, a.S * a.S, l);
+  return w;
+}
+
+// Walks from the segment (end t, state cs, duration cd, obs_sum o) towards t = 0, calling
+// emit(t, cs, cd, o, start) for every segment in walk order (the first one included); stops
+// when emit returns true, or after the first segment that ends below `stop`, starts at 0, or
+// has no predecessor.
+template <int R, int SMAX, typename Emit>
+__device__ void hs_walk(const HsWalk& w, int l, int t, int cs, int cd, float o, int stop, Emit&& emit) {
   constexpr int K = R / 64;
   constexpr int KS = (SMAX + 63) / 64;
-  extern __shared__ __attribute__((aligned(16))) char bsm[];
-  const int b = blockIdx.x, l = threadIdx.x;
-  const int T = a.T, S = a.S, Dm = a.Dm;
-  float* sdur = reinterpret_cast<float*>(bsm);
-  float* slt = sdur + S * Dm;
-  float* pcol = slt + S * S;
-  float* rcol = pcol + R;       // rare path: lp[tau - e][s'], (e, s' mod 64)
-  float* rmc = rcol + 64 * Dm;  //            M[tau - e - 1][s']
-  for (int i = l; i < S * Dm; i += 64) sdur[i] = a.dur[i];
-  for (int i = l; i < S * S; i += 64) slt[i] = a.logT[i];
-  const float* lp = a.lp + (size_t)b * T * S;
-  const float* Mb = a.Mg + (size_t)b * T * S;
-  const float* Db = a.Dg + (size_t)b * T * S;
-  int t = T - 1, cs = a.fin[2 * b], cd = a.fin[2 * b + 1];
-  float o = hs_obs_sum_global(lp, S, T - cd, cd, cs);  // the current segment's obs_sum
-  __syncthreads();
+  const int S = w.S, Dm = w.Dm;
+  const float* lp = w.lp;
+  const float* Mb = w.Mb;
+  const float* Db = w.Db;
+  float* sdur = w.sdur;
+  float* slt = w.slt;
+  float* pcol = w.pcol;
+  float* rcol = w.rcol;
+  float* rmc = w.rmc;
   while (t >= 0 && cd > 0) {
     int start = t - cd + 1;
     if (start < 0) start = 0;
-    for (int u = start + l; u <= t; u += 64) a.states[(size_t)b * T + u] = cs;
-    if (start == 0) break;
+    if (emit(t, cs, cd, o, start)) return;
+    if (start == 0 || t < stop) return;
     const int tau = start - 1;  // end of the previous segment
     // round trip 1: M and the Dm row at tau
     const float M = Mb[(size_t)tau * S + cs];
@@ -625,7 +687,7 @@ __global__ void __launch_bounds__(64) hsmm_backtrace_kernel(HsArgs a) {
         }
         ns = win / Dm;
         nd = win % Dm + 1;
-        on = hs_obs_sum_global(lp, S, tau - nd + 1, nd, ns);
+        on = hs_obs_sum_wave(lp, S, tau - nd + 1, nd, ns, pcol, l);
       }
       __syncthreads();  // the column is restaged for the next segment
     }
@@ -634,6 +696,193 @@ __global__ void __launch_bounds__(64) hsmm_backtrace_kernel(HsArgs a) {
     cd = nd;
     o = on;
   }
+}
+
+__device__ __forceinline__ void hs_write_states(int64_t* st, int start, int t, int cs, int l) {
+  for (int u = start + l; u <= t; u += 64) st[u] = cs;
+}
+
+// the serial backtrace: one wave walks the whole sequence from the final segment
+template <int R, int SMAX>
+__global__ void __launch_bounds__(64) hsmm_backtrace_kernel(HsArgs a) {
+  extern __shared__ __attribute__((aligned(16))) char bsm[];
+  const int b = blockIdx.x, l = threadIdx.x;
+  const HsWalk w = hs_walk_init<R>(a, bsm, b, l);
+  const int T = a.T, cs = a.fin[2 * b], cd = a.fin[2 * b + 1];
+  const float o = hs_obs_sum_wave(w.lp, a.S, T - cd, cd, cs, w.pcol, l);
+  int64_t* st = a.states + (size_t)b * T;
+  hs_walk<R, SMAX>(w, l, T - 1, cs, cd, o, -1, [&](int t, int s, int, float, int start) {
+    hs_write_states(st, start, t, s, l);
+    return false;
+  });
+}
+
+// ---- chunked backtrace: the walk is one dependent chain of segments (≈ 1-2 µs each), so
+// it is cut into time chunks of kHsChunk frames walked in parallel and stitched exactly.
+// hsmm_chunk_walk_kernel: chunk c's wave walks from a guessed segment 128 frames above
+//   the chunk (the best state ending there, d = 1; the true final segment for the top
+//   chunks) down to the first segment ending below c * kHsChunk, recording every segment.
+//   Walks from different segments merge quickly (the backpointers coalesce).
+// hsmm_stitch_kernel: one wave per sequence runs the chunks top-down with the true segment
+//   entering each chunk: found in the chunk's record, the record from there IS the true
+//   path (the walk is a deterministic function of the segment, its tie resolution included);
+//   not found (the guessed walk had not merged yet), the true walk continues serially until
+//   it meets the record or leaves the chunk.  Either way the result is the serial walk's, bit
+//   for bit.  (Warm-up 64 / 128 / 192 frames: the same within 1 % at config 5,
+//   profiles/r3u_warm.log.)
+constexpr int kHsChunk = 64;
+constexpr int kHsWarmMax = 256;
+inline int hsmm_warm() {  // frames walked above a chunk before it (HMM355_HSMM_WARM, diagnostic)
+  const char* e = getenv("HMM355_HSMM_WARM");
+  const int w = e ? atoi(e) : 128;
+  return w < 0 ? 0 : (w > kHsWarmMax ? kHsWarmMax : w);
+}
+constexpr int kHsCap = kHsChunk + kHsWarmMax + 2;  // segments per record (each >= 1 frame)
+struct HsChunks {
+  int4* rec;  // (B, C, kHsCap): {end, state, duration, obs_sum bits}
+  int* cnt;   // (B, C)
+  int C;
+  int warm;
+  int stage;  // chunks whose first 64 records the stitch stages in LDS (the top ones)
+};
+
+template <int R, int SMAX>
+__global__ void __launch_bounds__(64) hsmm_chunk_walk_kernel(HsArgs a, HsChunks c) {
+  extern __shared__ __attribute__((aligned(16))) char bsm[];
+  const int ch = blockIdx.x, b = blockIdx.y, l = threadIdx.x;
+  const int T = a.T, S = a.S;
+  const HsWalk w = hs_walk_init<R>(a, bsm, b, l);
+  const int t0 = min(T - 1, (ch + 1) * kHsChunk + c.warm - 1);
+  int cs, cd;
+  if (t0 == T - 1) {
+    cs = a.fin[2 * b];
+    cd = a.fin[2 * b + 1];
+  } else {
+    float bv = -INFINITY;
+    int bi = 0x7fffffff;
+#pragma unroll
+    for (int k = 0; k < (SMAX + 63) / 64; ++k) {
+      const int sp = l + 64 * k;
+      if (sp < S) argmax_combine(bv, bi, w.Db[(size_t)t0 * S + sp], sp);
+    }
+    wave_argmax(bv, bi);
+    cs = bi < S ? bi : 0;
+    cd = 1;
+  }
+  const float o = hs_obs_sum_wave(w.lp, S, t0 - cd + 1, cd, cs, w.pcol, l);
+  // the record is kept in LDS during the walk (a global store per segment would put its
+  // completion on the walk's next load) and written out at the end
+  int4* lrec = reinterpret_cast<int4*>(bsm + align16(hsmm_walk_lds(S, a.Dm, R)));
+  int n = 0;
+  hs_walk<R, SMAX>(w, l, t0, cs, cd, o, ch * kHsChunk, [&](int t, int s, int d, float ob, int) {
+    if (l == 0 && n < kHsCap) lrec[n] = make_int4(t, s, d, __float_as_int(ob));
+    ++n;
+    return false;
+  });
+  n = n < kHsCap ? n : kHsCap;
+  __syncthreads();
+  int4* rec = c.rec + ((size_t)b * c.C + ch) * kHsCap;
+  for (int j = l; j < n; j += 64) rec[j] = lrec[j];
+  if (l == 0) c.cnt[(size_t)b * c.C + ch] = n;
+}
+
+
+template <int R, int SMAX>
+__global__ void __launch_bounds__(64) hsmm_stitch_kernel(HsArgs a, HsChunks c) {
+  extern __shared__ __attribute__((aligned(16))) char bsm[];
+  const int b = blockIdx.x, l = threadIdx.x;
+  const int T = a.T;
+  const HsWalk w = hs_walk_init<R>(a, bsm, b, l);
+  // after the walker's tables: the first 64 records of the top kHsStage chunks, their counts
+  int4* srec = reinterpret_cast<int4*>(bsm + align16(hsmm_walk_lds(a.S, a.Dm, R)));
+  int* scnt = reinterpret_cast<int*>(srec + c.stage * 64);
+  const int4* recb = c.rec + (size_t)b * c.C * kHsCap;
+  const int* cntb = c.cnt + (size_t)b * c.C;
+  const int c0 = c.C - c.stage;  // staged: chunks c0 .. C-1
+  // independent loads (entries past a record's count are read but never used): one round trip
+  for (int ch = c0; ch < c.C; ++ch) srec[(ch - c0) * 64 + l] = recb[(size_t)ch * kHsCap + l];
+  for (int k = l; k < c.stage; k += 64) scnt[k] = cntb[c0 + k];
+  int t = T - 1, cs = a.fin[2 * b], cd = a.fin[2 * b + 1];
+  float o = hs_obs_sum_wave(w.lp, a.S, T - cd, cd, cs, w.pcol, l);
+  int64_t* st = a.states + (size_t)b * T;
+  // Records come from LDS (staged, n <= 64) or from global memory, never both in one loop:
+  // a load that may come from either makes the compiler wait for every outstanding global
+  // operation at the join, the state stores included.
+  auto from_lds = [&](int ch) { return [&, ch](int j) { return srec[(ch - c0) * 64 + j]; }; };
+  auto from_glb = [&](int ch) { return [&, ch](int j) { return recb[(size_t)ch * kHsCap + j]; }; };
+  bool done = false;
+  int serial = 0;  // segments the stitch walked itself (diagnostic count, after the chunk counts)
+  // the true segment (t, cs, cd) in chunk ch's record (n entries): its index, or -1
+  auto find = [&](auto&& rd, int n) -> int {
+    for (int base = 0; base < n; base += 64) {
+      const int4 e = base + l < n ? rd(base + l) : make_int4(-1, -1, -1, 0);
+      const unsigned long long m = __ballot(e.x == t && e.y == cs && e.z == cd);
+      if (m) return base + __ffsll((long long)m) - 1;
+    }
+    return -1;
+  };
+  // the record from index j on is the true path: write it down to the next chunk's entry
+  auto follow = [&](auto&& rd, int j, int n, int lo) {
+    for (;; ++j) {
+      if (j >= n) {  // the walk ended (no predecessor): nothing below is written
+        done = true;
+        return;
+      }
+      const int4 e = rd(j);  // the same address in every lane: a broadcast
+      if (e.x < lo) {  // enters the next chunk down
+        t = e.x;
+        cs = e.y;
+        cd = e.z;
+        o = __int_as_float(e.w);
+        return;
+      }
+      const int start = e.x - e.z + 1 < 0 ? 0 : e.x - e.z + 1;
+      hs_write_states(st, start, e.x, e.y, l);
+      if (start == 0) {
+        done = true;
+        return;
+      }
+    }
+  };
+  for (int ch = c.C - 1; ch >= 0 && !done; --ch) {
+    const int lo = ch * kHsChunk;
+    const bool lds = ch >= c0 && scnt[ch - c0] <= 64;
+    const int n = ch >= c0 ? scnt[ch - c0] : cntb[ch];
+    int at = lds ? find(from_lds(ch), n) : find(from_glb(ch), n);
+    if (at < 0) {
+      // not merged: walk serially from the true segment until it meets the record's first
+      // 64 segments (then the record is the true path from there) or leaves the chunk
+      bool below = false;
+      const int4 e0 = l < n ? (lds ? srec[(ch - c0) * 64 + l] : recb[(size_t)ch * kHsCap + l])
+                            : make_int4(-1, -1, -1, 0);
+      hs_walk<R, SMAX>(w, l, t, cs, cd, o, lo, [&](int et, int es, int ed, float eo, int start) {
+        ++serial;
+        if (et < lo) {
+          t = et;
+          cs = es;
+          cd = ed;
+          o = eo;
+          below = true;
+          return true;
+        }
+        const unsigned long long m = __ballot(e0.x == et && e0.y == es && e0.z == ed);
+        if (m) {
+          at = __ffsll((long long)m) - 1;
+          return true;
+        }
+        hs_write_states(st, start, et, es, l);
+        return false;
+      });
+      if (at < 0 && !below) done = true;
+    }
+    if (at >= 0) {
+      if (lds)
+        follow(from_lds(ch), at, n, lo);
+      else
+        follow(from_glb(ch), at, n, lo);
+    }
+  }
+  if (l == 0) c.cnt[(size_t)a.B * c.C + b] = serial;
 }
 
 // Geometries (S <= SMAX, Dmax < R).  The config-5 class S <= 64, Dmax <= 63 takes the
@@ -656,8 +905,15 @@ inline int hsmm_cfg(int S, int Dm) {
   return kHsNone;
 }
 
+inline int hsmm_chunks(int T) { return (T + kHsChunk - 1) / kHsChunk; }
+// the chunked backtrace from 3 chunks up (HMM355_HSMM_SERIAL=1: always the serial walk)
+inline bool hsmm_use_chunks(int T) {
+  const char* e = getenv("HMM355_HSMM_SERIAL");
+  return hsmm_chunks(T) >= 3 && !(e && e[0] == '1');
+}
+
 template <int SUB, int NJ, int SMAX>
-static hipError_t launch_hsmm(const HsArgs& ha, hipStream_t st) {
+static hipError_t launch_hsmm(const HsArgs& ha, const HsChunks& hc, hipStream_t st) {
   using G = HsG<SUB, NJ, SMAX>;
   const size_t lds = sizeof(HsLds<SMAX, G::DW>);
   hipError_t e = allow_lds(hsmm_fwd_kernel<SUB, NJ, SMAX>, lds);
@@ -665,8 +921,21 @@ static hipError_t launch_hsmm(const HsArgs& ha, hipStream_t st) {
   hipLaunchKernelGGL((hsmm_fwd_kernel<SUB, NJ, SMAX>), dim3(ha.B), dim3(G::NT), lds, st, ha);
   e = hipGetLastError();
   if (e != hipSuccess) return e;
-  const size_t blds = hsmm_backtrace_lds(ha.S, ha.Dm, G::R);
   if constexpr (kAbl & (1 << 22)) return hipSuccess;  // ablation: forward only (timing)
+  const size_t blds = hsmm_walk_lds(ha.S, ha.Dm, G::R);
+  if (hsmm_use_chunks(ha.T)) {
+    const size_t wlds = align16(blds) + kHsCap * sizeof(int4);
+    if ((e = allow_lds(hsmm_chunk_walk_kernel<G::R, SMAX>, wlds)) != hipSuccess) return e;
+    HsChunks hs = hc;
+    const long room = 163840 - (long)align16(blds) - 16;
+    hs.stage = (int)std::min<long>(hc.C, std::max<long>(0, room / (long)(64 * sizeof(int4) + sizeof(int))));
+    const size_t slds = align16(blds) + hs.stage * 64 * sizeof(int4) + hs.stage * sizeof(int);
+    if ((e = allow_lds(hsmm_stitch_kernel<G::R, SMAX>, slds)) != hipSuccess) return e;
+    hipLaunchKernelGGL((hsmm_chunk_walk_kernel<G::R, SMAX>), dim3(hc.C, ha.B), dim3(64), wlds, st, ha, hc);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    hipLaunchKernelGGL((hsmm_stitch_kernel<G::R, SMAX>), dim3(ha.B), dim3(64), slds, st, ha, hs);
+    return hipGetLastError();
+  }
   e = allow_lds(hsmm_backtrace_kernel<G::R, SMAX>, blds);
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL((hsmm_backtrace_kernel<G::R, SMAX>), dim3(ha.B), dim3(64), blds, st, ha);
@@ -679,8 +948,9 @@ using namespace hmm355;
 
 HMM355_API size_t hmm355_hsmm_workspace_bytes(int B, int T, int S, int Dmax) {
   if (B < 0 || T < 1 || hsmm_cfg(S, Dmax) == kHsNone) return 0;
-  const size_t n = (size_t)B * T * S;
-  return 2 * align_up(n * 4, 256) + align_up((size_t)B * 8, 256);
+  const size_t n = (size_t)B * T * S, nc = (size_t)B * hsmm_chunks(T);
+  return 2 * align_up(n * 4, 256) + align_up((size_t)B * 8, 256) + align_up(nc * kHsCap * sizeof(int4), 256) +
+         align_up((nc + B) * 4, 256);
 }
 
 HMM355_API int hmm355_hsmm_viterbi_f32(const float* lp, const float* dur_lp, const float* log_T, int B, int T,
@@ -698,15 +968,19 @@ HMM355_API int hmm355_hsmm_viterbi_f32(const float* lp, const float* dur_lp, con
   float* Mg = reinterpret_cast<float*>(ws);
   float* Dg = reinterpret_cast<float*>(ws + align_up(n * 4, 256));
   int* fin = reinterpret_cast<int*>(ws + 2 * align_up(n * 4, 256));
+  const size_t nc = (size_t)B * hsmm_chunks(T);
+  int4* rec = reinterpret_cast<int4*>(ws + 2 * align_up(n * 4, 256) + align_up((size_t)B * 8, 256));
+  int* cnt = reinterpret_cast<int*>(reinterpret_cast<char*>(rec) + align_up(nc * kHsCap * sizeof(int4), 256));
   HsArgs ha{lp, dur_lp, log_T, Mg, Dg, fin, scores, states, B, T, S, Dmax};
+  HsChunks hc{rec, cnt, hsmm_chunks(T), hsmm_warm(), 0};
   hipStream_t st = static_cast<hipStream_t>(stream);
   hipError_t e;
   switch (hsmm_cfg(S, Dmax)) {
-    case kHs16x4: e = launch_hsmm<16, 4, 64>(ha, st); break;
-    case kHs8x8s64: e = launch_hsmm<8, 8, 64>(ha, st); break;
-    case kHs4x16s64: e = launch_hsmm<4, 16, 64>(ha, st); break;
-    case kHs8x16: e = launch_hsmm<8, 16, 64>(ha, st); break;
-    default: e = launch_hsmm<4, 16, 128>(ha, st); break;
+    case kHs16x4: e = launch_hsmm<16, 4, 64>(ha, hc, st); break;
+    case kHs8x8s64: e = launch_hsmm<8, 8, 64>(ha, hc, st); break;
+    case kHs4x16s64: e = launch_hsmm<4, 16, 64>(ha, hc, st); break;
+    case kHs8x16: e = launch_hsmm<8, 16, 64>(ha, hc, st); break;
+    default: e = launch_hsmm<4, 16, 128>(ha, hc, st); break;
   }
   return e == hipSuccess ? HMM355_OK : (int)e;
 }

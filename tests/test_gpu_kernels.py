@@ -204,6 +204,35 @@ def test_hsmm_vs_c_oracle(B, T, S, Dm, sub, monkeypatch):
     assert np.array_equal(scores.cpu().numpy(), csc)
 
 
+@pytest.mark.parametrize("case", ["random", "peaked", "ties", "longdur", "s128"])
+def test_hsmm_chunked_backtrace_equals_serial(case, monkeypatch):
+    """The chunked backtrace (parallel chunk walks from guessed segments, stitched top-down,
+    csrc/hsmm.hip) against the serial walk and the C oracle: uniform random tables (short
+    segments), peaked emissions (long segments), coarse tie-heavy values, Dmax > the 64-frame
+    chunk, and 128 states."""
+    rng = np.random.default_rng(11)
+    B, T, S, Dm = {"random": (3, 700, 64, 40), "peaked": (2, 900, 32, 60), "ties": (2, 500, 20, 30),
+                   "longdur": (2, 600, 16, 127), "s128": (2, 400, 128, 40)}[case]
+    lp = (-(rng.random((B, T, S), dtype=np.float32) * 40 + 80)).astype(np.float32)
+    if case == "peaked":  # one favoured state per 37-frame run: long segments
+        good = (np.arange(T)[:, None] // 37) % S == np.arange(S)[None, :]
+        lp = (lp - 30 * ~good[None]).astype(np.float32)
+    if case == "ties":
+        lp = np.round(lp).astype(np.float32)
+    dur = np.log(rng.random((S, Dm), dtype=np.float32) + np.float32(1e-8)).astype(np.float32)
+    logT = np.log(rng.random((S, S), dtype=np.float32) + np.float32(1e-8)).astype(np.float32)
+    if case == "ties":
+        dur, logT = np.round(dur).astype(np.float32), np.round(logT).astype(np.float32)
+    cs, csc = O.c_hsmm(lp, dur, logT)
+    o = ops()
+    monkeypatch.setenv("HMM355_HSMM_SERIAL", "1")
+    s1, sc1 = o.hsmm_viterbi(t(lp), t(dur), t(logT))
+    monkeypatch.setenv("HMM355_HSMM_SERIAL", "0")
+    s2, sc2 = o.hsmm_viterbi(t(lp), t(dur), t(logT))
+    assert np.array_equal(s1.cpu().numpy(), cs) and np.array_equal(sc1.cpu().numpy(), csc)
+    assert np.array_equal(s2.cpu().numpy(), cs) and np.array_equal(sc2.cpu().numpy(), csc)
+
+
 @pytest.mark.parametrize("sub", ["4", "8", "16"])
 def test_hsmm_impossible_transitions_and_durations(sub, monkeypatch):
     """-inf in the tables (a left-to-right transition matrix, durations below a minimum, a state
