@@ -33,13 +33,14 @@
 //   segments starting at t+1) and Dm[t][s].  Geometries: (4, 16, 64) for the config-5 class
 //   (S <= 64, Dmax <= 63), (8, 8, 64) / (16, 4, 64) the same with 8- and 16-lane groups, (8, 16, 64) for Dmax <= 127 and (4, 16, 128) for 65 <= S <= 128 with
 //   Dmax <= 63.
-// hsmm_backtrace_kernel: one wave per sequence walks the segments (hsmm.py:331-352); for each
-//   segment it finds the first predecessor state attaining M from the stored Dm row (the
-//   forward's own candidate values), recomputes, bit-identically, that state's candidate
-//   deltas to find the first d' and xb (the best total of the earlier candidates), and
-//   re-resolves the rare case where an earlier candidate rounds to the same total.  Two
-//   dependent global round trips per segment; the tables sit in LDS and the next segment's
-//   obs_sum is the one this segment's candidate search already formed.
+// hsmm_backtrace_kernel / hsmm_chunk_walk_kernel + hsmm_stitch_kernel: the walk over the
+//   segments (hsmm.py:331-352).  For each segment it finds the first predecessor state
+//   attaining M from the stored Dm row (the forward's own candidate values), recomputes,
+//   bit-identically, that state's candidate deltas to find the first d' and xb (the best
+//   total of the earlier candidates), and re-resolves the rare case where an earlier
+//   candidate rounds to the same total.  Two dependent global round trips per segment, so
+//   from 3 chunks of 64 frames up the walk is cut into chunks walked in parallel and stitched
+//   exactly (see hsmm_chunk_walk_kernel).
 #include <stdlib.h>
 
 #include <algorithm>
