@@ -48,6 +48,9 @@ def parse():
                    help="strong scaling: --batch is the GLOBAL batch, split over the ranks "
                         "(default: weak scaling, --batch sequences per rank)")
     p.add_argument("--serial", action="store_true", help="run FB and Viterbi on one stream")
+    p.add_argument("--overlap-steps", action="store_true",
+                   help="layer workloads c2/c3/c5: consecutive steps on two alternating streams (step "
+                        "k+1's emission beside step k's recursion; two batches in flight)")
     p.add_argument("--cpu-seconds", type=float, default=12.0, help="bounded CPU-baseline budget (0 = skip)")
     p.add_argument("--no-graph", action="store_true",
                    help="launch every step eagerly instead of replaying one captured HIP graph")
@@ -352,18 +355,48 @@ def layer_workload(args, rank, world, dev):
         dom, flops, bytes_ = "hsmm_fwd_kernel", 2.0 * (S * S * Dm + S * S) * B * T, (4 * S + 8) * B * T
         models = {"hsmm_fwd": ("valu", 2.0 * (S * S * Dm + S * S)), "gmm_score": ("valu64", 4.0 * S * D)}
 
+    # --overlap-steps: consecutive steps alternate between two HIP streams (each step's own
+    # calls stay in order on its stream), so step k+1's full-chip emission scoring runs on the
+    # CUs that step k's per-sequence recursion leaves idle -- the throughput of a stream of
+    # batches, two in flight.  The serial step time (one stream) is measured too and reported
+    # beside it.  Off by default: the default line is one batch at a time.
+    overlap = args.overlap_steps and wl in ("c2", "c3", "c5")
+    main_s = torch.cuda.current_stream(dev)
+    side = [torch.cuda.Stream(dev), torch.cuda.Stream(dev)] if overlap else None
+
+    def run(k):
+        if side is None:
+            return step()
+        with torch.cuda.stream(side[k & 1]):
+            return step()
+    serial_ms = None
     with torch.no_grad():
-        for _ in range(max(args.warmup, 1)):
-            step()
+        for k in range(max(args.warmup, 1)):
+            run(k)
         torch.cuda.synchronize(dev)
+        if overlap:
+            n_ser = min(args.steps, 5)
+            s0, s1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            s0.record()
+            for _ in range(n_ser):
+                step()
+            s1.record()
+            torch.cuda.synchronize(dev)
+            serial_ms = s0.elapsed_time(s1) / n_ser
         if world > 1:
             dist.barrier()
         torch.cuda.synchronize(dev)
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         t0 = time.perf_counter()
         e0.record()
-        for _ in range(args.steps):
-            step()
+        if side is not None:
+            for s_ in side:
+                s_.wait_stream(main_s)
+        for k in range(args.steps):
+            run(k)
+        if side is not None:
+            for s_ in side:
+                main_s.wait_stream(s_)
         e1.record()
         torch.cuda.synchronize(dev)
         if world > 1:
@@ -404,6 +437,10 @@ def layer_workload(args, rank, world, dev):
            "data": "synthetic: randn features, random-init layer (seed 0)",
            "config": dict(desc, global_batch=desc["batch_per_gpu"] * world, parallelism=f"batch-sharded x{world}"),
            "roofline": roof}
+    if overlap:
+        out["step_overlap"] = ("consecutive steps on two alternating HIP streams (two batches in flight): "
+                               "step k+1's emission scoring runs beside step k's recursion")
+        out["ms_per_step_serial"] = serial_ms
     if kroof is not None and roof is not kroof:
         out["kernel_profile"] = kroof
     if rank == 0 and world == 1 and args.cpu_seconds > 0:
