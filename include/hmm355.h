@@ -35,7 +35,7 @@ extern "C" {
 #define HMM355_E_STATES (-2)    /* N outside [1, 256]                                  */
 #define HMM355_E_SHAPE (-3)     /* T < 1, or a size product overflows                  */
 #define HMM355_E_WORKSPACE (-4) /* workspace smaller than *_workspace_bytes() reports   */
-#define HMM355_E_DURATION (-5)  /* HSMM max_duration outside [1, 127] (>63 with S>64)  */
+#define HMM355_E_DURATION (-5)  /* HSMM max_duration outside [1, 1024]                  */
 
 /* Emission encodings accepted by the recursions. */
 #define HMM355_OBS_PROB 0   /* x is a probability: the kernel uses log(x + 1e-8) / x + 1e-8 (hmm.py:86,152) */
@@ -183,9 +183,11 @@ int hmm355_gmm_diag_logprob_f32(const float* x, const float* means, const float*
  * obs_sum, so paths are bit-identical given identical fp32 inputs.
  *   lp (B,T,S) obs log-probs; dur_lp (S,Dmax) = log(p_dur + 1e-8); log_T (S,S)
  *   states (B,T) int64; scores (B) fp32
- *   1 <= S <= 128 (HMM355_E_STATES beyond), 1 <= Dmax <= 127 and Dmax <= 63 when S > 64
- *   (HMM355_E_DURATION beyond): one workgroup per sequence keeps every open segment in
- *   registers and the tables in LDS.
+ *   1 <= S <= 1024 (HMM355_E_STATES beyond), 1 <= Dmax <= 1024 (HMM355_E_DURATION beyond).
+ *   S <= 64 with Dmax <= 127, or S <= 128 with Dmax <= 63: one workgroup per sequence keeps
+ *   every open segment in registers and the tables in LDS (csrc/hsmm.hip); larger sizes take
+ *   the general form (csrc/hsmm_wide.hip: M history and segment sums in the workspace,
+ *   B*T*S*(Dmax+1) floats).
  * ------------------------------------------------------------------------------ */
 size_t hmm355_hsmm_workspace_bytes(int B, int T, int S, int Dmax);
 int hmm355_hsmm_viterbi_f32(const float* lp, const float* dur_lp, const float* log_T, int B,

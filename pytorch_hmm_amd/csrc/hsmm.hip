@@ -943,12 +943,25 @@ static hipError_t launch_hsmm(const HsArgs& ha, const HsChunks& hc, hipStream_t 
   return hipGetLastError();
 }
 
+// hsmm_wide.hip: the general form for sizes the register-slot geometries cannot hold
+size_t hsmm_wide_workspace_bytes(int B, int T, int S, int Dm);
+bool hsmm_wide_fits(int S, int Dm);
+hipError_t launch_hsmm_wide(const float* lp, const float* dur, const float* logT, int B, int T, int S, int Dm,
+                            int64_t* states, float* scores, void* workspace, hipStream_t st);
+// HMM355_HSMM_WIDE=1 takes the general form for every size (tests / comparison)
+inline bool hsmm_wide(int S, int Dm) {
+  const char* e = getenv("HMM355_HSMM_WIDE");
+  return hsmm_wide_fits(S, Dm) && (hsmm_cfg(S, Dm) == kHsNone || (e && e[0] == '1'));
+}
+
 }  // namespace hmm355
 
 using namespace hmm355;
 
 HMM355_API size_t hmm355_hsmm_workspace_bytes(int B, int T, int S, int Dmax) {
-  if (B < 0 || T < 1 || hsmm_cfg(S, Dmax) == kHsNone) return 0;
+  if (B < 0 || T < 1) return 0;
+  if (hsmm_wide(S, Dmax)) return hsmm_wide_workspace_bytes(B, T, S, Dmax);
+  if (hsmm_cfg(S, Dmax) == kHsNone) return 0;
   const size_t n = (size_t)B * T * S, nc = (size_t)B * hsmm_chunks(T);
   return 2 * align_up(n * 4, 256) + align_up((size_t)B * 8, 256) + align_up(nc * kHsCap * sizeof(int4), 256) +
          align_up((nc + B) * 4, 256);
@@ -958,12 +971,18 @@ HMM355_API int hmm355_hsmm_viterbi_f32(const float* lp, const float* dur_lp, con
                                        int S, int Dmax, int64_t* states, float* scores, void* workspace,
                                        size_t workspace_bytes, void* stream) {
   if (B < 0 || S < 0 || Dmax < 0) return HMM355_E_ARG;
-  if (S < 1 || S > kHsSMax) return HMM355_E_STATES;
-  if (Dmax < 1 || Dmax > kHsDMax || hsmm_cfg(S, Dmax) == kHsNone) return HMM355_E_DURATION;  // S > 64: Dmax <= 63
+  if (S < 1 || S > 1024) return HMM355_E_STATES;
+  if (Dmax < 1 || Dmax > 1024) return HMM355_E_DURATION;
   if (T < 1) return HMM355_E_SHAPE;
   if (B == 0) return HMM355_OK;
   if (!lp || !dur_lp || !log_T || !states || !scores || !workspace) return HMM355_E_ARG;
+  if ((size_t)B * T * S * Dmax > ((size_t)1 << 40)) return HMM355_E_SHAPE;
   if (workspace_bytes < hmm355_hsmm_workspace_bytes(B, T, S, Dmax)) return HMM355_E_WORKSPACE;
+  if (hsmm_wide(S, Dmax)) {
+    const hipError_t e = launch_hsmm_wide(lp, dur_lp, log_T, B, T, S, Dmax, states, scores, workspace,
+                                          static_cast<hipStream_t>(stream));
+    return e == hipSuccess ? HMM355_OK : (int)e;
+  }
   const size_t n = (size_t)B * T * S;
   char* ws = static_cast<char*>(workspace);
   float* Mg = reinterpret_cast<float*>(ws);

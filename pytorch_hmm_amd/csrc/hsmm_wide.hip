@@ -1,0 +1,230 @@
+// hmm355 — HSMM segment Viterbi for sizes beyond the register-slot kernels of hsmm.hip
+// (S > 128, Dmax > 127, or S > 64 with Dmax > 63), up to S <= 1024 and Dmax <= 1024.
+//
+// Same recursion and the same exactness argument as hsmm.hip (reference hsmm.py:245-354; the
+// C restatement oracle/hmm_oracle.c hsmm_viterbi_fast, proven equal to the literal 5-deep
+// loop in tests/test_oracle.py):
+//   M[st][s] = max_{s' != s} fl(dmax_{st-1}[s'] + logT[s'][s]),   dmax_{st-1}[s'] = max_d' delta,
+//   delta(end e, s, d) = fl(fl(M[e-d+1][s] + obs_sum(e-d+1, d, s)) + dur[s][d-1])
+//                        (start 0: fl(obs_sum + dur)),
+// and the reference's first-candidate pointer (s' ascending, d' ascending, strict >) is
+// re-resolved exactly where an earlier candidate rounds to the same total.  Instead of
+// keeping every open segment in registers, this form keeps the (T, S) history of M in HBM
+// and the segment sums obs_sum(t0, d, s) in a (T, S, Dmax) table (hsmm_wide_osum_kernel,
+// torch-CPU's 4-accumulator order, O(1) per entry), so its limits are memory, not
+// registers.  The pointers are not stored: the backtrace recomputes the candidate set of
+// each segment it follows (S * Dmax values, one parallel pass per segment).
+//
+// Kernels: hsmm_wide_osum_kernel (one thread per (sequence, start, state)), then
+// hsmm_wide_kernel (one 1024-thread workgroup per sequence: per start time two parallel
+// phases and two barriers, then the segment walk).  Slower than the register-slot kernels
+// (it exists for the sizes they cannot hold), but exact.
+#include <stdint.h>
+#include <stdlib.h>
+
+#include "common.h"
+
+namespace hmm355 {
+
+constexpr int kHwSMax = 1024;
+constexpr int kHwDMax = 1024;
+constexpr int kHwNT = 1024;
+
+struct HwArgs {
+  const float* lp;    // (B,T,S)
+  const float* dur;   // (S,Dm)
+  const float* logT;  // (S,S)
+  float* Mh;          // (B,T,S) M[st][s]
+  float* os;          // (B,T,S,Dm) obs_sum(t0, d, s), d = 1..min(Dm, T - t0)
+  float* scores;      // (B)
+  int64_t* states;    // (B,T)
+  int B, T, S, Dm;
+};
+
+// obs_sum(t0, d, s) for d = 1..Dm in torch-CPU's order (oracle tsum): four strided partial
+// sums over the whole quads, the tail (d mod 4 frames) into the first, then ((a0 + a1) + a2) + a3
+// (with a leading 0 + a0).  The quads are shared by every d, so each entry is O(1).
+__global__ void __launch_bounds__(256) hsmm_wide_osum_kernel(HwArgs a) {
+  const size_t idx = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const size_t n = (size_t)a.B * a.T * a.S;
+  if (idx >= n) return;
+  const int s = (int)(idx % a.S);
+  const size_t bt = idx / a.S;
+  const int t0 = (int)(bt % a.T);
+  const int b = (int)(bt / a.T);
+  const float* col = a.lp + ((size_t)b * a.T + t0) * a.S + s;  // frame t0 + i at col[i * S]
+  float* out = a.os + idx * a.Dm;
+  const int dlim = a.Dm < a.T - t0 ? a.Dm : a.T - t0;
+  float q0 = 0.f, q1 = 0.f, q2 = 0.f, q3 = 0.f;  // sums over the whole quads so far
+  for (int d = 1; d <= dlim; ++d) {
+    const int m = d & ~3;
+    if (m == d && d >= 4) {  // a new whole quad: frames d-4 .. d-1
+      q0 += col[(size_t)(d - 4) * a.S];
+      q1 += col[(size_t)(d - 3) * a.S];
+      q2 += col[(size_t)(d - 2) * a.S];
+      q3 += col[(size_t)(d - 1) * a.S];
+    }
+    float a0 = q0;
+    for (int i = m; i < d; ++i) a0 += col[(size_t)i * a.S];
+    float r = 0.f + a0;
+    r = r + q1;
+    r = r + q2;
+    r = r + q3;
+    out[d - 1] = r;
+  }
+}
+
+// an L1-bypassing load (agent scope): M rows written earlier by other waves of this workgroup
+__device__ __forceinline__ float ld_fresh(const float* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// delta(end e, state s, duration d) from M (oracle DELTA_AT)
+__device__ __forceinline__ float hw_delta(const HwArgs& a, int b, int e, int s, int d) {
+  const int st = e - d + 1;
+  if (st < 0) return -INFINITY;
+  const float o = a.os[(((size_t)b * a.T + st) * a.S + s) * a.Dm + (d - 1)];
+  const float u = a.dur[(size_t)s * a.Dm + (d - 1)];
+  if (st == 0) return o + u;
+  const float m = ld_fresh(a.Mh + ((size_t)b * a.T + st) * a.S + s);
+  return m == -INFINITY ? -INFINITY : (m + o) + u;
+}
+
+// workgroup reductions over kHwNT threads (16 waves): max of a float; min of an int
+__device__ __forceinline__ float wg_max(float v, float* red) {
+  for (int off = 32; off >= 1; off >>= 1) v = fmaxf(v, __shfl_xor(v, off));
+  const int w = threadIdx.x >> 6;
+  __syncthreads();
+  if ((threadIdx.x & 63) == 0) red[w] = v;
+  __syncthreads();
+  float r = red[0];
+  for (int k = 1; k < kHwNT / 64; ++k) r = fmaxf(r, red[k]);
+  return r;
+}
+__device__ __forceinline__ int wg_min(int v, int* red) {
+  for (int off = 32; off >= 1; off >>= 1) v = min(v, __shfl_xor(v, off));
+  const int w = threadIdx.x >> 6;
+  __syncthreads();
+  if ((threadIdx.x & 63) == 0) red[w] = v;
+  __syncthreads();
+  int r = red[0];
+  for (int k = 1; k < kHwNT / 64; ++k) r = min(r, red[k]);
+  return r;
+}
+
+__global__ void __launch_bounds__(kHwNT) hsmm_wide_kernel(HwArgs a) {
+  __shared__ float dmax[kHwSMax];
+  __shared__ float redf[kHwNT / 64];
+  __shared__ int redi[kHwNT / 64];
+  const int b = blockIdx.x, tid = threadIdx.x, w = tid >> 6, l = tid & 63;
+  const int T = a.T, S = a.S, Dm = a.Dm;
+  float* Mrow = a.Mh + (size_t)b * T * S;
+
+  // ------------------------------------------------------------------ forward
+  for (int st = 1; st < T; ++st) {
+    // dmax[s'] = max_d' delta(st-1, s', d'): one wave per s', lanes over d'
+    for (int sp = w; sp < S; sp += kHwNT / 64) {
+      float m = -INFINITY;
+      for (int d0 = 0; d0 < Dm; d0 += 64) {
+        const int dp = d0 + l + 1;
+        if (dp <= Dm) m = fmaxf(m, hw_delta(a, b, st - 1, sp, dp));
+      }
+      for (int off = 32; off >= 1; off >>= 1) m = fmaxf(m, __shfl_xor(m, off));
+      if (l == 0) dmax[sp] = m;
+    }
+    __syncthreads();
+    // M[st][s] (s' ascending; the max is exact in any order)
+    for (int s = tid; s < S; s += kHwNT) {
+      float M = -INFINITY;
+      for (int sp = 0; sp < S; ++sp) {
+        const float dm = dmax[sp];
+        if (sp == s || dm == -INFINITY) continue;
+        M = fmaxf(M, dm + a.logT[(size_t)sp * S + s]);
+      }
+      Mrow[(size_t)st * S + s] = M;
+    }
+    // the M row is read by other waves (ld_fresh, from L2): the stores complete first
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  }
+
+  // ------------------------------------------------------- final argmax (s, d ascending)
+  const int nk = S * Dm;
+  float bv = -INFINITY;
+  for (int k = tid; k < nk; k += kHwNT) bv = fmaxf(bv, hw_delta(a, b, T - 1, k / Dm, k % Dm + 1));
+  const float best = wg_max(bv, redf);
+  int bk = 0x7fffffff;
+  for (int k = tid; k < nk; k += kHwNT)
+    if (hw_delta(a, b, T - 1, k / Dm, k % Dm + 1) == best) bk = min(bk, k);
+  bk = wg_min(bk, redi);
+  if (bk == 0x7fffffff) bk = 0;  // every score -inf: (s, d) = (0, 1) as the reference's init
+  if (tid == 0) a.scores[b] = best;
+
+  // --------------------------------------------------- segment walk (oracle hsmm_backtrack)
+  int64_t* sts = a.states + (size_t)b * T;
+  int t = T - 1, cs = bk / Dm, cd = bk % Dm + 1;
+  for (int guard = 0; guard <= T && t >= 0; ++guard) {
+    int start = t - cd + 1;
+    if (start < 0) start = 0;
+    for (int u = start + tid; u <= t; u += kHwNT) sts[u] = cs;
+    if (start <= 0) break;
+    // the pointer of segment (start, cs, cd): first candidate (s', d') whose total rounds to
+    // the winning value F = fl(fl(M + od) + ud)
+    const float M = ld_fresh(Mrow + (size_t)start * S + cs);
+    int ns = 0, nd = 0;
+    if (M != -INFINITY) {
+      const float* lT = a.logT + cs;
+      int p1 = 0x7fffffff;
+      for (int k = tid; k < nk; k += kHwNT) {
+        const int sp = k / Dm;
+        const float pv = hw_delta(a, b, start - 1, sp, k % Dm + 1);
+        const float x = (sp == cs || pv == -INFINITY) ? -INFINITY : pv + lT[(size_t)sp * S];
+        if (x == M) p1 = min(p1, k);
+      }
+      p1 = wg_min(p1, redi);
+      const float od = a.os[(((size_t)b * T + start) * S + cs) * Dm + (cd - 1)];
+      const float ud = a.dur[(size_t)cs * Dm + (cd - 1)];
+      const float F = (M + od) + ud;
+      // an earlier candidate (k < p1, so x < M) that rounds to the same total F
+      int win = 0x7fffffff;
+      for (int k = tid; k < p1; k += kHwNT) {
+        const int sp = k / Dm;
+        const float pv = hw_delta(a, b, start - 1, sp, k % Dm + 1);
+        const float x = (sp == cs || pv == -INFINITY) ? -INFINITY : pv + lT[(size_t)sp * S];
+        if (x != -INFINITY && (x + od) + ud == F) win = min(win, k);
+      }
+      win = wg_min(win, redi);
+      if (win == 0x7fffffff) win = p1;
+      ns = win / Dm;
+      nd = win % Dm + 1;
+    }
+    if (nd == 0) break;  // (never-written pointer: the reference's walk would not terminate)
+    t = start - 1;
+    cs = ns;
+    cd = nd;
+    __syncthreads();
+  }
+}
+
+size_t hsmm_wide_workspace_bytes(int B, int T, int S, int Dm) {
+  const size_t n = (size_t)B * T * S;
+  return align_up(n * 4, 256) + align_up(n * (size_t)Dm * 4, 256);
+}
+
+bool hsmm_wide_fits(int S, int Dm) { return S >= 1 && S <= kHwSMax && Dm >= 1 && Dm <= kHwDMax; }
+
+hipError_t launch_hsmm_wide(const float* lp, const float* dur, const float* logT, int B, int T, int S, int Dm,
+                            int64_t* states, float* scores, void* workspace, hipStream_t st) {
+  const size_t n = (size_t)B * T * S;
+  char* ws = static_cast<char*>(workspace);
+  HwArgs a{lp, dur, logT, reinterpret_cast<float*>(ws), reinterpret_cast<float*>(ws + align_up(n * 4, 256)),
+           scores, states, B, T, S, Dm};
+  const unsigned blocks = (unsigned)((n + 255) / 256);
+  hipLaunchKernelGGL(hsmm_wide_osum_kernel, dim3(blocks), dim3(256), 0, st, a);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(hsmm_wide_kernel, dim3(B), dim3(kHwNT), 0, st, a);
+  return hipGetLastError();
+}
+
+}  // namespace hmm355

@@ -24,18 +24,15 @@ class HSMMLayer(nn.Module):
     def __init__(self, num_states: int, feature_dim: int, duration_distribution: str = "gamma",
                  max_duration: int = 50, learnable_duration_params: bool = True, min_duration: int = 1):
         super().__init__()
-        # the segment-Viterbi kernel keeps every open segment of a sequence in registers and the
-        # tables in LDS, one workgroup per sequence (csrc/hsmm.hip): S <= 64 with Dmax <= 127, or
-        # S <= 128 with Dmax <= 63.
-        # The reference has no such limit; larger layers are rejected here, at construction,
-        # rather than at the first forward (BASELINE config 5 is S = 64, Dmax = 40).
-        if not 1 <= num_states <= 128:
-            raise ValueError(f"HSMMLayer on gfx950 supports 1 <= num_states <= 128, got {num_states}")
-        if not 1 <= max_duration <= 127:
-            raise ValueError(f"HSMMLayer on gfx950 supports 1 <= max_duration <= 127, got {max_duration}")
-        if num_states > 64 and max_duration > 63:
-            raise ValueError(f"HSMMLayer on gfx950 supports max_duration <= 63 with more than 64 states, got "
-                             f"num_states={num_states}, max_duration={max_duration}")
+        # the segment-Viterbi kernels (csrc/hsmm.hip): S <= 64 with Dmax <= 127, or S <= 128 with
+        # Dmax <= 63, keep every open segment in registers; larger layers, up to S <= 1024 and
+        # Dmax <= 1024, take the general form of csrc/hsmm_wide.hip (M history and segment sums
+        # in HBM).  The reference has no limit; beyond these sizes the layer is rejected here, at
+        # construction, rather than at the first forward (BASELINE config 5 is S = 64, Dmax = 40).
+        if not 1 <= num_states <= 1024:
+            raise ValueError(f"HSMMLayer on gfx950 supports 1 <= num_states <= 1024, got {num_states}")
+        if not 1 <= max_duration <= 1024:
+            raise ValueError(f"HSMMLayer on gfx950 supports 1 <= max_duration <= 1024, got {max_duration}")
         self.num_states = num_states
         self.feature_dim = feature_dim
         self.duration_distribution = duration_distribution

@@ -204,6 +204,31 @@ def test_hsmm_vs_c_oracle(B, T, S, Dm, sub, monkeypatch):
     assert np.array_equal(scores.cpu().numpy(), csc)
 
 
+# the general form (csrc/hsmm_wide.hip): sizes beyond the register-slot geometries, and
+# (HMM355_HSMM_WIDE=1) sizes those also cover, against the C oracle; uniform and coarse
+# tie-heavy tables
+@pytest.mark.parametrize("B,T,S,Dm,force,coarse", [(2, 120, 200, 12, "0", False), (1, 150, 70, 80, "0", False),
+                                                   (2, 90, 8, 150, "0", False), (2, 100, 140, 10, "0", True),
+                                                   (2, 200, 16, 12, "1", False), (1, 300, 64, 40, "1", False),
+                                                   (2, 150, 12, 33, "1", True)])
+def test_hsmm_wide_vs_c_oracle(B, T, S, Dm, force, coarse, monkeypatch):
+    monkeypatch.setenv("HMM355_HSMM_WIDE", force)
+    rng = np.random.default_rng(T + S + Dm)
+    if coarse:
+        lp = np.round(-(rng.random((B, T, S)) * 8 + 4), 1).astype(np.float32)
+        dur = np.round(np.log(rng.random((S, Dm)) + 1e-3), 1).astype(np.float32)
+        logT = np.round(np.log(rng.random((S, S)) + 1e-3), 1).astype(np.float32)
+    else:
+        lp = (-(rng.random((B, T, S), dtype=np.float32) * 40 + 80)).astype(np.float32)
+        dur = np.log(rng.random((S, Dm), dtype=np.float32) + np.float32(1e-8)).astype(np.float32)
+        logT = np.log(rng.random((S, S), dtype=np.float32) + np.float32(1e-8)).astype(np.float32)
+    cs, csc = O.c_hsmm(lp, dur, logT)
+    o = ops()
+    states, scores = o.hsmm_viterbi(t(lp), t(dur), t(logT))
+    assert np.array_equal(states.cpu().numpy(), cs)
+    assert np.array_equal(scores.cpu().numpy(), csc)
+
+
 @pytest.mark.parametrize("case", ["random", "peaked", "ties", "longdur", "s128"])
 def test_hsmm_chunked_backtrace_equals_serial(case, monkeypatch):
     """The chunked backtrace (parallel chunk walks from guessed segments, stitched top-down,

@@ -126,12 +126,12 @@ def test_mixture_full_init_and_cholesky_match_reference():
 
 def test_hsmm_layer_rejects_sizes_beyond_the_kernel():
     with pytest.raises(ValueError):
-        ph.HSMMLayer(129, 4)
+        ph.HSMMLayer(1025, 4)
     with pytest.raises(ValueError):
-        ph.HSMMLayer(8, 4, max_duration=128)
-    with pytest.raises(ValueError):
-        ph.HSMMLayer(65, 4, max_duration=64)
+        ph.HSMMLayer(8, 4, max_duration=1025)
     ph.HSMMLayer(64, 4, max_duration=63)    # BASELINE config 5 is S = 64, Dmax = 40
     ph.HSMMLayer(64, 4, max_duration=127)   # the geometries of csrc/hsmm.hip
     ph.HSMMLayer(128, 4, max_duration=63)
     ph.HSMMLayer(100, 4)                    # the reference's default max_duration = 50
+    ph.HSMMLayer(65, 4, max_duration=64)    # the general form of csrc/hsmm_wide.hip
+    ph.HSMMLayer(300, 4)

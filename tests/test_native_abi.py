@@ -96,13 +96,19 @@ def test_argument_rejection_before_launch(L):
     # HSMM: duration table out of range
     rc = L.hmm355_hsmm_viterbi_f32(fake, fake, fake, 1, 10, 4, 0, fake, fake, fake, 1 << 30, None)
     assert rc == d["HMM355_E_DURATION"]
-    rc = L.hmm355_hsmm_viterbi_f32(fake, fake, fake, 1, 10, 4, 128, fake, fake, fake, 1 << 30, None)
+    rc = L.hmm355_hsmm_viterbi_f32(fake, fake, fake, 1, 10, 4, 1025, fake, fake, fake, 1 << 30, None)
     assert rc == d["HMM355_E_DURATION"]
-    rc = L.hmm355_hsmm_viterbi_f32(fake, fake, fake, 1, 10, 129, 8, fake, fake, fake, 1 << 30, None)
+    rc = L.hmm355_hsmm_viterbi_f32(fake, fake, fake, 1, 10, 1025, 8, fake, fake, fake, 1 << 30, None)
     assert rc == d["HMM355_E_STATES"]
-    rc = L.hmm355_hsmm_viterbi_f32(fake, fake, fake, 1, 10, 65, 64, fake, fake, fake, 1 << 30, None)
-    assert rc == d["HMM355_E_DURATION"]   # S > 64 takes Dmax <= 63
+    # the register-slot geometries and the general form (csrc/hsmm_wide.hip: S * (Dmax + 1)
+    # floats per frame) both report a workspace; beyond S, Dmax <= 1024 nothing does
     assert L.hmm355_hsmm_workspace_bytes(2, 100, 64, 127) > 0 and L.hmm355_hsmm_workspace_bytes(2, 100, 128, 63) > 0
-    assert L.hmm355_hsmm_workspace_bytes(2, 100, 129, 8) == 0 and L.hmm355_hsmm_workspace_bytes(2, 100, 65, 64) == 0
+    assert L.hmm355_hsmm_workspace_bytes(2, 100, 129, 8) >= 2 * 100 * 129 * 9 * 4
+    assert L.hmm355_hsmm_workspace_bytes(2, 100, 65, 64) >= 2 * 100 * 65 * 65 * 4
+    assert L.hmm355_hsmm_workspace_bytes(2, 100, 1025, 8) == 0 and L.hmm355_hsmm_workspace_bytes(2, 100, 8, 1025) == 0
+    # a workspace one byte short of the general form's
+    need = L.hmm355_hsmm_workspace_bytes(1, 10, 200, 8)
+    rc = L.hmm355_hsmm_viterbi_f32(fake, fake, fake, 1, 10, 200, 8, fake, fake, fake, need - 1, None)
+    assert rc == d["HMM355_E_WORKSPACE"]
     # B == 0 is a no-op success
     assert L.hmm355_viterbi_f32(None, 0, None, None, 0, 10, 8, None, None, None, None, 0, None) == 0
