@@ -35,7 +35,7 @@ struct HwArgs {
   const float* dur;   // (S,Dm)
   const float* logT;  // (S,S)
   float* Mh;          // (B,T,S) M[st][s]
-  float* os;          // (B,T,S,Dm) obs_sum(t0, d, s), d = 1..min(Dm, T - t0)
+  float* os;          // (B,T,Dm,S) by END time: os[e][d-1][s] = obs_sum(e-d+1, d, s)
   float* scores;      // (B)
   int64_t* states;    // (B,T)
   int B, T, S, Dm;
@@ -53,7 +53,9 @@ __global__ void __launch_bounds__(256) hsmm_wide_osum_kernel(HwArgs a) {
   const int t0 = (int)(bt % a.T);
   const int b = (int)(bt / a.T);
   const float* col = a.lp + ((size_t)b * a.T + t0) * a.S + s;  // frame t0 + i at col[i * S]
-  float* out = a.os + idx * a.Dm;
+  // written by end time e = t0 + d - 1 (lanes over s: coalesced), where the recursion reads it
+  float* out = a.os + (((size_t)b * a.T + t0) * a.Dm) * a.S + s;
+  const size_t estep = (size_t)(a.Dm + 1) * a.S;  // (e + 1, d + 1) from (e, d)
   const int dlim = a.Dm < a.T - t0 ? a.Dm : a.T - t0;
   float q0 = 0.f, q1 = 0.f, q2 = 0.f, q3 = 0.f;  // sums over the whole quads so far
   for (int d = 1; d <= dlim; ++d) {
@@ -70,7 +72,7 @@ __global__ void __launch_bounds__(256) hsmm_wide_osum_kernel(HwArgs a) {
     r = r + q1;
     r = r + q2;
     r = r + q3;
-    out[d - 1] = r;
+    out[(size_t)(d - 1) * estep] = r;
   }
 }
 
@@ -83,7 +85,7 @@ __device__ __forceinline__ float ld_fresh(const float* p) {
 __device__ __forceinline__ float hw_delta(const HwArgs& a, int b, int e, int s, int d) {
   const int st = e - d + 1;
   if (st < 0) return -INFINITY;
-  const float o = a.os[(((size_t)b * a.T + st) * a.S + s) * a.Dm + (d - 1)];
+  const float o = a.os[(((size_t)b * a.T + e) * a.Dm + (d - 1)) * a.S + s];
   const float u = a.dur[(size_t)s * a.Dm + (d - 1)];
   if (st == 0) return o + u;
   const float m = ld_fresh(a.Mh + ((size_t)b * a.T + st) * a.S + s);
@@ -114,6 +116,8 @@ __device__ __forceinline__ int wg_min(int v, int* red) {
 
 __global__ void __launch_bounds__(kHwNT) hsmm_wide_kernel(HwArgs a) {
   __shared__ float dmax[kHwSMax];
+  __shared__ float mpart[kHwNT];
+  extern __shared__ float dpart[];  // [16][kHwSMax] per-wave partial maxima (dynamic: 64 KiB)
   __shared__ float redf[kHwNT / 64];
   __shared__ int redi[kHwNT / 64];
   const int b = blockIdx.x, tid = threadIdx.x, w = tid >> 6, l = tid & 63;
@@ -122,25 +126,42 @@ __global__ void __launch_bounds__(kHwNT) hsmm_wide_kernel(HwArgs a) {
 
   // ------------------------------------------------------------------ forward
   for (int st = 1; st < T; ++st) {
-    // dmax[s'] = max_d' delta(st-1, s', d'): one wave per s', lanes over d'
-    for (int sp = w; sp < S; sp += kHwNT / 64) {
+    // dmax[s'] = max_d' delta(st-1, s', d'): lanes over s' (coalesced rows of os and M), wave w
+    // over d' = w+1, w+17, ...; the 16 waves' partial maxima combined through LDS
+    for (int sp0 = 0; sp0 < S; sp0 += 64) {
+      const int sp = sp0 + l;
       float m = -INFINITY;
-      for (int d0 = 0; d0 < Dm; d0 += 64) {
-        const int dp = d0 + l + 1;
-        if (dp <= Dm) m = fmaxf(m, hw_delta(a, b, st - 1, sp, dp));
+      if (sp < S) {
+#pragma unroll 4
+        for (int dp = w + 1; dp <= Dm; dp += kHwNT / 64) m = fmaxf(m, hw_delta(a, b, st - 1, sp, dp));
+        dpart[w * kHwSMax + sp] = m;
       }
-      for (int off = 32; off >= 1; off >>= 1) m = fmaxf(m, __shfl_xor(m, off));
-      if (l == 0) dmax[sp] = m;
     }
     __syncthreads();
-    // M[st][s] (s' ascending; the max is exact in any order)
-    for (int s = tid; s < S; s += kHwNT) {
+    for (int sp = tid; sp < S; sp += kHwNT) {
+      float m = dpart[sp];
+      for (int k = 1; k < kHwNT / 64; ++k) m = fmaxf(m, dpart[k * kHwSMax + sp]);
+      dmax[sp] = m;
+    }
+    __syncthreads();
+    // M[st][s] = max_{s' != s} fl(dmax[s'] + logT[s'][s]) (exact in any order): P = 1024 / S
+    // threads per state, each over every P-th s', then the P partial maxima
+    const int P = kHwNT / S;
+    if (tid < P * S) {
+      const int s = tid % S, part = tid / S;
       float M = -INFINITY;
-      for (int sp = 0; sp < S; ++sp) {
+#pragma unroll 4
+      for (int sp = part; sp < S; sp += P) {
         const float dm = dmax[sp];
-        if (sp == s || dm == -INFINITY) continue;
-        M = fmaxf(M, dm + a.logT[(size_t)sp * S + s]);
+        const float v = dm + a.logT[(size_t)sp * S + s];
+        M = (sp == s || dm == -INFINITY) ? M : fmaxf(M, v);
       }
+      mpart[tid] = M;
+    }
+    __syncthreads();
+    for (int s = tid; s < S; s += kHwNT) {
+      float M = mpart[s];
+      for (int part = 1; part < P; ++part) M = fmaxf(M, mpart[part * S + s]);
       Mrow[(size_t)st * S + s] = M;
     }
     // the M row is read by other waves (ld_fresh, from L2): the stores complete first
@@ -149,13 +170,15 @@ __global__ void __launch_bounds__(kHwNT) hsmm_wide_kernel(HwArgs a) {
   }
 
   // ------------------------------------------------------- final argmax (s, d ascending)
+  // candidates enumerated as j = (d-1) * S + s (s fastest: coalesced rows of os and M); the
+  // reference's order is k = s * Dm + d - 1 (s ascending, then d), kept for the first index
   const int nk = S * Dm;
   float bv = -INFINITY;
-  for (int k = tid; k < nk; k += kHwNT) bv = fmaxf(bv, hw_delta(a, b, T - 1, k / Dm, k % Dm + 1));
+  for (int j = tid; j < nk; j += kHwNT) bv = fmaxf(bv, hw_delta(a, b, T - 1, j % S, j / S + 1));
   const float best = wg_max(bv, redf);
   int bk = 0x7fffffff;
-  for (int k = tid; k < nk; k += kHwNT)
-    if (hw_delta(a, b, T - 1, k / Dm, k % Dm + 1) == best) bk = min(bk, k);
+  for (int j = tid; j < nk; j += kHwNT)
+    if (hw_delta(a, b, T - 1, j % S, j / S + 1) == best) bk = min(bk, (j % S) * Dm + j / S);
   bk = wg_min(bk, redi);
   if (bk == 0x7fffffff) bk = 0;  // every score -inf: (s, d) = (0, 1) as the reference's init
   if (tid == 0) a.scores[b] = best;
@@ -175,21 +198,22 @@ __global__ void __launch_bounds__(kHwNT) hsmm_wide_kernel(HwArgs a) {
     if (M != -INFINITY) {
       const float* lT = a.logT + cs;
       int p1 = 0x7fffffff;
-      for (int k = tid; k < nk; k += kHwNT) {
-        const int sp = k / Dm;
-        const float pv = hw_delta(a, b, start - 1, sp, k % Dm + 1);
+      for (int j = tid; j < nk; j += kHwNT) {
+        const int sp = j % S, dp = j / S + 1;
+        const float pv = hw_delta(a, b, start - 1, sp, dp);
         const float x = (sp == cs || pv == -INFINITY) ? -INFINITY : pv + lT[(size_t)sp * S];
-        if (x == M) p1 = min(p1, k);
+        if (x == M) p1 = min(p1, sp * Dm + dp - 1);
       }
       p1 = wg_min(p1, redi);
-      const float od = a.os[(((size_t)b * T + start) * S + cs) * Dm + (cd - 1)];
+      const float od = a.os[(((size_t)b * T + (start + cd - 1)) * Dm + (cd - 1)) * S + cs];
       const float ud = a.dur[(size_t)cs * Dm + (cd - 1)];
       const float F = (M + od) + ud;
       // an earlier candidate (k < p1, so x < M) that rounds to the same total F
       int win = 0x7fffffff;
-      for (int k = tid; k < p1; k += kHwNT) {
-        const int sp = k / Dm;
-        const float pv = hw_delta(a, b, start - 1, sp, k % Dm + 1);
+      for (int j = tid; j < nk; j += kHwNT) {
+        const int sp = j % S, dp = j / S + 1, k = sp * Dm + dp - 1;
+        if (k >= p1) continue;
+        const float pv = hw_delta(a, b, start - 1, sp, dp);
         const float x = (sp == cs || pv == -INFINITY) ? -INFINITY : pv + lT[(size_t)sp * S];
         if (x != -INFINITY && (x + od) + ud == F) win = min(win, k);
       }
@@ -223,7 +247,10 @@ hipError_t launch_hsmm_wide(const float* lp, const float* dur, const float* logT
   hipLaunchKernelGGL(hsmm_wide_osum_kernel, dim3(blocks), dim3(256), 0, st, a);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
-  hipLaunchKernelGGL(hsmm_wide_kernel, dim3(B), dim3(kHwNT), 0, st, a);
+  const size_t lds = sizeof(float) * (kHwNT / 64) * kHwSMax;
+  e = allow_lds(hsmm_wide_kernel, lds);
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(hsmm_wide_kernel, dim3(B), dim3(kHwNT), lds, st, a);
   return hipGetLastError();
 }
 
