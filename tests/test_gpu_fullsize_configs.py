@@ -119,6 +119,25 @@ def test_config5_hsmm_fullsize_vs_c_oracle():
         assert len(seg) > 20 and seg.max() <= Dm
 
 
+@torch.no_grad()
+def test_hsmm_layer_beyond_register_kernels_vs_c_oracle():
+    """An HSMMLayer the register-slot kernels cannot hold (150 states with the reference's
+    default max_duration = 50) runs end to end on the general form (csrc/hsmm_wide.hip)."""
+    import pytorch_hmm_amd as ph
+    B, T, S, D, Dm = 2, 400, 150, 16, 50
+    torch.manual_seed(1)
+    layer = ph.HSMMLayer(S, D).to(DEV)
+    assert layer.max_duration == Dm
+    x = torch.from_numpy(O.uniform_obs(7, (B, T, D), -2.0, 2.0)).to(DEV)
+    states, scores = layer(x)
+    lp = layer.get_observation_log_probs(x).cpu().numpy()
+    dur = torch.log(layer.get_duration_probabilities() + layer.eps)[:, :Dm].cpu().numpy()
+    lT = torch.log(layer.get_transition_matrix() + layer.eps).cpu().numpy()
+    cs, csc = O.c_hsmm(lp, dur, lT)
+    assert np.array_equal(states.cpu().numpy(), cs)
+    assert np.array_equal(scores.cpu().numpy().view(np.int32), csc.view(np.int32))
+
+
 # ------------------------------------------------------------- large-batch pair kernel
 @torch.no_grad()
 def test_pair_kernel_b256_fullsize(monkeypatch):
