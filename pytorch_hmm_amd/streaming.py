@@ -81,9 +81,17 @@ class StreamingHMMProcessor(nn.Module):
 
     def _log_transitions(self):
         """log(softmax + 1e-8) (streaming.py:289-290), formed on a CPU copy — the reference's
-        path is torch-CPU — so the kernels see its bits."""
-        lt = torch.log(F.softmax(self.transition_logits.detach().cpu(), dim=-1) + 1e-8)
-        return lt.to(self.transition_logits.device)
+        path is torch-CPU — so the kernels see its bits.  Cached on the parameter's identity,
+        storage and version: a chunk makes no device -> host -> device round trip (and no host
+        sync) unless the transition logits changed since the last chunk."""
+        p = self.transition_logits
+        key = (p.data_ptr(), p._version, str(p.device))
+        c = getattr(self, "_log_t_cache", None)
+        if c is None or c[0] != key or c[1] is not p:
+            lt = torch.log(F.softmax(p.detach().cpu(), dim=-1) + 1e-8).to(p.device)
+            self._log_t_cache = (key, p, lt)
+            c = self._log_t_cache
+        return c[2]
 
     # -- async helpers (streaming.py:123-181) -----------------------------------------------
     # Same public calls and drop semantics as the reference (a full input queue refuses the

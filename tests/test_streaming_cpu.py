@@ -113,3 +113,22 @@ def test_async_worker_queue_semantics():
     p.stop_async_processing()
     assert _t.time() - t0 < 2 and p.processing_thread is None and not p.is_processing
     assert p.get_result_async() is None
+
+
+def test_log_transition_table_cached_per_parameter_version():
+    """The per-chunk log(softmax + 1e-8) table is built once per parameter version (no host
+    round trip per chunk), and rebuilt when the logits change in place or are replaced."""
+    from pytorch_hmm_amd.streaming import StreamingHMMProcessor
+    torch.manual_seed(0)
+    p = StreamingHMMProcessor(6, 4, chunk_size=16, overlap_size=4)
+    a = p._log_transitions()
+    assert p._log_transitions() is a
+    ref = torch.log(torch.softmax(p.transition_logits.detach(), -1) + 1e-8)
+    assert torch.equal(a, ref)
+    with torch.no_grad():
+        p.transition_logits.add_(0.5 * torch.randn_like(p.transition_logits))
+    b = p._log_transitions()
+    assert b is not a and torch.equal(b, torch.log(torch.softmax(p.transition_logits.detach(), -1) + 1e-8))
+    p.transition_logits = torch.nn.Parameter(torch.zeros(6, 6))
+    c = p._log_transitions()
+    assert c is not b and torch.allclose(c, torch.full((6, 6), float(np.log(1 / 6 + 1e-8))))
