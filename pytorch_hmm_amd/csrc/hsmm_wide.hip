@@ -197,28 +197,21 @@ __global__ void __launch_bounds__(kHwNT) hsmm_wide_kernel(HwArgs a) {
     int ns = 0, nd = 0;
     if (M != -INFINITY) {
       const float* lT = a.logT + cs;
-      int p1 = 0x7fffffff;
+      // the reference's total of candidate k is g(x_k) = fl(fl(x_k + od) + ud), monotone in x_k,
+      // and the winner's is F = g(M): the pointer is the first k with g(x_k) == F (the first
+      // candidate attaining M, or an earlier one that rounds to the same total), one pass
+      const float od = a.os[(((size_t)b * T + (start + cd - 1)) * Dm + (cd - 1)) * S + cs];
+      const float ud = a.dur[(size_t)cs * Dm + (cd - 1)];
+      const float F = (M + od) + ud;
+      int win = 0x7fffffff;
       for (int j = tid; j < nk; j += kHwNT) {
         const int sp = j % S, dp = j / S + 1;
         const float pv = hw_delta(a, b, start - 1, sp, dp);
         const float x = (sp == cs || pv == -INFINITY) ? -INFINITY : pv + lT[(size_t)sp * S];
-        if (x == M) p1 = min(p1, sp * Dm + dp - 1);
-      }
-      p1 = wg_min(p1, redi);
-      const float od = a.os[(((size_t)b * T + (start + cd - 1)) * Dm + (cd - 1)) * S + cs];
-      const float ud = a.dur[(size_t)cs * Dm + (cd - 1)];
-      const float F = (M + od) + ud;
-      // an earlier candidate (k < p1, so x < M) that rounds to the same total F
-      int win = 0x7fffffff;
-      for (int j = tid; j < nk; j += kHwNT) {
-        const int sp = j % S, dp = j / S + 1, k = sp * Dm + dp - 1;
-        if (k >= p1) continue;
-        const float pv = hw_delta(a, b, start - 1, sp, dp);
-        const float x = (sp == cs || pv == -INFINITY) ? -INFINITY : pv + lT[(size_t)sp * S];
-        if (x != -INFINITY && (x + od) + ud == F) win = min(win, k);
+        if (x != -INFINITY && (x + od) + ud == F) win = min(win, sp * Dm + dp - 1);
       }
       win = wg_min(win, redi);
-      if (win == 0x7fffffff) win = p1;
+      if (win == 0x7fffffff) win = 0;  // (unreachable: the candidate attaining M qualifies)
       ns = win / Dm;
       nd = win % Dm + 1;
     }
