@@ -39,6 +39,7 @@ struct HwArgs {
   float* scores;      // (B)
   int64_t* states;    // (B,T)
   int B, T, S, Dm;
+  int tlds;           // 1: logT staged in LDS (behind the partial maxima) when it fits
 };
 
 // obs_sum(t0, d, s) for d = 1..Dm in torch-CPU's order (oracle tsum): four strided partial
@@ -117,12 +118,20 @@ __device__ __forceinline__ int wg_min(int v, int* red) {
 __global__ void __launch_bounds__(kHwNT) hsmm_wide_kernel(HwArgs a) {
   __shared__ float dmax[kHwSMax];
   __shared__ float mpart[kHwNT];
-  extern __shared__ float dpart[];  // [16][kHwSMax] per-wave partial maxima (dynamic: 64 KiB)
+  extern __shared__ float dpart[];  // [16][S] per-wave partial maxima, then logT (a.tlds)
   __shared__ float redf[kHwNT / 64];
   __shared__ int redi[kHwNT / 64];
   const int b = blockIdx.x, tid = threadIdx.x, w = tid >> 6, l = tid & 63;
   const int T = a.T, S = a.S, Dm = a.Dm;
   float* Mrow = a.Mh + (size_t)b * T * S;
+  // logT is read S * S times per start time: from LDS where it fits beside the partial maxima
+  const float* lTs = a.logT;
+  if (a.tlds) {
+    float* t = dpart + (kHwNT / 64) * S;
+    for (int k = tid; k < S * S; k += kHwNT) t[k] = a.logT[k];
+    __syncthreads();
+    lTs = t;
+  }
 
   // ------------------------------------------------------------------ forward
   for (int st = 1; st < T; ++st) {
@@ -134,13 +143,13 @@ __global__ void __launch_bounds__(kHwNT) hsmm_wide_kernel(HwArgs a) {
       if (sp < S) {
 #pragma unroll 4
         for (int dp = w + 1; dp <= Dm; dp += kHwNT / 64) m = fmaxf(m, hw_delta(a, b, st - 1, sp, dp));
-        dpart[w * kHwSMax + sp] = m;
+        dpart[w * S + sp] = m;
       }
     }
     __syncthreads();
     for (int sp = tid; sp < S; sp += kHwNT) {
       float m = dpart[sp];
-      for (int k = 1; k < kHwNT / 64; ++k) m = fmaxf(m, dpart[k * kHwSMax + sp]);
+      for (int k = 1; k < kHwNT / 64; ++k) m = fmaxf(m, dpart[k * S + sp]);
       dmax[sp] = m;
     }
     __syncthreads();
@@ -153,7 +162,7 @@ __global__ void __launch_bounds__(kHwNT) hsmm_wide_kernel(HwArgs a) {
 #pragma unroll 4
       for (int sp = part; sp < S; sp += P) {
         const float dm = dmax[sp];
-        const float v = dm + a.logT[(size_t)sp * S + s];
+        const float v = dm + lTs[(size_t)sp * S + s];
         M = (sp == s || dm == -INFINITY) ? M : fmaxf(M, v);
       }
       mpart[tid] = M;
@@ -196,7 +205,7 @@ __global__ void __launch_bounds__(kHwNT) hsmm_wide_kernel(HwArgs a) {
     const float M = ld_fresh(Mrow + (size_t)start * S + cs);
     int ns = 0, nd = 0;
     if (M != -INFINITY) {
-      const float* lT = a.logT + cs;
+      const float* lT = lTs + cs;
       // the reference's total of candidate k is g(x_k) = fl(fl(x_k + od) + ud), monotone in x_k,
       // and the winner's is F = g(M): the pointer is the first k with g(x_k) == F (the first
       // candidate attaining M, or an earlier one that rounds to the same total), one pass
@@ -234,13 +243,15 @@ hipError_t launch_hsmm_wide(const float* lp, const float* dur, const float* logT
                             int64_t* states, float* scores, void* workspace, hipStream_t st) {
   const size_t n = (size_t)B * T * S;
   char* ws = static_cast<char*>(workspace);
+  const size_t part = sizeof(float) * (kHwNT / 64) * S, tab = sizeof(float) * (size_t)S * S;
+  const int tlds = part + tab + 16384 <= 163840 ? 1 : 0;  // (static LDS: dmax, mpart, reductions)
   HwArgs a{lp, dur, logT, reinterpret_cast<float*>(ws), reinterpret_cast<float*>(ws + align_up(n * 4, 256)),
-           scores, states, B, T, S, Dm};
+           scores, states, B, T, S, Dm, tlds};
   const unsigned blocks = (unsigned)((n + 255) / 256);
   hipLaunchKernelGGL(hsmm_wide_osum_kernel, dim3(blocks), dim3(256), 0, st, a);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
-  const size_t lds = sizeof(float) * (kHwNT / 64) * kHwSMax;
+  const size_t lds = part + (tlds ? tab : 0);
   e = allow_lds(hsmm_wide_kernel, lds);
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL(hsmm_wide_kernel, dim3(B), dim3(kHwNT), lds, st, a);
