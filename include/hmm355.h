@@ -184,7 +184,11 @@ int hmm355_gmm_diag_logprob_f32(const float* x, const float* means, const float*
  *   lp (B,T,S) obs log-probs; dur_lp (S,Dmax) = log(p_dur + 1e-8); log_T (S,S)
  *   states (B,T) int64; scores (B) fp32
  *   1 <= S <= 1024 (HMM355_E_STATES beyond), 1 <= Dmax <= 1024 (HMM355_E_DURATION beyond).
- *   S <= 64 with Dmax <= 127, or S <= 128 with Dmax <= 63: one workgroup per sequence keeps
+ *   obs_sum follows ATen's cascade_sum order (csrc/tsum.h; it changes from 72 frames on).
+ *   S = 1: the slice is contiguous and takes torch's vectorised order; the path is all 0.
+ *   Frames the walk never reaches (no predecessor path: every score -inf) are written 0,
+ *   the reference's torch.zeros initial value.
+ *   S <= 64 with Dmax <= 71, or S <= 128 with Dmax <= 63: one workgroup per sequence keeps
  *   every open segment in registers and the tables in LDS (csrc/hsmm.hip); larger sizes take
  *   the general form (csrc/hsmm_wide.hip: M history and segment sums in the workspace,
  *   B*T*S*(Dmax+1) floats).

@@ -11,9 +11,8 @@
  *   fb_f64              hmm.py:89-130 in float64 (tolerance reference, not bit-exact).
  *   gmm_diag_f64        mixture_gaussian.py:157-214 in float64 (tolerance reference).
  *   hsmm_viterbi_literal hsmm.py:245-354, the literal 5-deep loop, incl. torch's CPU order
- *                       for sum(obs_log_probs[t:t+d, s]) (strided slice: 4 accumulators over
- *                       whole groups of 4, tail folded into acc0, then ((a0+a1)+a2)+a3 —
- *                       measured 31200/31200 matches against torch 2.10 CPU).
+ *                       for sum(obs_log_probs[t:t+d, s]): ATen's cascade_sum restated
+ *                       (torch_sum_f32 below; equal to torch.sum for every d = 1..1024).
  *   tv_viterbi_f32      neural.py:463-511 — Viterbi with one transition matrix per step
  *                       (log_A (B,T,N,N); step t uses matrix t-1), exact as viterbi_f32.
  *   tv_fb_f64           neural.py:391-461 in float64 (forward step t uses matrix t-1,
@@ -25,6 +24,7 @@
 #include <math.h>
 #include <stdint.h>
 #include <stdlib.h>
+#include <stddef.h>
 #include <string.h>
 
 /* ---------------------------------------------------------------- Viterbi (exact) */
@@ -202,22 +202,73 @@ void gmm_diag_f64(const float* x, const float* means, const float* log_vars, con
 }
 
 /* ----------------------------------------------------------------- HSMM (exact) */
-/* torch 2.10 CPU order for torch.sum over a strided 1-D slice of length d. */
-static float tsum(const float* lp, int S, int t0, int d, int s) {
-    float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
-    int m = d & ~3, i = 0;
-    for (; i < m; i += 4) {
-        a0 += lp[(size_t)(t0 + i) * S + s];
-        a1 += lp[(size_t)(t0 + i + 1) * S + s];
-        a2 += lp[(size_t)(t0 + i + 2) * S + s];
-        a3 += lp[(size_t)(t0 + i + 3) * S + s];
-    }
-    for (; i < d; ++i) a0 += lp[(size_t)(t0 + i) * S + s];
-    float r = 0.f + a0;
-    r = r + a1;
-    r = r + a2;
-    r = r + a3;
+/* torch 2.10 CPU order for torch.sum over a 1-D fp32 slice (the reference's
+ * torch.sum(obs_log_probs[t:t+d, s]), hsmm.py:273,285).  ATen's cascade_sum
+ * (aten/src/ATen/native/cpu/SumKernel.cpp, accumulating in fp32), restated:
+ *   multi_row_sum: `lanes` independent accumulators over `nrow` rows, with 4 cascade levels:
+ *     after every 2^lp rows level 0 is added into level 1 and cleared, level j into j+1
+ *     while the row count is a multiple of 2^(j*lp) (lp = max(4, ceil_log2(nrow) / 4)),
+ *     and at the end acc0 = ((acc0 + acc1) + acc2) + acc3;
+ *   strided slice (stride != 1): row_sum = multi_row_sum over rows of 4 (lanes 0..3), the
+ *     d mod 4 tail into lane 0, then ((l0 + l1) + l2) + l3;
+ *   contiguous slice (stride 1, d >= 8: the 8-wide Vectorized<float> of the kernel torch
+ *     dispatches on both AVX2 and AVX512 hosts): row_sum over 8-wide vectors (lanes 0..31 =
+ *     4 vectors), tail vectors into vector 0, vectors summed lane-wise, then
+ *     r = 0, the d mod 8 tail scalars, then the 8 lanes in order.
+ * Checked against torch.sum for d = 1..1024 (and longer) at strides 1, 5, 64, 150
+ * (tests/test_oracle.py::test_tsum_matches_torch_sum). */
+static int ceil_log2_i64(int64_t x) {
+    if (x <= 2) return 1;
+    int r = 0;
+    for (uint64_t v = (uint64_t)(x - 1); v; v >>= 1) ++r;
     return r;
+}
+static void multi_row_sum(const float* x, ptrdiff_t stride, int64_t nrow, int lanes, float* out) {
+    float acc[4][32];
+    memset(acc, 0, sizeof(acc));
+    int lp = ceil_log2_i64(nrow) / 4;
+    if (lp < 4) lp = 4;
+    const int64_t step = (int64_t)1 << lp, mask = step - 1;
+    int64_t i = 0;
+    while (i + step <= nrow) {
+        for (int64_t j = 0; j < step; ++j, ++i)
+            for (int k = 0; k < lanes; ++k) acc[0][k] += x[(i * lanes + k) * stride];
+        for (int j = 1; j < 4; ++j) {
+            for (int k = 0; k < lanes; ++k) {
+                acc[j][k] += acc[j - 1][k];
+                acc[j - 1][k] = 0.f;
+            }
+            if (i & (mask << (j * lp))) break;
+        }
+    }
+    for (; i < nrow; ++i)
+        for (int k = 0; k < lanes; ++k) acc[0][k] += x[(i * lanes + k) * stride];
+    for (int j = 1; j < 4; ++j)
+        for (int k = 0; k < lanes; ++k) acc[0][k] += acc[j][k];
+    for (int k = 0; k < lanes; ++k) out[k] = acc[0][k];
+}
+float torch_sum_f32(const float* x, ptrdiff_t stride, int64_t n) {
+    if (stride != 1 || n < 8) {
+        float ps[4];
+        const int64_t nr = n / 4;
+        multi_row_sum(x, stride, nr, 4, ps);
+        for (int64_t i = nr * 4; i < n; ++i) ps[0] += x[i * stride];
+        return ((ps[0] + ps[1]) + ps[2]) + ps[3];
+    }
+    const int64_t nv = n / 8, nr = nv / 4;
+    float ps[32];
+    multi_row_sum(x, 1, nr, 32, ps);
+    for (int64_t v = nr * 4; v < nv; ++v)
+        for (int j = 0; j < 8; ++j) ps[j] += x[v * 8 + j];
+    for (int k = 1; k < 4; ++k)
+        for (int j = 0; j < 8; ++j) ps[j] += ps[k * 8 + j];
+    float r = 0.f;
+    for (int64_t i = nv * 8; i < n; ++i) r += x[i];
+    for (int j = 0; j < 8; ++j) r += ps[j];
+    return r;
+}
+static float tsum(const float* lp, int S, int t0, int d, int s) {
+    return torch_sum_f32(lp + (size_t)t0 * S + s, S, d);
 }
 
 static void hsmm_backtrack(int T, int S, int Dm, const int16_t* psi_s, const int16_t* psi_d,

@@ -299,6 +299,8 @@ def c_oracle():
     lib.tv_fb_f64.argtypes = [P, P, L, L, P, I, I, I, P, P, P, P]
     lib.hsmm_viterbi_literal.argtypes = [P, P, P, I, I, I, P, P]
     lib.hsmm_viterbi_fast.argtypes = [P, P, P, I, I, I, P, P]
+    lib.torch_sum_f32.argtypes = [P, ctypes.c_ssize_t, ctypes.c_longlong]
+    lib.torch_sum_f32.restype = ctypes.c_float
     lib.smk_quad_f32.argtypes = [P, P, P, I, I, I, P]
     lib.smk_viterbi_literal.argtypes = [P, P, P, P, P, I, I, I, P, P, P]
     lib.smk_viterbi_literal.restype = I
@@ -377,8 +379,9 @@ def c_gmm64(x, means, log_vars, log_w):
     return out
 
 
-def c_hsmm(lp, dur_lp, log_T, literal=False):
-    """lp (B,T,S); returns states (B,T) int64 and scores (B,) float32."""
+def c_hsmm(lp, dur_lp, log_T, literal=False, workers=1):
+    """lp (B,T,S); returns states (B,T) int64 and scores (B,) float32.  `workers` > 1 runs the
+    sequences on that many threads (ctypes releases the GIL)."""
     lp = _f32(lp)
     B, T, S = lp.shape
     Dm = dur_lp.shape[1]
@@ -386,13 +389,31 @@ def c_hsmm(lp, dur_lp, log_T, literal=False):
     states = np.zeros((B, T), np.int64)
     scores = np.zeros(B, np.float32)
     fn = c_oracle().hsmm_viterbi_literal if literal else c_oracle().hsmm_viterbi_fast
-    for b in range(B):
+
+    def one(b):
         lpb = np.ascontiguousarray(lp[b])
         sb = np.zeros(T, np.int64)
         sc = np.zeros(1, np.float32)
         fn(_p(lpb), _p(du), _p(lT), T, S, Dm, _p(sb), _p(sc))
         states[b], scores[b] = sb, sc[0]
+
+    if workers > 1 and B > 1:
+        from concurrent.futures import ThreadPoolExecutor
+        with ThreadPoolExecutor(max_workers=min(workers, B)) as ex:
+            list(ex.map(one, range(B)))
+    else:
+        for b in range(B):
+            one(b)
     return states, scores
+
+
+def c_torch_sum(col):
+    """torch.sum of a 1-D float32 view (any stride), in torch-CPU's cascade order
+    (oracle/hmm_oracle.c torch_sum_f32; reference hsmm.py:273,285)."""
+    a = np.asarray(col)
+    assert a.dtype == np.float32 and a.ndim == 1
+    stride = a.strides[0] // 4 if a.size > 1 else 1
+    return np.float32(c_oracle().torch_sum_f32(a.ctypes.data_as(ctypes.c_void_p), stride, a.size))
 
 
 def c_smk_quad(x, means, var):

@@ -42,18 +42,33 @@ def build(force=False, verbose=False, defines=(), out=None):
         if all(os.path.getmtime(d) <= lt for d in deps if os.path.exists(d)):
             return LIB
     hipcc = _hipcc()
-    tag = os.path.splitext(os.path.basename(lib))[0]
+    # objects are reused only under the same flags, defines and target (a hash in the dir name)
+    import hashlib
+    fh = hashlib.sha256("\0".join([*FLAGS, *defines, ARCH]).encode()).hexdigest()[:12]
+    tag = os.path.splitext(os.path.basename(lib))[0] + "-" + fh
     objdir = os.path.join(os.path.dirname(lib), "obj", tag)
     os.makedirs(objdir, exist_ok=True)
 
-    headers = [d for d in deps if not d.endswith(".hip")]
-    hdr_time = max(os.path.getmtime(d) for d in headers if os.path.exists(d))
+    def includes(path, seen):
+        """the quoted #includes of `path`, transitively (csrc headers and the public header)"""
+        with open(path) as f:
+            for line in f:
+                t = line.strip()
+                if t.startswith("#include \""):
+                    inc = os.path.normpath(os.path.join(os.path.dirname(path), t.split('"')[1]))
+                    if inc not in seen and os.path.exists(inc):
+                        seen.add(inc)
+                        includes(inc, seen)
+        return seen
+
+    this = os.path.abspath(__file__)
 
     def compile_one(s):
         obj = os.path.join(objdir, s.replace(".hip", ".o"))
         src = os.path.join(CSRC, s)
-        # an object newer than its source and every header is reused (per-object staleness)
-        if not force and os.path.exists(obj) and os.path.getmtime(obj) >= max(os.path.getmtime(src), hdr_time):
+        # an object newer than its source, the headers it includes and this script is reused
+        newest = max(os.path.getmtime(d) for d in includes(src, {src, this}))
+        if not force and os.path.exists(obj) and os.path.getmtime(obj) >= newest:
             return obj
         cmd = [hipcc, *FLAGS, *["-D" + d for d in defines], "-c", src, "-o", obj]
         if verbose:

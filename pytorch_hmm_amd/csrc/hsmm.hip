@@ -15,8 +15,9 @@
 //   final value — so the forward stores only M and Dm, and the backtrace finds p1 and
 //   xb = max over the candidates before p1 for the segments on the decoded path and
 //   re-resolves exactly there (rare).
-//   obs_sum is torch-CPU's order for a strided slice of length d: four accumulators over
-//   whole groups of 4, the tail folded into the first, then ((a0+a1)+a2)+a3.
+//   obs_sum is torch-CPU's order for a strided slice of length d (tsum.h): four accumulators
+//   over whole groups of 4 with ATen's cascade step every 16 groups, the tail folded into the
+//   first, then ((a0+a1)+a2)+a3.
 //
 // hsmm_fwd_kernel<SUB, NJ, SMAX>: one workgroup per sequence (SMAX * SUB threads), the segment
 //   END time t as the loop index (semimarkov.hip's layout): SUB lanes (a DPP group) per state;
@@ -31,7 +32,8 @@
 //   durations beyond Dmax or padding states read -inf from the duration table.  Per end time t
 //   the kernel stores M[t][s] (the best fl(delta + logT) over predecessors ending at t, for
 //   segments starting at t+1) and Dm[t][s].  Geometries: (4, 16, 64) for the config-5 class
-//   (S <= 64, Dmax <= 63), (8, 8, 64) / (16, 4, 64) the same with 8- and 16-lane groups, (8, 16, 64) for Dmax <= 127 and (4, 16, 128) for 65 <= S <= 128 with
+//   (S <= 64, Dmax <= 63), (8, 8, 64) / (16, 4, 64) the same with 8- and 16-lane groups, (8, 16, 64) for Dmax <= 71 (longer segments take torch's
+//   cascade order: hsmm_wide.hip) and (4, 16, 128) for 65 <= S <= 128 with
 //   Dmax <= 63.
 // hsmm_backtrace_kernel / hsmm_chunk_walk_kernel + hsmm_stitch_kernel: the walk over the
 //   segments (hsmm.py:331-352).  For each segment it finds the first predecessor state
@@ -48,12 +50,13 @@
 #include <type_traits>
 
 #include "common.h"
+#include "tsum.h"
 
 namespace hmm355 {
 
 constexpr int kHsL = 128;    // lp row ring (two 64-row chunks)
 constexpr int kHsSMax = 128; // states (the largest geometry below)
-constexpr int kHsDMax = 127; // durations (slot ring R = 128)
+constexpr int kHsRegDMax = 71;  // the longest duration the register-slot kernels take (tsum.h)
 
 typedef float hs_f2 __attribute__((ext_vector_type(2)));
 
@@ -197,6 +200,9 @@ __global__ void __launch_bounds__((HsG<SUB, NJ, SMAX>::NT)) hsmm_fwd_kernel(HsAr
   // xr[t & 3]) when the group closes: G_i += x_{t-3+i} (the same fp32 adds as accumulating
   // each element into its own accumulator as it arrives).  (The leading 0 + a0 of torch's
   // sum is an identity here: a0 is never -0, every accumulator starting from +0.)
+  // Durations stay below 72 (hsmm_cfg), so torch's cascade step (tsum.h), which first changes
+  // the order at 72 frames, never applies here: a 64..71-frame sum is fl(R + A) with R the last
+  // row or two, the same value as A + R.
   hs_f2 Gs[NP2][4], A0[NP2], mp[NP2];
 #pragma unroll
   for (int p = 0; p < NP2; ++p) {
@@ -428,21 +434,7 @@ __global__ void __launch_bounds__((HsG<SUB, NJ, SMAX>::NT)) hsmm_fwd_kernel(HsAr
 // torch-order sum of the d elements col[d-1-e], e = 0..d-1 (a segment's column in time
 // order, staged newest-first in LDS)
 __device__ __forceinline__ float hs_obs_sum_lds(const float* col, int d) {
-  float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
-  const int m = d & ~3;
-  int i = 0;
-  for (; i < m; i += 4) {
-    a0 += col[d - 1 - i];
-    a1 += col[d - 2 - i];
-    a2 += col[d - 3 - i];
-    a3 += col[d - 4 - i];
-  }
-  for (; i < d; ++i) a0 += col[d - 1 - i];
-  float r = 0.f + a0;
-  r = r + a1;
-  r = r + a2;
-  r = r + a3;
-  return r;
+  return tsum_strided([&](int i) { return col[d - 1 - i]; }, d);
 }
 
 // The segment walker of the backtrace (hsmm.py:331-352), one wave.  R >= the longest
@@ -655,20 +647,7 @@ __device__ void hs_walk(const HsWalk& w, int l, int t, int cs, int cd, float o, 
             for (int dp = 1; dp <= lim; ++dp) {
               // delta of (s', d'), exactly as the forward forms it: torch-order sum of the
               // d' elements rcol[e][l], e = d'-1 .. 0 (time order)
-              float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
-              const int m = dp & ~3;
-              int i = 0;
-              for (; i < m; i += 4) {
-                a0 += rcol[(dp - 1 - i) * 64 + l];
-                a1 += rcol[(dp - 2 - i) * 64 + l];
-                a2 += rcol[(dp - 3 - i) * 64 + l];
-                a3 += rcol[(dp - 4 - i) * 64 + l];
-              }
-              for (; i < dp; ++i) a0 += rcol[(dp - 1 - i) * 64 + l];
-              float oc = 0.f + a0;
-              oc = oc + a1;
-              oc = oc + a2;
-              oc = oc + a3;
+              const float oc = tsum_strided([&](int i) { return rcol[(dp - 1 - i) * 64 + l]; }, dp);
               const float uc = sdur[sp * Dm + dp - 1];
               const float mc = rmc[(dp - 1) * 64 + l];
               const float dlt = tau - dp + 1 == 0 ? oc + uc : (mc == -INFINITY ? -INFINITY : (mc + oc) + uc);
@@ -901,7 +880,10 @@ inline int hsmm_cfg(int S, int Dm) {
     if (e && e[0] == '8') return kHs8x8s64;
     return kHs4x16s64;
   }
-  if (S <= 64 && Dm < 128) return kHs8x16;
+  // Dm <= 71: from 72 frames on torch's cascade step changes the segment-sum order (tsum.h);
+  // its extra per-slot accumulators do not fit this geometry's registers (measured: 189 VGPRs
+  // spilled), so longer durations take the general form (hsmm_wide.hip), which has it
+  if (S <= 64 && Dm <= kHsRegDMax) return kHs8x16;
   if (S <= 128 && Dm < 64) return kHs4x16;
   return kHsNone;
 }
@@ -943,6 +925,21 @@ static hipError_t launch_hsmm(const HsArgs& ha, const HsChunks& hc, hipStream_t 
   return hipGetLastError();
 }
 
+// One state (S = 1): the reference skips every s' == s candidate, so only the segment that
+// starts at 0 and ends at T-1 can score: delta = fl(sum(lp[0:T]) + dur[T-1]) when T <= Dmax,
+// else -inf (hsmm.py:266-329).  obs_log_probs[b] is (T, 1), so that slice is CONTIGUOUS and
+// torch.sum takes its vectorised order (tsum.h tsum_contig).  The path is all zeros (the
+// reference's torch.zeros states; with a -inf score its walk does not terminate when T > 1).
+__global__ void __launch_bounds__(64) hsmm_single_state_kernel(HsArgs a) {
+  const int b = blockIdx.x, l = threadIdx.x, T = a.T;
+  int64_t* st = a.states + (size_t)b * T;
+  for (int u = l; u < T; u += 64) st[u] = 0;
+  if (l == 0) {
+    const float* x = a.lp + (size_t)b * T;
+    a.scores[b] = T <= a.Dm ? tsum_contig([&](int i) { return x[i]; }, T) + a.dur[T - 1] : -INFINITY;
+  }
+}
+
 // hsmm_wide.hip: the general form for sizes the register-slot geometries cannot hold
 size_t hsmm_wide_workspace_bytes(int B, int T, int S, int Dm);
 bool hsmm_wide_fits(int S, int Dm);
@@ -978,7 +975,7 @@ HMM355_API int hmm355_hsmm_viterbi_f32(const float* lp, const float* dur_lp, con
   if (!lp || !dur_lp || !log_T || !states || !scores || !workspace) return HMM355_E_ARG;
   if ((size_t)B * T * S * Dmax > ((size_t)1 << 40)) return HMM355_E_SHAPE;
   if (workspace_bytes < hmm355_hsmm_workspace_bytes(B, T, S, Dmax)) return HMM355_E_WORKSPACE;
-  if (hsmm_wide(S, Dmax)) {
+  if (hsmm_wide(S, Dmax) && S > 1) {
     const hipError_t e = launch_hsmm_wide(lp, dur_lp, log_T, B, T, S, Dmax, states, scores, workspace,
                                           static_cast<hipStream_t>(stream));
     return e == hipSuccess ? HMM355_OK : (int)e;
@@ -995,6 +992,14 @@ HMM355_API int hmm355_hsmm_viterbi_f32(const float* lp, const float* dur_lp, con
   HsChunks hc{rec, cnt, hsmm_chunks(T), hsmm_warm(), 0};
   hipStream_t st = static_cast<hipStream_t>(stream);
   hipError_t e;
+  if (S == 1) {
+    hipLaunchKernelGGL(hsmm_single_state_kernel, dim3(B), dim3(64), 0, st, ha);
+    e = hipGetLastError();
+    return e == hipSuccess ? HMM355_OK : (int)e;
+  }
+  // frames the walk never reaches (a segment without a predecessor path ends it) keep the
+  // reference's torch.zeros initial value (hsmm.py:332)
+  if ((e = hipMemsetAsync(states, 0, (size_t)B * T * sizeof(int64_t), st)) != hipSuccess) return (int)e;
   switch (hsmm_cfg(S, Dmax)) {
     case kHs16x4: e = launch_hsmm<16, 4, 64>(ha, hc, st); break;
     case kHs8x8s64: e = launch_hsmm<8, 8, 64>(ha, hc, st); break;

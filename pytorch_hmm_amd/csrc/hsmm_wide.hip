@@ -23,6 +23,7 @@
 #include <stdlib.h>
 
 #include "common.h"
+#include "tsum.h"
 
 namespace hmm355 {
 
@@ -42,9 +43,10 @@ struct HwArgs {
   int tlds;           // 1: logT staged in LDS (behind the partial maxima) when it fits
 };
 
-// obs_sum(t0, d, s) for d = 1..Dm in torch-CPU's order (oracle tsum): four strided partial
-// sums over the whole quads, the tail (d mod 4 frames) into the first, then ((a0 + a1) + a2) + a3
-// (with a leading 0 + a0).  The quads are shared by every d, so each entry is O(1).
+// obs_sum(t0, d, s) for d = 1..Dm in torch-CPU's order (tsum.h; oracle torch_sum_f32): four
+// strided lane sums over the whole quads with the cascade step every 16 quads (R_k, A_k), the
+// tail (d mod 4 frames) into lane 0, then ((l0 + l1) + l2) + l3.  The quads are shared by every
+// d, so each entry is O(1).
 __global__ void __launch_bounds__(256) hsmm_wide_osum_kernel(HwArgs a) {
   const size_t idx = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   const size_t n = (size_t)a.B * a.T * a.S;
@@ -58,22 +60,25 @@ __global__ void __launch_bounds__(256) hsmm_wide_osum_kernel(HwArgs a) {
   float* out = a.os + (((size_t)b * a.T + t0) * a.Dm) * a.S + s;
   const size_t estep = (size_t)(a.Dm + 1) * a.S;  // (e + 1, d + 1) from (e, d)
   const int dlim = a.Dm < a.T - t0 ? a.Dm : a.T - t0;
-  float q0 = 0.f, q1 = 0.f, q2 = 0.f, q3 = 0.f;  // sums over the whole quads so far
+  float q0 = 0.f, q1 = 0.f, q2 = 0.f, q3 = 0.f;  // R_k: lane sums since the last 16-quad block
+  float c0 = 0.f, c1 = 0.f, c2 = 0.f, c3 = 0.f;  // A_k: the completed blocks (cascade level 1)
+  float l0 = 0.f, l1 = 0.f, l2 = 0.f, l3 = 0.f;  // fl(R_k + A_k)
   for (int d = 1; d <= dlim; ++d) {
     const int m = d & ~3;
-    if (m == d && d >= 4) {  // a new whole quad: frames d-4 .. d-1
+    if (m == d) {  // a new whole quad: frames d-4 .. d-1
       q0 += col[(size_t)(d - 4) * a.S];
       q1 += col[(size_t)(d - 3) * a.S];
       q2 += col[(size_t)(d - 2) * a.S];
       q3 += col[(size_t)(d - 1) * a.S];
+      if ((d & (kTsumBlockElems - 1)) == 0) {
+        c0 += q0; c1 += q1; c2 += q2; c3 += q3;
+        q0 = q1 = q2 = q3 = 0.f;
+      }
+      l0 = q0 + c0; l1 = q1 + c1; l2 = q2 + c2; l3 = q3 + c3;
     }
-    float a0 = q0;
+    float a0 = l0;
     for (int i = m; i < d; ++i) a0 += col[(size_t)i * a.S];
-    float r = 0.f + a0;
-    r = r + q1;
-    r = r + q2;
-    r = r + q3;
-    out[(size_t)(d - 1) * estep] = r;
+    out[(size_t)(d - 1) * estep] = ((a0 + l1) + l2) + l3;
   }
 }
 
@@ -224,7 +229,7 @@ __global__ void __launch_bounds__(kHwNT) hsmm_wide_kernel(HwArgs a) {
       ns = win / Dm;
       nd = win % Dm + 1;
     }
-    if (nd == 0) break;  // (never-written pointer: the reference's walk would not terminate)
+    if (nd == 0) break;  // (no predecessor: frames below keep 0; the reference's walk would not terminate)
     t = start - 1;
     cs = ns;
     cd = nd;
@@ -247,9 +252,12 @@ hipError_t launch_hsmm_wide(const float* lp, const float* dur, const float* logT
   const int tlds = part + tab + 16384 <= 163840 ? 1 : 0;  // (static LDS: dmax, mpart, reductions)
   HwArgs a{lp, dur, logT, reinterpret_cast<float*>(ws), reinterpret_cast<float*>(ws + align_up(n * 4, 256)),
            scores, states, B, T, S, Dm, tlds};
+  // frames the walk never reaches keep the reference's torch.zeros value (hsmm.py:332)
+  hipError_t e = hipMemsetAsync(states, 0, (size_t)B * T * sizeof(int64_t), st);
+  if (e != hipSuccess) return e;
   const unsigned blocks = (unsigned)((n + 255) / 256);
   hipLaunchKernelGGL(hsmm_wide_osum_kernel, dim3(blocks), dim3(256), 0, st, a);
-  hipError_t e = hipGetLastError();
+  e = hipGetLastError();
   if (e != hipSuccess) return e;
   const size_t lds = part + (tlds ? tab : 0);
   e = allow_lds(hsmm_wide_kernel, lds);

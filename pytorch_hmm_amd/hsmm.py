@@ -6,7 +6,10 @@ Parameters keep the reference's names, shapes and initialisation (``transition_l
 (weibull), ``duration_means`` and ``duration_range`` buffers; hsmm.py:61-106).  The duration
 and transition tables are the reference's torch expressions (tiny, S x Dmax); the
 observation scores run in the gfx950 GMM scorer (one component) and the segment Viterbi
-(hsmm.py:208-354) in the HSMM kernel (csrc/hsmm.hip), bit-exact given the same tables.
+(hsmm.py:208-354) in the HSMM kernels (csrc/hsmm.hip, csrc/hsmm_wide.hip), bit-exact given the
+same tables at every supported size: the segment sums follow torch.sum's CPU cascade order
+(csrc/tsum.h), pinned to torch.sum for every length 1..1024 and to a reference fixture with
+83- and 82-frame segments (tests/golden/hsmm_d96.npz).
 """
 import math
 import warnings
@@ -24,7 +27,7 @@ class HSMMLayer(nn.Module):
     def __init__(self, num_states: int, feature_dim: int, duration_distribution: str = "gamma",
                  max_duration: int = 50, learnable_duration_params: bool = True, min_duration: int = 1):
         super().__init__()
-        # the segment-Viterbi kernels (csrc/hsmm.hip): S <= 64 with Dmax <= 127, or S <= 128 with
+        # the segment-Viterbi kernels (csrc/hsmm.hip): S <= 64 with Dmax <= 71, or S <= 128 with
         # Dmax <= 63, keep every open segment in registers; larger layers, up to S <= 1024 and
         # Dmax <= 1024, take the general form of csrc/hsmm_wide.hip (M history and segment sums
         # in HBM).  The reference has no limit; beyond these sizes the layer is rejected here, at

@@ -201,12 +201,33 @@ def hsmm_viterbi(lp: Tensor, dur_lp: Tensor, log_T: Tensor) -> Tuple[Tensor, Ten
     if B == 0:
         return states, scores
     L = nat.lib()
-    ws = _workspace(L.hmm355_hsmm_workspace_bytes(B, T, S, Dm), dev)
+    # The general form (S or Dmax beyond the register-slot kernels) keeps a (B,T,S,Dmax+1) fp32
+    # table: checked against the device's free memory up front, and decoded in batch slices
+    # that fit when the whole batch does not (sequences are independent).
+    per_seq = L.hmm355_hsmm_workspace_bytes(1, T, S, Dm)
+    need = L.hmm355_hsmm_workspace_bytes(B, T, S, Dm)
+    Bc = B
+    if need > _HSMM_WS_CHECK_BYTES:
+        free, _ = torch.cuda.mem_get_info(dev)
+        avail = free + torch.cuda.memory_reserved(dev) - torch.cuda.memory_allocated(dev)
+        if per_seq > 0.9 * avail:
+            raise torch.cuda.OutOfMemoryError(
+                f"HSMM decode of one sequence (T={T}, S={S}, max_duration={Dm}) needs "
+                f"{per_seq / 2**30:.1f} GiB of workspace (T*S*(max_duration+1)*4 bytes), "
+                f"{avail / 2**30:.1f} GiB are available on {dev}")
+        Bc = max(1, min(B, int(0.9 * avail) // per_seq))
+    ws = _workspace(L.hmm355_hsmm_workspace_bytes(Bc, T, S, Dm), dev)
     with torch.cuda.device(dev):
-        nat.check(L.hmm355_hsmm_viterbi_f32(
-            nat.ptr(lp), nat.ptr(dur_lp), nat.ptr(log_T), B, T, S, Dm, nat.ptr(states),
-            nat.ptr(scores), nat.ptr(ws), ws.numel(), nat.stream_of(dev)))
+        for b0 in range(0, B, Bc):
+            nb = min(Bc, B - b0)
+            nat.check(L.hmm355_hsmm_viterbi_f32(
+                nat.ptr(lp[b0:b0 + nb]), nat.ptr(dur_lp), nat.ptr(log_T), nb, T, S, Dm,
+                nat.ptr(states[b0:b0 + nb]), nat.ptr(scores[b0:b0 + nb]), nat.ptr(ws), ws.numel(),
+                nat.stream_of(dev)))
     return states, scores
+
+
+_HSMM_WS_CHECK_BYTES = 1 << 30  # workspaces above this are checked against free device memory
 
 
 @hsmm_viterbi.register_fake

@@ -219,10 +219,15 @@ def fx_mixture_full(name, S, D, C, B, T, seed):
          states=npf(states), scores=npf(scores), input_sha256=sha(npf(x)))
 
 
-def fx_hsmm(name, S, D, Dmax, B, T, seed):
-    """HSMMLayer segment Viterbi (hsmm.py:181-354); the literal 5-deep loop, small sizes only."""
+def fx_hsmm(name, S, D, Dmax, B, T, seed, dur_params=None):
+    """HSMMLayer segment Viterbi (hsmm.py:181-354); the literal 5-deep loop, small sizes only.
+    dur_params = (shape, rate) raw parameter values (before softplus) to favour long segments."""
     torch.manual_seed(seed)
     h = HSMMLayer(S, D, max_duration=Dmax)
+    if dur_params is not None:
+        with torch.no_grad():
+            h.duration_shape.fill_(dur_params[0])
+            h.duration_rate.fill_(dur_params[1])
     x = torch.randn(B, T, D)
     with torch.no_grad():
         lp = h.get_observation_log_probs(x)
@@ -468,6 +473,9 @@ def main():
         ("hsmm_s5", lambda: fx_hsmm("hsmm_s5", 5, 30, 20, 2, 30, 0)),
         ("hsmm_s2", lambda: fx_hsmm("hsmm_s2", 2, 3, 2, 1, 4, 1)),
         ("hsmm_s8", lambda: fx_hsmm("hsmm_s8", 8, 20, 10, 1, 40, 2)),
+        # segments of 72+ frames (decoded: 83 + 82) whose sums take torch.sum's cascade order
+        # (hsmm.py:273,285), not the plain 4-lane order: gamma mode ~85 frames
+        ("hsmm_d96", lambda: fx_hsmm("hsmm_d96", 3, 6, 96, 1, 165, 1, dur_params=(30.0, -0.9))),
         ("smk_gamma", lambda: fx_semimarkov("smk_gamma", 4, 6, 10, 30, 2, 0)),
         ("smk_poisson", lambda: fx_semimarkov("smk_poisson", 5, 8, 8, 40, 1, 1, dist="poisson", min_duration=2)),
         ("smk_gaussian", lambda: fx_semimarkov("smk_gaussian", 6, 5, 12, 48, 1, 2, dist="gaussian")),

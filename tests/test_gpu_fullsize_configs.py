@@ -95,8 +95,10 @@ def test_config2_gaussian_fullsize_vs_reference():
 # --------------------------------------------------------------------------- config 5
 @torch.no_grad()
 def test_config5_hsmm_fullsize_vs_c_oracle():
+    """BASELINE config 5 at the bench's own size (B = 16: the chunk-walk and stitch grid of
+    the chunked backtrace at its real extent), bit-exact against the C restatement."""
     import pytorch_hmm_amd as ph
-    B, T, S, D, Dm = 3, 2000, 64, 80, 40
+    B, T, S, D, Dm = 16, 2000, 64, 80, 40
     torch.manual_seed(0)
     layer = ph.HSMMLayer(S, D, max_duration=Dm).to(DEV)
     x = torch.from_numpy(O.uniform_obs(5, (B, T, D), -2.0, 2.0)).to(DEV)
@@ -104,7 +106,7 @@ def test_config5_hsmm_fullsize_vs_c_oracle():
     lp = layer.get_observation_log_probs(x).cpu().numpy()
     dur = torch.log(layer.get_duration_probabilities() + layer.eps)[:, :Dm].cpu().numpy()
     lT = torch.log(layer.get_transition_matrix() + layer.eps).cpu().numpy()
-    cs, csc = O.c_hsmm(lp, dur, lT)
+    cs, csc = O.c_hsmm(lp, dur, lT, workers=8)
     st = states.cpu().numpy()
     assert np.array_equal(st, cs), "HSMM segmentation != C oracle at T=2000"
     assert np.array_equal(scores.cpu().numpy().view(np.int32), csc.view(np.int32))

@@ -158,7 +158,7 @@ def test_mixture_viterbi_bitexact_given_lp(name):
 
 
 # ---------------------------------------------------------------------------- HSMM
-@pytest.mark.parametrize("name", ["hsmm_s5", "hsmm_s2", "hsmm_s8"])
+@pytest.mark.parametrize("name", ["hsmm_s5", "hsmm_s2", "hsmm_s8", "hsmm_d96"])
 def test_hsmm_bitexact_given_lp(name):
     g = golden(name)
     o = ops()
@@ -277,6 +277,70 @@ def test_hsmm_impossible_transitions_and_durations(sub, monkeypatch):
     states, scores = o.hsmm_viterbi(t(lp), t(dur), t(logT))
     assert np.array_equal(states.cpu().numpy(), cs)
     assert np.array_equal(scores.cpu().numpy(), csc)
+
+
+@pytest.mark.parametrize("T,Dm", [(1, 1), (7, 7), (50, 64), (300, 400), (1024, 1024), (90, 40)])
+def test_hsmm_single_state_contiguous_sum(T, Dm):
+    """num_states = 1: obs_log_probs[b] is (T, 1), so the reference's only scoring segment
+    sum(lp[0:T, 0]) is a CONTIGUOUS slice and torch.sum takes its vectorised order; pinned to
+    torch.sum itself (hsmm.py:266-274).  T > Dmax: no segment scores (-inf; the reference's walk
+    would not terminate), the path stays the reference's torch.zeros."""
+    rng = np.random.default_rng(T + Dm)
+    lp = (-(rng.random((3, T, 1), dtype=np.float32) * 40 + 80)).astype(np.float32)
+    dur = np.log(rng.random((1, Dm), dtype=np.float32) + np.float32(1e-8)).astype(np.float32)
+    logT = np.zeros((1, 1), np.float32)
+    o = ops()
+    states, scores = o.hsmm_viterbi(t(lp), t(dur), t(logT))
+    assert np.array_equal(states.cpu().numpy(), np.zeros((3, T), np.int64))
+    lpt = torch.from_numpy(lp)
+    for b in range(3):
+        want = (torch.sum(lpt[b][0:T, 0]) + torch.from_numpy(dur)[0, T - 1]).numpy() if T <= Dm else np.float32(-np.inf)
+        assert scores[b].cpu().numpy().tobytes() == np.float32(want).tobytes()
+
+
+@pytest.mark.parametrize("S,Dm,wide", [(4, 20, "0"), (40, 100, "0"), (6, 30, "1")])
+def test_hsmm_no_path_leaves_reference_zeros(S, Dm, wide, monkeypatch):
+    """A left-to-right chain of S states with durations <= Dm cannot cover T > S * Dm frames:
+    every final score is -inf, the walk has no predecessor after its first segment, and the
+    frames it never reaches keep the reference's torch.zeros value (hsmm.py:332; the reference's
+    own walk would not terminate here).  Both the register-slot and the general form."""
+    monkeypatch.setenv("HMM355_HSMM_WIDE", wide)
+    rng = np.random.default_rng(S)
+    T = S * Dm + 10
+    lp = (-(rng.random((2, T, S), dtype=np.float32) * 10 + 5)).astype(np.float32)
+    dur = np.log(rng.random((S, Dm), dtype=np.float32) + np.float32(1e-3)).astype(np.float32)
+    logT = np.full((S, S), -np.inf, np.float32)
+    for i in range(S - 1):
+        logT[i, i + 1] = 0.0
+    o = ops()
+    for _ in range(2):  # the second call reuses a dirty output buffer from the caching allocator
+        states, scores = o.hsmm_viterbi(t(lp), t(dur), t(logT))
+        assert np.all(np.isneginf(scores.cpu().numpy()))
+        assert np.array_equal(states.cpu().numpy(), np.zeros((2, T), np.int64))
+
+
+def test_hsmm_workspace_check_slices_the_batch(monkeypatch):
+    """The general form's (B,T,S,Dmax+1) workspace is checked against free device memory: a
+    batch that does not fit is decoded in slices that do (same results), and a single sequence
+    that does not fit raises OutOfMemoryError with the sizes, before any allocation."""
+    from pytorch_hmm_amd import ops as o
+    import pytorch_hmm_amd._native as nat
+    rng = np.random.default_rng(9)
+    B, T, S, Dm = 5, 120, 70, 80
+    lp = (-(rng.random((B, T, S), dtype=np.float32) * 40 + 80)).astype(np.float32)
+    dur = np.log(rng.random((S, Dm), dtype=np.float32) + np.float32(1e-8)).astype(np.float32)
+    logT = np.log(rng.random((S, S), dtype=np.float32) + np.float32(1e-8)).astype(np.float32)
+    cs, csc = O.c_hsmm(lp, dur, logT)
+    per_seq = nat.lib().hmm355_hsmm_workspace_bytes(1, T, S, Dm)
+    monkeypatch.setattr(o, "_HSMM_WS_CHECK_BYTES", 0)
+    monkeypatch.setattr(torch.cuda, "memory_reserved", lambda *a: 0)
+    monkeypatch.setattr(torch.cuda, "memory_allocated", lambda *a: 0)
+    monkeypatch.setattr(torch.cuda, "mem_get_info", lambda *a: (int(2.5 * per_seq / 0.9), 1 << 40))
+    states, scores = o.hsmm_viterbi(t(lp), t(dur), t(logT))   # slices of 2, 2, 1
+    assert np.array_equal(states.cpu().numpy(), cs) and np.array_equal(scores.cpu().numpy(), csc)
+    monkeypatch.setattr(torch.cuda, "mem_get_info", lambda *a: (per_seq // 2, 1 << 40))
+    with pytest.raises(torch.cuda.OutOfMemoryError, match="max_duration"):
+        o.hsmm_viterbi(t(lp), t(dur), t(logT))
 
 
 # ---------------------------------------------- forward-backward on log-emissions (OBS_LOG)

@@ -102,7 +102,7 @@ def test_mixture_chunked_emission_identical():
     assert eq(O.mixture_log_probs(*args, t_chunk=37), g["log_probs"])
 
 
-@pytest.mark.parametrize("name", ["hsmm_s5", "hsmm_s2", "hsmm_s8"])
+@pytest.mark.parametrize("name", ["hsmm_s5", "hsmm_s2", "hsmm_s8", "hsmm_d96"])
 def test_hsmm_oracle(name):
     g = golden(name)
     x = torch.from_numpy(g["x"])
@@ -179,3 +179,23 @@ def test_c_tv_oracle_matches_reference(name):
     assert np.abs(post - g["posterior"]).max() < 1e-4   # the reference is fp32
     np.testing.assert_allclose(la, g["log_forward"], rtol=2e-5, atol=2e-5)
     np.testing.assert_allclose(lb, g["log_backward"], rtol=2e-5, atol=2e-5)
+
+
+@pytest.mark.parametrize("S", [1, 2, 5, 64, 150])
+def test_tsum_matches_torch_sum(S):
+    """The HSMM segment sum torch.sum(obs_log_probs[t:t+d, s]) (reference hsmm.py:273,285) in
+    the oracle's restatement of torch-CPU's cascade order, for every d = 1..1024 (the cascade
+    levels change the order from d = 72 on; S = 1 is the contiguous, vectorised path)."""
+    rng = np.random.default_rng(S)
+    T = 1100
+    lp = torch.from_numpy((rng.standard_normal((T, S)) * 3 - 5).astype(np.float32))
+    lpn = lp.numpy()
+    s = S // 2
+    bad = []
+    for d in range(1, 1025):
+        t0 = int(rng.integers(0, T - d + 1))
+        want = torch.sum(lp[t0:t0 + d, s]).numpy()
+        got = O.c_torch_sum(lpn[t0:t0 + d, s])
+        if want.tobytes() != got.tobytes():
+            bad.append(d)
+    assert not bad, bad[:20]
