@@ -79,15 +79,34 @@ class StreamingHMMProcessor(nn.Module):
     def get_transition_matrix(self) -> torch.Tensor:
         return F.softmax(self.transition_logits, dim=-1)
 
+    def refresh_transitions(self):
+        """Drop the cached log-transition table: the next chunk re-forms it.  Needed only after
+        writing the logits through ``.data`` (``p.data.copy_(...)``, ``p.data -= ...``) in eval
+        mode: such writes do not bump the parameter's version counter, so the cache cannot see
+        them.  (In-place ops on the parameter itself, ``load_state_dict``, ``train()``/``eval()``
+        and replacing the parameter are all seen; in training mode the table is re-formed on
+        every chunk, as the reference does.)"""
+        self._log_t_cache = None
+
+    def train(self, mode: bool = True):
+        self._log_t_cache = None
+        return super().train(mode)
+
+    def _load_from_state_dict(self, *args, **kwargs):
+        self._log_t_cache = None
+        return super()._load_from_state_dict(*args, **kwargs)
+
     def _log_transitions(self):
         """log(softmax + 1e-8) (streaming.py:289-290), formed on a CPU copy — the reference's
-        path is torch-CPU — so the kernels see its bits.  Cached on the parameter's identity,
-        storage and version: a chunk makes no device -> host -> device round trip (and no host
-        sync) unless the transition logits changed since the last chunk."""
+        path is torch-CPU — so the kernels see its bits.  In eval mode it is cached on the
+        parameter's identity, storage and version: a chunk makes no device -> host -> device
+        round trip (and no host sync) unless the transition logits changed since the last chunk
+        (see refresh_transitions for ``.data`` writes).  In training mode, where an optimiser
+        may write the logits in any way between chunks, it is re-formed every chunk."""
         p = self.transition_logits
         key = (p.data_ptr(), p._version, str(p.device))
         c = getattr(self, "_log_t_cache", None)
-        if c is None or c[0] != key or c[1] is not p:
+        if c is None or c[0] != key or c[1] is not p or (self.training and p.requires_grad):
             lt = torch.log(F.softmax(p.detach().cpu(), dim=-1) + 1e-8).to(p.device)
             self._log_t_cache = (key, p, lt)
             c = self._log_t_cache

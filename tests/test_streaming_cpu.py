@@ -120,7 +120,7 @@ def test_log_transition_table_cached_per_parameter_version():
     round trip per chunk), and rebuilt when the logits change in place or are replaced."""
     from pytorch_hmm_amd.streaming import StreamingHMMProcessor
     torch.manual_seed(0)
-    p = StreamingHMMProcessor(6, 4, chunk_size=16, overlap_size=4)
+    p = StreamingHMMProcessor(6, 4, chunk_size=16, overlap_size=4).eval()
     a = p._log_transitions()
     assert p._log_transitions() is a
     ref = torch.log(torch.softmax(p.transition_logits.detach(), -1) + 1e-8)
@@ -132,3 +132,30 @@ def test_log_transition_table_cached_per_parameter_version():
     p.transition_logits = torch.nn.Parameter(torch.zeros(6, 6))
     c = p._log_transitions()
     assert c is not b and torch.allclose(c, torch.full((6, 6), float(np.log(1 / 6 + 1e-8))))
+
+
+def test_log_transition_cache_sees_data_writes_state_dicts_and_training():
+    """writes through .data do not bump the version counter.  Training mode re-forms
+    the table every chunk (as the reference does); in eval mode load_state_dict, train()/eval()
+    and refresh_transitions() invalidate it."""
+    from pytorch_hmm_amd.streaming import StreamingHMMProcessor
+    torch.manual_seed(1)
+    p = StreamingHMMProcessor(5, 4, chunk_size=16, overlap_size=4)
+    want = lambda: torch.log(torch.softmax(p.transition_logits.detach(), -1) + 1e-8)
+    assert p.training
+    a = p._log_transitions()
+    p.transition_logits.data -= 0.3 * torch.randn(5, 5)      # an optimiser writing .data
+    assert torch.equal(p._log_transitions(), want()) and not torch.equal(a, want())
+    p.eval()
+    b = p._log_transitions()
+    assert p._log_transitions() is b
+    sd = {k: v.clone() for k, v in p.state_dict().items()}
+    sd["transition_logits"] = torch.randn(5, 5)
+    p.load_state_dict(sd)
+    assert torch.equal(p._log_transitions(), want())
+    p.transition_logits.data.copy_(torch.randn(5, 5))        # bypasses the version counter...
+    p.refresh_transitions()                                  # ...so the documented hook
+    assert torch.equal(p._log_transitions(), want())
+    p.transition_logits.data.mul_(2.0)
+    p.train(); p.eval()
+    assert torch.equal(p._log_transitions(), want())
