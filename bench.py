@@ -620,9 +620,14 @@ class NsStep:
                 post.record_stream(sc)
                 states.record_stream(sc)
             with torch.cuda.stream(sc):
+                if self.timing is not None:
+                    g0 = torch.cuda.Event(enable_timing=True)
+                    g0.record(sc)
                 self.gatherer(post, states)
-                ev = torch.cuda.Event()
+                ev = torch.cuda.Event(enable_timing=self.timing is not None)
                 ev.record(sc)
+                if self.timing is not None:
+                    self.timing["gather"].append((g0, ev))
             self.read_done[slot] = ev
         self.k += 1
 
@@ -692,7 +697,7 @@ def main():
     # per-op launch durations for the roofline: HIP events on each op's own stream around its
     # graph replay, over the timed steps (an event pair costs the step ~1-2 us of queue work;
     # the wall clock below is what `value` uses)
-    step.timing = {n: [] for n in step.names}
+    step.timing = {n: [] for n in (*step.names, "gather")}
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
@@ -708,6 +713,17 @@ def main():
     ev, step.timing = step.timing, None
     fb_ms = sum(a.elapsed_time(b) for a, b in ev["fb"]) / len(ev["fb"])
     vit_ms = sum(a.elapsed_time(b) for a, b in ev["vit"]) / len(ev["vit"])
+    gather_info = None
+    if ev["gather"]:
+        # the gather's own time on the communication stream (events around the dist.gather
+        # calls), and the bytes it moves into rank 0 per step: (world - 1) slices of posteriors
+        # (B*T*N fp32) + states (B*T int64); DESIGN.md §6 models it against xGMI
+        g_ms = [a.elapsed_time(b) for a, b in ev["gather"]]
+        rx = (world - 1) * B * T * (4 * N + 8)
+        gather_info = {"gather_ms": sum(g_ms) / len(g_ms), "gather_ms_max": max(g_ms),
+                       "bytes_into_rank0_per_step": rx,
+                       "rank0_rx_GBps": rx / (sum(g_ms) / len(g_ms) * 1e-3) / 1e9,
+                       "model_ms_at_153GBps_per_link": B * T * (4 * N + 8) / 153e9 * 1e3}
     global_b = args.batch if args.strong else B * world
     value = global_b * T * args.steps / elapsed
     ms_per_step = elapsed / args.steps * 1e3
@@ -724,6 +740,13 @@ def main():
         kernels = "vit_fwd_kernel + vit_psi_kernel + vit_backtrace_kernel"
     achieved = bytes_per_launch / (dur_ms * 1e-3) / 1e9
     traffic, traffic_src = profiled_traffic(dom, B, T, N, args.transition)
+    # both ops' fractions (north_star's target names forward-backward's)
+    op_roofline = {}
+    for name, ms, bpl in (("forward_backward", fb_ms, 16 * N * B * T), ("viterbi", vit_ms, (8 * N + 8) * B * T)):
+        a_ = bpl / (ms * 1e-3) / 1e9
+        tr, trs = profiled_traffic(name, B, T, N, args.transition)
+        op_roofline[name] = {"achieved": a_, "frac": a_ / HBM_PEAK_GBS, "bytes_per_launch": bpl,
+                             "avg_launch_ms": ms, "traffic": tr, "traffic_source": trs}
     out = {
         "metric": "frames/sec forward-backward+Viterbi, B=32 T=2000 N=128, 1/2/4/8 GPU",
         "value": value, "unit": "frames/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
@@ -745,7 +768,10 @@ def main():
                      "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
                      "traffic": traffic, "traffic_source": traffic_src,
                      "bytes_per_launch": bytes_per_launch, "avg_launch_ms": dur_ms},
+        "roofline_ops": op_roofline,
     }
+    if gather_info is not None:
+        out["gather"] = gather_info
     if rank == 0 and world == 1 and args.cpu_seconds > 0:
         out["cpu_baseline"] = cpu_baseline(B, T, N, args.cpu_seconds, hmm.P)
         out["cpu_baseline"]["speedup_gpu_over_cpu"] = value / out["cpu_baseline"]["value"]
