@@ -135,6 +135,16 @@ int hmm355_viterbi_plan_f32(const float* obs, int obs_mode, const float* log_P, 
                             const void* plan, int B, int T, int N, int64_t* states,
                             float* log_delta, float* final_score, void* workspace,
                             size_t workspace_bytes, void* stream);
+/* Viterbi with flags.  HMM355_VIT_PLAN_BANDED: the caller read hmm355_plan_banded(plan) == 1
+ * for this plan.  The chain kernel then finishes the decode itself (chunk maps composed while
+ * the chain runs, the backtrace after it: one launch instead of three) when N > 64 and
+ * T <= 262144; otherwise the flag is ignored.  Passing the flag with a plan that is not banded
+ * is a caller error: the states come back as -1 and the final score as NaN. */
+#define HMM355_VIT_PLAN_BANDED 0x1u
+int hmm355_viterbi_plan_ex_f32(const float* obs, int obs_mode, const float* log_P, const float* init,
+                               const void* plan, unsigned flags, int B, int T, int N, int64_t* states,
+                               float* log_delta, float* final_score, void* workspace,
+                               size_t workspace_bytes, void* stream);
 
 /* ---------------------------------------------------------------------------------
  * Viterbi.  Replaces HMMPyTorch.viterbi_decode (hmm.py:132-184) and
@@ -163,7 +173,7 @@ int hmm355_viterbi_f32(const float* obs, int obs_mode, const float* log_P, const
  *   x (B,T,D); means, log_vars (S,C,D); log_w (S,C) = log(clamp(softmax(w),1e-8));
  *   out (B,T,S) = LSE_c[ -0.5*(sum_d (x-mu)^2/exp(lv) + sum_d lv + D*log(2pi)) + log_w ].
  * `mix_lse` selects the reference's mixture LSE (clamped sum, :141-155); with C == 1 pass 0
- * to get the plain component log-density.  Supported: 1 <= D <= 128, 1 <= C <= 256,
+ * to get the plain component log-density.  Supported: 1 <= D <= 8192, 1 <= C <= 256,
  * 1 <= S*C <= 65536, B*T < 2^31.  workspace >= hmm355_gmm_workspace_bytes(B,T,D,S,C)
  * (per-component scales and an fp64 copy of the frames; written by the call).  The
  * quadratic form is accumulated in fp64 and each score rounded to fp32 once, so the scores

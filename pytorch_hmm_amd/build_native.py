@@ -15,7 +15,8 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
 LIBDIR = os.path.join(HERE, "lib")
 LIB = os.path.join(LIBDIR, "libhmm355.so")
-SOURCES = ["capi.hip", "fb.hip", "viterbi.hip", "gmm.hip", "hsmm.hip", "hsmm_wide.hip", "tv.hip", "semimarkov.hip", "stream.hip", "adjoint.hip"]
+SOURCES = ["capi.hip", "fb.hip", "fb_np64.hip", "fb_np128.hip", "fb_np256.hip", "viterbi.hip", "vit_np64.hip",
+           "vit_np128.hip", "vit_np256.hip", "gmm.hip", "hsmm.hip", "hsmm_wide.hip", "tv.hip", "semimarkov.hip", "stream.hip", "adjoint.hip"]
 ARCH = os.environ.get("HMM355_ARCH", "gfx950")
 FLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-fno-slp-vectorize", "-fno-honor-nans",
          "-Wno-unused-result", "-I" + os.path.join(HERE, "..", "include")]

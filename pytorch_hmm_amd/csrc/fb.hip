@@ -28,17 +28,11 @@
 
 namespace hmm355 {
 
+// per-NP launchers (fb_kern.h, instantiated in fb_np64/128/256.hip)
 template <int NP>
-__global__ void __launch_bounds__(RC<NP>::NT) fb_recur_kernel(RecArgs fa, RecArgs fb) {
-  extern __shared__ __attribute__((aligned(16))) float lds[];
-  const int b = blockIdx.x >> 1;
-  if (blockIdx.x & 1) {
-    if (!(kAbl & (1 << 20))) rec_dispatch<NP, kFbBeta>(fb, lds, b);  // diagnostic: alpha only
-  } else {
-    if (!(kAbl & (1 << 21))) rec_dispatch<NP, kFbAlpha>(fa, lds, b);  // diagnostic: beta only
-  }
-}
-
+hipError_t launch_fb(const RecArgs& fa, const RecArgs& fb, const PostArgs& pa, bool prep, hipStream_t st);
+template <int NP>
+hipError_t launch_fb_pair(const PairArgs& pa, int B, hipStream_t st);
 // OBS_LOG: the row maxima M_t = max_j lo_t[j] (one wave per (b,t) row, grid-stride); the
 // chains stage e_t = exp(lo_t - M_t) and add M_t to the log-scales (recur.h rec_stage /
 // rec_flush), so log-emissions far below -87 (Gaussian log-densities at D = 80) do not
@@ -54,24 +48,6 @@ __global__ void __launch_bounds__(256) row_max_kernel(const float* __restrict__ 
     v = wave_max_dpp2(v);
     if (l == 0) m[row] = (v > -INFINITY && v < INFINITY) ? v : 0.f;
   }
-}
-
-template <int NP>
-static hipError_t launch_fb(const RecArgs& fa, const RecArgs& fb, const PostArgs& pa, bool prep, hipStream_t st) {
-  hipError_t e = allow_lds(fb_recur_kernel<NP>, kExclusiveLds);  // own the CU (recur.h)
-  if (e != hipSuccess) return e;
-  if (fa.band && prep) {
-    e = launch_band_prep(fa.mat, fa.N, const_cast<BandDesc*>(fa.band), st);
-    if (e != hipSuccess) return e;
-  }
-  hipLaunchKernelGGL(fb_recur_kernel<NP>, dim3(2 * fa.B), dim3(RC<NP>::NT), kExclusiveLds, st, fa, fb);
-  e = hipGetLastError();
-  if (e != hipSuccess) return e;
-  const size_t rows = (size_t)pa.B * pa.T;
-  const size_t waves = rows < (size_t)kPostWaves ? rows : (size_t)kPostWaves;
-  const unsigned blocks = (unsigned)((waves + 3) / 4);
-  hipLaunchKernelGGL(fb_posterior_kernel<NP>, dim3(blocks), dim3(256), 0, st, pa);
-  return hipGetLastError();
 }
 
 // Workspace layout (documented in include/hmm355.h for adjoint callers):
@@ -183,17 +159,7 @@ HMM355_API int hmm355_forward_backward_plan_f32(const float* obs, int obs_mode, 
       (size_t)T * NP * sizeof(float) < ((size_t)1 << 31)) {
     // both chains of a sequence in one workgroup, outputs formed inside it (fbpair.h)
     PairArgs pa{fa, fb, posterior, forward, backward, lik_ref, out_mask};
-    hipError_t e;
-    if (NP == 64) {
-      e = allow_lds(fb_pair_kernel<64>, PairL<64>::LDS_FLOATS * sizeof(float));
-      if (e == hipSuccess)
-        hipLaunchKernelGGL(fb_pair_kernel<64>, dim3(B), dim3(PairL<64>::NT), PairL<64>::LDS_FLOATS * sizeof(float), st0, pa);
-    } else {
-      e = allow_lds(fb_pair_kernel<128>, PairL<128>::LDS_FLOATS * sizeof(float));
-      if (e == hipSuccess)
-        hipLaunchKernelGGL(fb_pair_kernel<128>, dim3(B), dim3(PairL<128>::NT), PairL<128>::LDS_FLOATS * sizeof(float), st0, pa);
-    }
-    if (e == hipSuccess) e = hipGetLastError();
+    const hipError_t e = NP == 64 ? launch_fb_pair<64>(pa, B, st0) : launch_fb_pair<128>(pa, B, st0);
     return e == hipSuccess ? HMM355_OK : (int)e;
   }
   // the chains' flushes write forward / backward (exp(log u + LA), exp(log v + LB)) from their
@@ -230,8 +196,3 @@ HMM355_API int hmm355_forward_backward_f32(const float* obs, int obs_mode, const
                                         backward, loglik, lik_ref, workspace, workspace_bytes, stream);
 }
 
-#if HMM355_STAMP
-HMM355_API int hmm355_debug_stamps_fb(unsigned long long* out, int n) {
-  return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(hmm355::g_rec_stamps), sizeof(unsigned long long) * (size_t)n);
-}
-#endif

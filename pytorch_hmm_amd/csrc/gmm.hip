@@ -35,6 +35,9 @@ constexpr int kGmmThreads = 256;
 constexpr int kGmmFrames = 64;  // frames per workgroup (accumulators per lane)
 constexpr int kGmmDc = 8;       // dims per chunk (one s_load_dwordx16 of fp64 per frame)
 constexpr int kGmmSub = 16;     // frames per LDS LSE tile
+// feature dimensions: the scorer walks D in 8-dim chunks with no per-D register or LDS state,
+// so D is bounded only by the workspace (frames * D * 8 bytes for the fp64 frame tiles)
+constexpr int kGmmDMax = 8192;
 
 __global__ void gmm_prep_kernel(const float* __restrict__ means, const float* __restrict__ log_vars,
                                 const float* __restrict__ log_w, double* __restrict__ pw,
@@ -202,7 +205,7 @@ static size_t gmm_ws_layout(int B, int T, int D, int S, int C, char* base, GmmWs
 using namespace hmm355;
 
 HMM355_API size_t hmm355_gmm_workspace_bytes(int B, int T, int D, int S, int C) {
-  if (B < 0 || T < 0 || D < 1 || D > 128 || S < 1 || C < 1 || C > 256) return 0;
+  if (B < 0 || T < 0 || D < 1 || D > kGmmDMax || S < 1 || C < 1 || C > 256) return 0;
   return gmm_ws_layout(B, T, D, S, C, nullptr, nullptr);
 }
 
@@ -210,7 +213,7 @@ HMM355_API int hmm355_gmm_diag_logprob_f32(const float* x, const float* means, c
                                            const float* log_w, int B, int T, int D, int S, int C, int mix_lse,
                                            float* out, void* workspace, size_t workspace_bytes, void* stream) {
   if (B < 0 || T < 0 || D < 1 || S < 1 || C < 1) return HMM355_E_ARG;
-  if (D > 128 || C > 256 || (size_t)S * C > 65536) return HMM355_E_SHAPE;
+  if (D > kGmmDMax || C > 256 || (size_t)S * C > 65536) return HMM355_E_SHAPE;
   if ((size_t)B * T == 0) return HMM355_OK;
   if ((size_t)B * T > ((size_t)1 << 31) - kGmmFrames) return HMM355_E_SHAPE;
   if (!x || !means || !log_vars || !out || !workspace) return HMM355_E_ARG;

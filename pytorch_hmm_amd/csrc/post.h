@@ -167,6 +167,7 @@ struct VitArgs {
   uint8_t* G;            // (B,nchunks,NP) workspace
   int B, T, N, obs_mode, nchunks;
   const BandDesc* band;  // banded decomposition (band.h) or null
+  int vdiag;             // diagnostic bits for RecArgs::vtail (timing only)
 };
 
 // chunk map: G[j] = state at t_lo - 1 given state j at t_hi (psi rows of the chunk in LDS)

@@ -55,6 +55,13 @@ struct RC {
   static constexpr int OFF_LOGT = OFF_M + MRING;           // [256] doubles: Viterbi log table (logcr.h)
   static constexpr int LDS_FLOATS = OFF_LOGT + 512;
   static_assert(LDS_FLOATS * 4 <= kExclusiveLds, "LDS layout too large");
+  // fused Viterbi decode only (RecArgs::vtail; the chain kernel owns all 160 KiB): the psi rows
+  // of the last 64 steps (bytes [64][NP]) and the composer's running chunk map F (bytes [NP])
+  static constexpr int PSR = 64;
+  static constexpr int OFF_PSR = LDS_FLOATS;
+  static constexpr int OFF_FMAP = OFF_PSR + PSR * NP / 4;
+  static constexpr int OFF_GMAP = OFF_FMAP + NP / 4;  // chunk maps for the tail's walk (as many as fit)
+  static_assert(OFF_GMAP * 4 <= kExclusiveLds, "fused Viterbi LDS layout too large");
 };
 
 // Sum over all 64 lanes with DPP only (row sums, then row_bcast:15 / row_bcast:31), read
@@ -210,6 +217,13 @@ struct RecArgs {
   uint8_t* psi;          // Viterbi, fused banded chain only: (B,T,NP) argmax pointers (kVitFused)
   const float* rmax;     // FB with OBS_LOG: (B,T) row maxima M_t (e_t = exp(lo_t - M_t)), else null
   float* out_exp;        // FB: (B,T,N) forward (alpha) / backward (beta) output written at flush, or null
+  // Viterbi with vtail = 1 (fused banded chain only, kVitFused): the chain kernel finishes the
+  // decode itself -- chunk maps composed during the chain, then the backtrace (rec_band)
+  uint8_t* G;            // (B, nchunks, NP) chunk maps
+  int64_t* states;       // (B,T) decoded path
+  float* final_score;    // (B) max of the last trellis row, or null
+  int nchunks;
+  int vtail;
 };
 
 // The banded Viterbi chain computes the argmax pointers psi itself (helper waves on the idle
@@ -1235,10 +1249,13 @@ __device__ __forceinline__ void rec_band(const RecArgs& a, float* lds, int b, co
   const int grp = (w >> 3) * 3 + (w & 3) - 1;  // WIDE: waves 1,2,3 / 5,6,7 -> 0,1,2; 9,.. / 13,.. -> 3,4,5
   const bool stager = WIDE ? ((w & 4) == 0 && (w & 3) != 0) : (w > 0 && w <= NH);
   const bool psiw = WIDE && (w & 4) != 0 && (w & 3) != 0;
+  // fused decode (a.vtail): wave 4 (the chain's SIMD, otherwise idle) composes the chunk maps
+  // while the chain runs, and every live wave joins the backtrace after it (vit_tail below)
+  const bool composer = FUSE && a.vtail && w == 4;
   const int hi = WIDE ? grp : w - 1;
   auto vw_of = [&](int h) -> int { return hi + h * NH; };  // virtual staging wave h of this helper
   constexpr bool FB = KIND != kVit;
-  if (w != 0 && !stager && !psiw) return;  // ended waves take no part in s_barrier
+  if (w != 0 && !stager && !psiw && !composer) return;  // ended waves take no part in s_barrier
   const int T = a.T, N = a.N;
   const int nblocks = (T + 15) / 16;
   double base = (KIND == kFbBeta && a.bscale) ? (double)a.bscale[b] : 0.0;
@@ -1263,8 +1280,194 @@ __device__ __forceinline__ void rec_band(const RecArgs& a, float* lds, int b, co
   }
   lds_barrier();
 
+  // ---- fused decode (vtail): chunk maps and the backtrace inside the chain kernel.
+  // The psi waves also keep the last 64 psi rows in LDS (OFF_PSR); the composer wave folds each
+  // block's rows into the running map of its 64-step chunk, F_t[s] = F_{t-1}[psi_t[s]] (F = the
+  // state at the chunk's first step - 1 given state s at t; one dependent LDS gather per row),
+  // three blocks behind the chain, and stores the chunk map G_c = F_{t_hi} (post.h
+  // compose_chunk_map's map, built forward instead of backward).  After the chain: wave 0 walks
+  // the maps from the final state (first argmax of delta_{T-1}, hmm.py:174) down to chunk 0,
+  // then every live wave expands whole chunks, walking psi rows held in registers with
+  // v_readlane (hmm.py:177-178).  Replaces vit_psi_kernel + vit_backtrace_kernel and their two
+  // launches.
+  // chunk maps kept in LDS for the tail's walk (OFF_GMAP, map c at index c - 1) while they fit;
+  // beyond that the walk stages them from G in batches
+  constexpr int GMAP_CAP = ((int)(kExclusiveLds / 4) - C::OFF_GMAP) * 4 / NP < 256
+                               ? ((int)(kExclusiveLds / 4) - C::OFF_GMAP) * 4 / NP : 256;
+  [[maybe_unused]] unsigned fr = 0;  // the composer's running map F: NB bytes, states NB*l + j
+  [[maybe_unused]] auto compose_block = [&](int bk) {
+    if constexpr (FUSE) {
+      if (bk < 0 || (a.vtail & 2)) return;  // (vtail bit 1: diagnostic, no composition)
+      const uint8_t* psr = reinterpret_cast<const uint8_t*>(lds + C::OFF_PSR);
+      const int t0 = 16 * bk;
+      // the block's psi bytes of this lane's states: 16 independent LDS reads, one wait
+      unsigned pr[16];
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int t = t0 + r < T ? t0 + r : T - 1;
+        const uint8_t* src = psr + (t & (C::PSR - 1)) * NP + NB * l;
+        pr[r] = NB == 2 ? (unsigned)*reinterpret_cast<const uint16_t*>(src) : *reinterpret_cast<const unsigned*>(src);
+      }
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int t = t0 + r;
+        if (t < T && t >= kPsiChunk) {  // (chunk 0 has no map)
+          unsigned nf = 0;
+          if ((t & (kPsiChunk - 1)) == 0) {
+            nf = pr[r];  // F at the chunk's first step is psi itself
+          } else {
+            // F_t[s] = F_{t-1}[psi_t[s]]: F_{t-1}[p] is byte p % NB of lane p / NB's register
+#pragma unroll
+            for (int j = 0; j < NB; ++j) {
+              const unsigned p = (pr[r] >> (8 * j)) & 0xffu;
+              const unsigned v = (unsigned)__builtin_amdgcn_ds_bpermute((int)((p / NB) * 4), (int)fr);
+              nf |= ((v >> (8 * (p % NB))) & 0xffu) << (8 * j);
+            }
+          }
+          fr = nf;
+          if ((t & (kPsiChunk - 1)) == kPsiChunk - 1 || t == T - 1) {
+            const int c = t >> 6;
+            uint8_t* gdst = a.G + ((size_t)b * a.nchunks + c) * NP + NB * l;
+            uint8_t* ldst = reinterpret_cast<uint8_t*>(lds + C::OFF_GMAP) + (c - 1) * NP + NB * l;
+            if constexpr (NB == 2) {
+              *reinterpret_cast<uint16_t*>(gdst) = (uint16_t)nf;
+              if (c - 1 < GMAP_CAP) *reinterpret_cast<uint16_t*>(ldst) = (uint16_t)nf;
+            } else {
+              *reinterpret_cast<uint32_t*>(gdst) = nf;
+              if (c - 1 < GMAP_CAP) *reinterpret_cast<uint32_t*>(ldst) = nf;
+            }
+          }
+        }
+      }
+    }
+  };
+  [[maybe_unused]] auto vit_tail = [&]() {
+    if constexpr (FUSE) {
+      // every psi row (global + LDS) and chunk map stored before the barriers that publish them
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      lds_barrier();  // the psi waves' last rows are in the LDS ring
+      if (composer) {
+        compose_block(nblocks - 2);
+        compose_block(nblocks - 1);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
+      lds_barrier();  // every chunk map is in G (and in LDS while they fit)
+      const int nc = a.nchunks;
+      constexpr int GB = 64;  // chunk maps staged per LDS batch (when they are not all in LDS)
+      uint8_t* gl = reinterpret_cast<uint8_t*>(lds);      // [GB][NP] (the chain's staging area: free now)
+      int* send = reinterpret_cast<int*>(gl + GB * NP);   // [nc] the state at each chunk's last step
+      if (w == 0 && !(a.vtail & 8)) {  // (vtail bit 3: diagnostic, no map walk)
+        const float* drow = lds + C::OFF_RING + ((T - 1) & (C::RING - 1)) * NP;
+        float bv = -INFINITY;
+        int bi = 0x7fffffff;
+#pragma unroll
+        for (int k = 0; k < NB; ++k) {
+          const int j = l + 64 * k;
+          if (j < N) argmax_combine(bv, bi, drow[j], j);
+        }
+        wave_argmax_dpp(bv, bi);
+        if (l == 0 && a.final_score) a.final_score[b] = bv;
+        int s = bi < N ? bi : 0;
+        if (l == 0) send[nc - 1] = s;
+        if (nc - 1 <= GMAP_CAP) {
+          const uint8_t* gm = reinterpret_cast<const uint8_t*>(lds + C::OFF_GMAP);
+          for (int c = nc - 1; c >= 1; --c) {
+            s = gm[(c - 1) * NP + s];
+            if (l == 0) send[c - 1] = s;
+          }
+        } else {
+          for (int chi = nc - 1; chi >= 1; chi -= GB) {
+            const int clo = chi - GB + 1 > 1 ? chi - GB + 1 : 1;
+            const int cnt = chi - clo + 1;
+            const unsigned* gsrc = reinterpret_cast<const unsigned*>(a.G + ((size_t)b * nc + clo) * NP);
+            for (int i0 = 0; i0 < cnt * NP / 4; i0 += 64 * 8) {  // 8 loads per lane in flight
+              unsigned v[8];
+#pragma unroll
+              for (int k = 0; k < 8; ++k) {
+                const int i = i0 + 64 * k + l;
+                v[k] = i < cnt * NP / 4 ? __hip_atomic_load(gsrc + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0u;
+              }
+#pragma unroll
+              for (int k = 0; k < 8; ++k) {
+                const int i = i0 + 64 * k + l;
+                if (i < cnt * NP / 4) reinterpret_cast<unsigned*>(gl)[i] = v[k];
+              }
+            }
+            for (int c = chi; c >= clo; --c) {
+              s = gl[(c - clo) * NP + s];
+              if (l == 0) send[c - 1] = s;
+            }
+          }
+        }
+      }
+      lds_barrier();
+      if (a.vtail & 4) return;  // (diagnostic: no expansion)
+      // expansion: live waves 0..7, 9..11, 13..15 (8 and 12 ended at the start) take whole
+      // chunks; a chunk is two groups of GR = 32 rows, walked from the top, the next group's
+      // psi rows loaded while the current one is walked
+      const int widx = w - (w > 8) - (w > 12);
+      constexpr int NAL = 14;
+      constexpr int RPV = 256 / NP;  // psi rows per VGPR (one row = NP bytes = NP/4 lanes)
+      constexpr int LPR = NP / 4;
+      constexpr int GR = 32;         // rows per register group
+      constexpr int NV = GR / RPV;
+      const uint8_t* pb = a.psi + (size_t)b * T * NP;
+      int64_t* sb = a.states + (size_t)b * T;
+      const int nitems = widx < nc ? 2 * ((nc - widx + NAL - 1) / NAL) : 0;
+      auto group = [&](int i, int& c, int& ghi, int& glo) {
+        c = widx + NAL * (i >> 1);
+        const int t_lo = c * kPsiChunk;
+        const int t_hi = (t_lo + kPsiChunk < T ? t_lo + kPsiChunk : T) - 1;
+        ghi = t_hi - GR * (i & 1);
+        glo = ghi - GR + 1 > t_lo ? ghi - GR + 1 : t_lo;
+      };
+      auto load = [&](int i, unsigned(&pv)[NV]) {
+        int c = 0, ghi = -1, glo = 0;
+        if (i < nitems) group(i, c, ghi, glo);
+#pragma unroll
+        for (int v = 0; v < NV; ++v) {
+          const int t = glo + v * RPV + l / LPR;
+          pv[v] = (i < nitems && t <= ghi)
+                      ? __hip_atomic_load(reinterpret_cast<const unsigned*>(pb + (size_t)t * NP) + (l % LPR),
+                                          __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                      : 0u;
+        }
+      };
+      int s = 0;
+      auto walk = [&](int i, const unsigned(&pv)[NV]) {
+        if (i >= nitems) return;
+        int c, ghi, glo;
+        group(i, c, ghi, glo);
+        if ((i & 1) == 0) s = send[c];
+        if (ghi < glo) return;  // (the lower group of a short last chunk)
+        int stv = 0;
+        static_for<0, GR>([&](auto KK) {
+          constexpr int k = GR - 1 - decltype(KK)::value;
+          if (glo + k <= ghi) {
+            const int su = __builtin_amdgcn_readfirstlane(s);  // (uniform: keeps it in an SGPR)
+            asm("v_writelane_b32 %0, %1, %2" : "+v"(stv) : "s"(su), "i"(k));
+            const unsigned word = __builtin_amdgcn_readlane(pv[k / RPV], (k % RPV) * LPR + (su >> 2));
+            s = (int)((word >> ((su & 3) * 8)) & 0xffu);
+          }
+        });
+        if (l < GR && glo + l <= ghi) sb[glo + l] = stv;
+      };
+      unsigned pa[NV], pq[NV];
+      load(0, pa);
+      for (int i = 0; i < nitems; i += 2) {
+        load(i + 1, pq);
+        walk(i, pa);
+        load(i + 2, pa);
+        walk(i + 1, pq);
+      }
+    }
+  };
+
   if (w == 0) {
     band_chain<NP, KIND, WP, TD0, TW>(a, lds, b, d);
+    if constexpr (FUSE) {
+      if (a.vtail) vit_tail();
+    }
   } else {
     // ---------------------------------------------------------------- helper waves
     // Fused psi (vit_psi_kernel's banded rule, psi_band_rows in viterbi.hip), on the
@@ -1357,8 +1560,15 @@ __device__ __forceinline__ void rec_band(const RecArgs& a, float* lds, int b, co
           }
           if (r < 16 && 16 * bk + r < T) {
             uint8_t* gdst = a.psi + ((size_t)b * T + t) * NP + NB * l;
-            if constexpr (NB == 2) *reinterpret_cast<uint16_t*>(gdst) = (uint16_t)pk;
-            else *reinterpret_cast<uint32_t*>(gdst) = pk;
+            // and the LDS ring of the last 64 rows, for the composer (fused decode)
+            uint8_t* ldst = reinterpret_cast<uint8_t*>(lds + C::OFF_PSR) + (t & (C::PSR - 1)) * NP + NB * l;
+            if constexpr (NB == 2) {
+              *reinterpret_cast<uint16_t*>(gdst) = (uint16_t)pk;
+              *reinterpret_cast<uint16_t*>(ldst) = (uint16_t)pk;
+            } else {
+              *reinterpret_cast<uint32_t*>(gdst) = pk;
+              *reinterpret_cast<uint32_t*>(ldst) = pk;
+            }
           }
         }
       }
@@ -1393,6 +1603,17 @@ __device__ __forceinline__ void rec_band(const RecArgs& a, float* lds, int b, co
         lds_barrier();  // the chain's last row
         psi_rows(nblocks - 2);
         psi_rows(nblocks - 1);
+        if (a.vtail) vit_tail();
+        return;
+      }
+      if (composer) {  // block kb - 3's psi rows were written during block kb - 1
+        for (int kb = 0; kb < nblocks; ++kb) {
+          compose_block(kb - 3);
+          if (!(kAbl & 16384)) lds_barrier();
+        }
+        lds_barrier();  // the chain's last row (block nblocks - 3's psi rows are in the ring)
+        compose_block(nblocks - 3);
+        vit_tail();
         return;
       }
     }
@@ -1417,6 +1638,9 @@ __device__ __forceinline__ void rec_band(const RecArgs& a, float* lds, int b, co
         if (KIND == kFbAlpha && a.loglik && vw == C::NW - 1 && l == 0)
           a.loglik[b] = (float)(base + (double)__logf(lds[C::OFF_SC + 64 * ((T - 1) & (C::RING - 1))]));
       }
+    }
+    if constexpr (FUSE) {
+      if (a.vtail) vit_tail();
     }
   }
 }
@@ -1456,6 +1680,15 @@ __device__ __forceinline__ void rec_dispatch(const RecArgs& a, float* lds, int b
     case 16 * 3 - 1 + 2: rec_band<NP, KIND, 2, -1, 3>(a, lds, b, a.band); break;
     case 16 * 3 + 0 + 2: rec_band<NP, KIND, 2, 0, 3>(a, lds, b, a.band); break;
     default:
+      if constexpr (KIND == kVit) {
+        // a fused-decode launch (vtail) on a plan that is not banded: the caller's hint
+        // (HMM355_VIT_PLAN_BANDED) was wrong.  No psi pass follows this kernel, so the path is
+        // marked invalid (states -1, final score NaN) instead of left stale.
+        if (a.vtail) {
+          for (int t = threadIdx.x; t < a.T; t += blockDim.x) a.states[(size_t)b * a.T + t] = -1;
+          if (threadIdx.x == 0 && a.final_score) a.final_score[b] = __builtin_nanf("");
+        }
+      }
       if (threadIdx.x >= RC<NP>::NT) return;  // (a wider Viterbi launch: waves beyond NW end here)
       // (diagnostic ablation bits: 1 << 25 the round-2 register-operand chain (NP <= 128),
       // 1 << 24 the DPP-broadcast chain)

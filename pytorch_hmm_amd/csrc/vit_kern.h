@@ -1,0 +1,232 @@
+// hmm355 — Viterbi kernels and their per-NP launcher (included by vit_np*.hip, one translation
+// unit per padded state count, so the three instantiations compile in parallel).
+#pragma once
+#include "recur.h"
+#include "post.h"
+
+namespace hmm355 {
+
+
+template <int NP>
+__global__ void __launch_bounds__(kVitNT<NP>) vit_fwd_kernel(RecArgs ra) {
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  rec_dispatch<NP, kVit>(ra, lds, blockIdx.x);
+}
+
+// psi rows of one chunk -> HBM, and the chunk map G[j] = state at t_lo - 1 given j at t_hi
+template <int NP>
+__device__ __forceinline__ void psi_write_rows(const VitArgs& a, uint8_t (*prow)[NP], int b, int chunk, int t_lo,
+                                               int t_hi) {
+  using C = VF<NP>;
+  const int tid = threadIdx.x;
+  const int T = a.T, N = a.N;
+  const int rows = t_hi - t_lo + 1;
+  uint8_t* pdst = a.psi + ((size_t)b * T + t_lo) * NP;
+  for (int idx = tid; idx < rows * NP / 16; idx += C::NT) {
+    const int row = idx / (NP / 16), c16 = (idx % (NP / 16)) * 16;
+    *reinterpret_cast<uint4*>(pdst + (size_t)row * NP + c16) = *reinterpret_cast<const uint4*>(&prow[row][c16]);
+  }
+  compose_chunk_map<NP>(a, prow, b, chunk, t_lo, t_hi);
+}
+
+// Banded psi rows (band.h): psi_t[o] = first argmax_i fl(delta_{t-1,i} + L[i][o]).  With
+// g_i = fl(delta_{t-1,i} + r_i), M = max_i g_i and i1 its first index, the maximum is
+// v = max(M, window values) and its first index is min({i1 if M == v} U {window i with
+// value == v}): an index outside the window has value g_i, and no g_j == M precedes i1;
+// i1 itself attains v whenever M == v (inside the window its value is >= g_i1 = M = v).
+template <int NP>
+__device__ __forceinline__ void psi_band_rows(const VitArgs& a, uint8_t (*prow)[NP], float* rowM, int* rowI,
+                                              float* drows, int b, int t_lo, int t_hi) {
+  using C = VF<NP>;
+  const BandDesc* __restrict__ d = a.band;
+  const int tid = threadIdx.x, w = tid >> 6, l = tid & 63;
+  const int T = a.T, N = a.N, W = d->wcp;
+  const int t_first = t_lo > 0 ? t_lo : 1;
+  const int rows = t_hi - t_first + 1;
+  // the chunk's delta rows t_first-1 .. t_hi-1, coalesced, into LDS (row stride NP)
+  const float* dsrc = a.delta + ((size_t)b * T + (t_first - 1)) * N;
+  if (N == NP && (reinterpret_cast<uintptr_t>(dsrc) & 15) == 0) {
+    // full rows: 16-B loads, no index division
+    const float4* s4 = reinterpret_cast<const float4*>(dsrc);
+    float4* d4 = reinterpret_cast<float4*>(drows);
+    for (int idx = tid; idx < rows * (NP / 4); idx += C::NT) d4[idx] = s4[idx];
+  } else {
+    for (int idx = tid; idx < rows * N; idx += C::NT) {
+      const int r = idx / N, c = idx - r * N;
+      drows[r * NP + c] = dsrc[idx];
+    }
+  }
+  __syncthreads();
+  float rf[C::NBLK];
+#pragma unroll
+  for (int blk = 0; blk < C::NBLK; ++blk) rf[blk] = d->rfl[64 * blk + l];
+  for (int r = w; r < rows; r += C::NW) {
+    float bv = -INFINITY;
+    int bi = 0x7fffffff;
+#pragma unroll
+    for (int blk = 0; blk < C::NBLK; ++blk) {
+      const int i = 64 * blk + l;
+      if (i < N) argmax_combine(bv, bi, drows[r * NP + i] + rf[blk], i);
+    }
+    wave_argmax_dpp(bv, bi);
+    if (l == 0) { rowM[r] = bv; rowI[r] = bi; }
+  }
+  // each thread keeps one output column o for all rows (NT is a multiple of NP)
+  static_assert(C::NT % NP == 0, "psi layout");
+  const int o = tid % NP;
+  const int lo = d->clo[o];
+  float wl[kBandMax];
+#pragma unroll
+  for (int k = 0; k < kBandMax; ++k) wl[k] = (k < W && lo + k < N) ? d->cL[o][k] : -INFINITY;
+  __syncthreads();
+  for (int r = tid / NP; r < rows; r += C::NT / NP) {
+    int arg = 0;
+    if (o < N) {
+      const float M = rowM[r];
+      float v = M;
+      float val[kBandMax];
+#pragma unroll
+      for (int k = 0; k < kBandMax; ++k) {
+        val[k] = (k < W && lo + k < N) ? drows[r * NP + lo + k] + wl[k] : -INFINITY;
+        v = fmaxf(v, val[k]);
+      }
+      arg = M == v ? rowI[r] : 0x7fffffff;
+#pragma unroll
+      for (int k = 0; k < kBandMax; ++k)
+        if (k < W && val[k] == v && lo + k < arg) arg = lo + k;
+    }
+    prow[t_first + r - t_lo][o] = (uint8_t)arg;
+  }
+}
+
+template <int NP>
+__global__ void __launch_bounds__(VF<NP>::NT) vit_psi_kernel(VitArgs a) {
+  using C = VF<NP>;
+  static_assert(kPsiChunk == kChunk, "chunk length shared with the fused banded chain");
+  __shared__ __attribute__((aligned(16))) uint8_t prow[kChunk][NP];
+  const int chunk = blockIdx.x, b = blockIdx.y;
+  const int tid = threadIdx.x;
+  if (kVitFused<NP> && a.band && a.band->wc <= kBandMax) {
+    // the banded chain's helpers wrote the psi rows (recur.h kVitFused): compose the map only
+    if (chunk == 0) return;
+    const int t_lo = chunk * kChunk;
+    const int t_hi = (t_lo + kChunk < a.T ? t_lo + kChunk : a.T) - 1;
+    const uint8_t* psrc = a.psi + ((size_t)b * a.T + t_lo) * NP;
+    for (int idx = tid; idx < (t_hi - t_lo + 1) * NP / 16; idx += C::NT)
+      *reinterpret_cast<uint4*>(&prow[0][0] + idx * 16) = *reinterpret_cast<const uint4*>(psrc + idx * 16);
+    __syncthreads();
+    compose_chunk_map<NP>(a, prow, b, chunk, t_lo, t_hi);
+    return;
+  }
+  const int w = tid >> 6, l = tid & 63, r = l >> 4, c = l & 15;
+  const int o = 16 * w + c;
+  const int T = a.T, N = a.N;
+  const int t_lo = chunk * kChunk;
+  const int t_hi = (t_lo + kChunk < T ? t_lo + kChunk : T) - 1;
+
+  float M[C::NBLK][16];
+#pragma unroll
+  for (int blk = 0; blk < C::NBLK; ++blk)
+#pragma unroll
+    for (int n = 0; n < 16; ++n) {
+      const int i = 64 * blk + 16 * r + n;
+      const bool ok = i < N && o < N;
+      const float v = a.log_P[ok ? (size_t)i * N + o : 0];
+      M[blk][n] = ok ? v : -INFINITY;
+    }
+  if (t_lo == 0 && tid < NP) prow[0][tid] = 0;  // psi_0 (hmm.py:156 zeros)
+  if (a.band && a.band->wc <= kBandMax) {
+    __shared__ float rowM[kChunk];
+    __shared__ int rowI[kChunk];
+    extern __shared__ __attribute__((aligned(16))) float drows[];  // [kChunk][NP] (dynamic)
+    psi_band_rows<NP>(a, prow, rowM, rowI, drows, b, t_lo, t_hi);
+    __syncthreads();
+    psi_write_rows<NP>(a, prow, b, chunk, t_lo, t_hi);
+    return;
+  }
+
+  const float* dbase = a.delta + (size_t)b * T * N;
+  auto load_row = [&](int t, float(&yv)[C::NBLK]) {
+#pragma unroll
+    for (int blk = 0; blk < C::NBLK; ++blk) {
+      const int i = 64 * blk + l;
+      const bool ok = i < N;
+      const float v = dbase[(size_t)(t - 1) * N + (ok ? i : 0)];
+      yv[blk] = ok ? v : -INFINITY;
+    }
+  };
+  const int t_first = t_lo > 0 ? t_lo : 1;
+  float ycur[C::NBLK], ynext[C::NBLK];
+  if (t_first <= t_hi) load_row(t_first, ycur);
+  for (int t = t_first; t <= t_hi; ++t) {
+    if (t + 1 <= t_hi) load_row(t + 1, ynext);
+    // lane-local scan in increasing i (i = 64*blk + 16r + n): strict > keeps the first
+    float bv = row_bcast<0>(ycur[0]) + M[0][0];
+    int bk = 0;  // local index 16*blk + n
+#pragma unroll
+    for (int blk = 0; blk < C::NBLK; ++blk) {
+#define PSI_STEP(n)                                                  \
+  if (blk != 0 || n != 0) {                                          \
+    const float s = row_bcast<n>(ycur[blk]) + M[blk][n];             \
+    const bool gt = s > bv;                                          \
+    bv = gt ? s : bv;                                                \
+    bk = gt ? 16 * blk + n : bk;                                     \
+  }
+      PSI_STEP(0) PSI_STEP(1) PSI_STEP(2) PSI_STEP(3) PSI_STEP(4) PSI_STEP(5) PSI_STEP(6) PSI_STEP(7)
+      PSI_STEP(8) PSI_STEP(9) PSI_STEP(10) PSI_STEP(11) PSI_STEP(12) PSI_STEP(13) PSI_STEP(14) PSI_STEP(15)
+#undef PSI_STEP
+    }
+    int bi = 64 * (bk >> 4) + 16 * r + (bk & 15);
+    // combine the four row groups: (value, index) lexicographic, ties -> smaller index
+    {
+      float va = bv, vb = bv;
+      int ia = bi, ib = bi;
+      permlane16_swap(va, vb);
+      permlane16_swap_i(ia, ib);
+      argmax_combine(va, ia, vb, ib);
+      float vc = va, vd = va;
+      int ic = ia, id = ia;
+      permlane32_swap(vc, vd);
+      permlane32_swap_i(ic, id);
+      argmax_combine(vc, ic, vd, id);
+      bi = ic;
+    }
+    if (r == 0) prow[t - t_lo][o] = (uint8_t)bi;
+#pragma unroll
+    for (int blk = 0; blk < C::NBLK; ++blk) ycur[blk] = ynext[blk];
+  }
+  __syncthreads();
+  psi_write_rows<NP>(a, prow, b, chunk, t_lo, t_hi);
+}
+
+template <int NP>
+hipError_t launch_vit(const VitArgs& va, bool prep, bool tail, hipStream_t sm) {
+  hipError_t e = allow_lds(vit_fwd_kernel<NP>, kExclusiveLds);  // own the CU (recur.h)
+  if (e != hipSuccess) return e;
+  if (va.band && prep) {
+    e = launch_band_prep(va.log_P, va.N, const_cast<BandDesc*>(va.band), sm);
+    if (e != hipSuccess) return e;
+  }
+  RecArgs ra{va.obs, va.log_P, va.init, va.delta, nullptr, nullptr, va.B, va.T, va.N, va.obs_mode, va.N, va.band,
+             nullptr, nullptr, va.psi};
+  if (tail) {  // the fused decode: chunk maps and backtrace inside the chain kernel (recur.h vtail)
+    ra.G = va.G;
+    ra.states = va.states;
+    ra.final_score = va.final_score;
+    ra.nchunks = va.nchunks;
+    ra.vtail = 1 | va.vdiag;
+  }
+  hipLaunchKernelGGL(vit_fwd_kernel<NP>, dim3(va.B), dim3(kVitNT<NP>), kExclusiveLds, sm, ra);
+  e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  if (tail) return hipSuccess;
+  // banded psi stages the chunk's delta rows in LDS (dynamic, kChunk x NP floats)
+  const size_t psi_lds = va.band ? (size_t)kChunk * NP * sizeof(float) : 0;
+  hipLaunchKernelGGL(vit_psi_kernel<NP>, dim3(va.nchunks, va.B), dim3(VF<NP>::NT), psi_lds, sm, va);
+  e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(vit_backtrace_kernel<NP>, dim3(va.nchunks, va.B), dim3(64), 0, sm, va);
+  return hipGetLastError();
+}
+
+}  // namespace hmm355

@@ -1,0 +1,6 @@
+// hmm355 — Viterbi kernels for NP = 64 (vit_kern.h; one translation unit per NP).
+#include "vit_kern.h"
+
+namespace hmm355 {
+template hipError_t launch_vit<64>(const VitArgs& va, bool prep, bool tail, hipStream_t sm);
+}  // namespace hmm355

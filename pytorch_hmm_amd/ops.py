@@ -27,6 +27,7 @@ OBS_PROB = nat.OBS_PROB
 OBS_LOG = nat.OBS_LOG
 FB_POSTERIOR = nat.FB_POSTERIOR
 FB_PAIR = nat.FB_PAIR
+VIT_PLAN_BANDED = nat.VIT_PLAN_BANDED
 FB_FORWARD = nat.FB_FORWARD
 FB_BACKWARD = nat.FB_BACKWARD
 
@@ -149,10 +150,14 @@ def viterbi(obs: Tensor, log_P: Tensor, init: Tensor, obs_mode: int,
     if B == 0:
         return states, delta, final
     ws = _workspace(L.hmm355_viterbi_workspace_bytes(B, T, N), dev)
+    # a banded plan: the chain kernel finishes the decode itself (one launch; HMM355_VIT_TAIL=0
+    # keeps the separate psi / backtrace kernels, for comparison)
+    flags = VIT_PLAN_BANDED if (plan is not None and getattr(plan, "_hmm355_banded", False)
+                                and os.environ.get("HMM355_VIT_TAIL", "1") != "0") else 0
     with torch.cuda.device(dev):
-        nat.check(L.hmm355_viterbi_plan_f32(
-            nat.ptr(obs), obs_mode, nat.ptr(log_P), nat.ptr(init), nat.ptr(plan), B, T, N, nat.ptr(states),
-            nat.ptr(delta), nat.ptr(final), nat.ptr(ws), ws.numel(), nat.stream_of(dev)))
+        nat.check(L.hmm355_viterbi_plan_ex_f32(
+            nat.ptr(obs), obs_mode, nat.ptr(log_P), nat.ptr(init), nat.ptr(plan), flags, B, T, N,
+            nat.ptr(states), nat.ptr(delta), nat.ptr(final), nat.ptr(ws), ws.numel(), nat.stream_of(dev)))
     return states, delta, final
 
 

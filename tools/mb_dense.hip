@@ -1,0 +1,437 @@
+// Diagnostic microbenchmark (not part of the product): the dense max-plus / sum-product chain
+// step of recur.h in several lane layouts, to pick the layout with the shortest step.
+//   NW waves, each lane owns KO outputs x KI inputs of the NP x NP matrix (registers);
+//   GI = NP / KI lanes (a DPP row or half row) reduce-scatter each output group.
+// One workgroup per sequence, T steps, the previous row read from an LDS exchange ring,
+// one s_barrier per step; every row is stored to global memory (checked on the host:
+// Viterbi bit-exact against a C loop, FB within 1e-5 relative).
+//   hipcc -O3 --offload-arch=gfx950 -std=c++17 tools/mb_dense.hip -o /tmp/mb_dense
+#include <hip/hip_runtime.h>
+#include <math.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include <vector>
+
+constexpr int NP = 128;
+constexpr int EROWS = 256;  // emission rows kept in LDS (step q uses row q % EROWS)
+
+#define CHECK(x)                                                                       \
+  do {                                                                                 \
+    hipError_t e_ = (x);                                                               \
+    if (e_ != hipSuccess) {                                                            \
+      fprintf(stderr, "%s:%d %s\n", __FILE__, __LINE__, hipGetErrorString(e_));        \
+      exit(1);                                                                         \
+    }                                                                                  \
+  } while (0)
+
+#define DPP_RED(name, op, ctrl)                                                                   \
+  __device__ __forceinline__ void name(float& dst, float src) {                                   \
+    asm("s_nop 1\n\t" op " %0, %1, %0 " ctrl " row_mask:0xf bank_mask:0xf" : "+v"(dst) : "v"(src)); \
+  }
+DPP_RED(max_mirror, "v_max_f32_dpp", "row_mirror")
+DPP_RED(max_hmirror, "v_max_f32_dpp", "row_half_mirror")
+DPP_RED(max_x3, "v_max_f32_dpp", "quad_perm:[3,2,1,0]")
+DPP_RED(max_x2, "v_max_f32_dpp", "quad_perm:[2,3,0,1]")
+DPP_RED(max_x1, "v_max_f32_dpp", "quad_perm:[1,0,3,2]")
+DPP_RED(add_mirror, "v_add_f32_dpp", "row_mirror")
+DPP_RED(add_hmirror, "v_add_f32_dpp", "row_half_mirror")
+DPP_RED(add_x3, "v_add_f32_dpp", "quad_perm:[3,2,1,0]")
+DPP_RED(add_x2, "v_add_f32_dpp", "quad_perm:[2,3,0,1]")
+DPP_RED(add_x1, "v_add_f32_dpp", "quad_perm:[1,0,3,2]")
+
+__device__ __forceinline__ void barrier_lds() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+template <typename T>
+__device__ __forceinline__ void keep(T& v) { asm volatile("" : "+v"(v)); }
+
+typedef float f2 __attribute__((ext_vector_type(2)));
+
+// slot permutation: slot k of lane gi holds output go*KO + (k ^ ysel(gi))
+template <int GI, int KO>
+__device__ __forceinline__ int ysel(int gi) {
+  if constexpr (GI == 16 && KO == 4) return gi >> 2;
+  if constexpr (GI == 16 && KO == 8) return gi >> 1;
+  if constexpr (GI == 16 && KO == 2) return gi >> 3;
+  if constexpr (GI == 8 && KO == 4) return (gi & 7) >> 1;
+  if constexpr (GI == 8 && KO == 2) return (gi & 7) >> 2;
+  return 0;
+}
+
+// reduce-scatter of the KO slot partials over the GI lanes: slot 0 ends with output
+// go*KO + ysel(gi) reduced over all GI lanes
+template <int GI, int KO, bool FB>
+__device__ __forceinline__ void reduce(float (&s)[KO]) {
+#define RED(kind, a, b) \
+  if constexpr (FB) add_##kind(a, b); else max_##kind(a, b);
+  if constexpr (GI == 16 && KO == 4) {
+    RED(mirror, s[0], s[3]); RED(mirror, s[1], s[2]);
+    RED(hmirror, s[0], s[1]);
+    RED(x3, s[0], s[0]); RED(x1, s[0], s[0]);
+  } else if constexpr (GI == 16 && KO == 8) {
+    RED(mirror, s[0], s[7]); RED(mirror, s[1], s[6]); RED(mirror, s[2], s[5]); RED(mirror, s[3], s[4]);
+    RED(hmirror, s[0], s[3]); RED(hmirror, s[1], s[2]);
+    RED(x2, s[0], s[1]);
+    RED(x1, s[0], s[0]);
+  } else if constexpr (GI == 16 && KO == 2) {
+    RED(mirror, s[0], s[1]);
+    RED(hmirror, s[0], s[0]);
+    RED(x1, s[0], s[0]); RED(x2, s[0], s[0]);
+  } else if constexpr (GI == 8 && KO == 4) {
+    RED(hmirror, s[0], s[3]); RED(hmirror, s[1], s[2]);
+    RED(x2, s[0], s[1]);
+    RED(x1, s[0], s[0]);
+  } else if constexpr (GI == 8 && KO == 2) {
+    RED(hmirror, s[0], s[1]);
+    RED(x1, s[0], s[0]); RED(x2, s[0], s[0]);
+  }
+#undef RED
+}
+
+template <int GI, int KO>
+__device__ __forceinline__ bool is_writer(int gi) {
+  if constexpr (GI == 16 && KO == 4) return (gi & 3) == 0;
+  if constexpr (GI == 16 && KO == 8) return (gi & 1) == 0;
+  if constexpr (GI == 16 && KO == 2) return (gi & 7) == 0;
+  if constexpr (GI == 8 && KO == 4) return (gi & 1) == 0;
+  if constexpr (GI == 8 && KO == 2) return (gi & 3) == 0;
+  return false;
+}
+
+// mat[i*NP + o]: Viterbi log A; FB: A (probabilities).  emis (EROWS, NP): Viterbi log-emission,
+// FB emission.  out (B, T, NP): every row.
+// ABL (timing only, results wrong): 1 no products, 2 no barrier, 4 no global store, 8 no reduction
+template <int NW, int KO, int KI, bool FB, int ABL = 0>
+__global__ void __launch_bounds__(NW * 64) chain(const float* mat, const float* emis, float* out, int T) {
+  constexpr int GI = NP / KI, GO = NP / KO, NM = KI / 4;
+  static_assert(GI * GO == NW * 64, "layout");
+  extern __shared__ float lds[];
+  float* ring = lds;              // [2][NP]
+  float* em = lds + 2 * NP;       // [EROWS][NP]
+  const int tid = threadIdx.x, b = blockIdx.x;
+  const int gi = tid % GI, go = tid / GI;
+  const int y = ysel<GI, KO>(gi);
+  const int o = go * KO + y;  // the output this lane finishes
+  f2 Mk[KO][NM][2];
+#pragma unroll
+  for (int k = 0; k < KO; ++k)
+#pragma unroll
+    for (int m = 0; m < NM; ++m)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int i = KI * gi + 4 * m + e, ok = go * KO + (k ^ y);
+        Mk[k][m][e >> 1][e & 1] = mat[i * NP + ok];
+      }
+  for (int i = tid; i < EROWS * NP; i += NW * 64) em[i] = emis[i];
+  const bool wr = is_writer<GI, KO>(gi);
+  __syncthreads();
+  float* ob = out + (size_t)b * T * NP;
+  if (wr) {
+    const float v0 = FB ? em[o] : em[o];
+    ring[o] = v0;
+    ob[o] = v0;
+  }
+  barrier_lds();
+  for (int q = 1; q < T; ++q) {
+    const float* src = ring + ((q - 1) & 1) * NP;
+    float eo = em[(q % EROWS) * NP + o];
+    f2 yin[NM][2];
+#pragma unroll
+    for (int m = 0; m < NM; ++m) {
+      const float4 v4 = *reinterpret_cast<const float4*>(src + KI * gi + 4 * m);
+      yin[m][0] = f2{v4.x, v4.y};
+      yin[m][1] = f2{v4.z, v4.w};
+    }
+    keep(eo);
+    float s[KO];
+    if constexpr (ABL & 1) {
+#pragma unroll
+      for (int k = 0; k < KO; ++k) s[k] = yin[0][0].x + yin[NM - 1][1].y;
+    } else if constexpr (FB) {
+      f2 acc[KO];
+#pragma unroll
+      for (int k = 0; k < KO; ++k) acc[k] = f2{0.f, 0.f};
+#pragma unroll
+      for (int m = 0; m < NM; ++m)
+#pragma unroll
+        for (int p = 0; p < 2; ++p)
+#pragma unroll
+          for (int k = 0; k < KO; ++k) acc[k] = __builtin_elementwise_fma(yin[m][p], Mk[k][m][p], acc[k]);
+#pragma unroll
+      for (int k = 0; k < KO; ++k) s[k] = acc[k].x + acc[k].y;
+    } else if constexpr (ABL & 16) {
+      // scheduled: the KO packed sums of one input pair first, then their max3 folds, so no
+      // max waits on the packed add just issued; the first pair initialises the maxima
+#pragma unroll
+      for (int m = 0; m < NM; ++m)
+#pragma unroll
+        for (int p = 0; p < 2; ++p) {
+          f2 t[KO];
+#pragma unroll
+          for (int k = 0; k < KO; ++k) t[k] = yin[m][p] + Mk[k][m][p];
+#pragma unroll
+          for (int k = 0; k < KO; ++k) {
+            if (m == 0 && p == 0) s[k] = fmaxf(t[k].x, t[k].y);
+            else s[k] = fmaxf(fmaxf(s[k], t[k].x), t[k].y);
+          }
+        }
+    } else {
+#pragma unroll
+      for (int k = 0; k < KO; ++k) s[k] = -INFINITY;
+#pragma unroll
+      for (int m = 0; m < NM; ++m)
+#pragma unroll
+        for (int p = 0; p < 2; ++p)
+#pragma unroll
+          for (int k = 0; k < KO; ++k) {
+            const f2 t = yin[m][p] + Mk[k][m][p];
+            s[k] = fmaxf(s[k], fmaxf(t.x, t.y));
+          }
+    }
+    if constexpr (!(ABL & 8)) reduce<GI, KO, FB>(s);
+    const float val = FB ? s[0] * eo : s[0] + eo;
+    if constexpr (ABL & 32) {
+      // every lane of an output's group holds the same value: all write it, no branch (and no
+      // per-step global store: the product flushes rows every 16 steps)
+      ring[(q & 1) * NP + o] = val;
+    } else if (wr) {
+      ring[(q & 1) * NP + o] = val;
+      if constexpr (!(ABL & 4)) ob[(size_t)q * NP + o] = val;
+    }
+    if constexpr (ABL & 2)
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    else
+      barrier_lds();
+  }
+}
+
+// Two sequences per workgroup, their steps interleaved: phase A computes sequence 0's step
+// while sequence 1's inputs (written before the barrier that opened the phase) are read ahead,
+// so each phase's LDS read latency hides behind the other sequence's compute.  Viterbi only.
+template <int NW, int KO, int KI, int NS>
+__global__ void __launch_bounds__(NW * 64) chain_multi(const float* mat, const float* emis, float* out, int T) {
+  constexpr int GI = NP / KI, GO = NP / KO, NM = KI / 4;
+  static_assert(GI * GO == NW * 64, "layout");
+  extern __shared__ float lds[];
+  float* ring = lds;                  // [NS][2][NP]
+  float* em = lds + NS * 2 * NP;      // [EROWS][NP]
+  const int tid = threadIdx.x, b0 = blockIdx.x * NS;
+  const int gi = tid % GI, go = tid / GI;
+  const int y = ysel<GI, KO>(gi);
+  const int o = go * KO + y;
+  f2 Mk[KO][NM][2];
+#pragma unroll
+  for (int k = 0; k < KO; ++k)
+#pragma unroll
+    for (int m = 0; m < NM; ++m)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int i = KI * gi + 4 * m + e, ok = go * KO + (k ^ y);
+        Mk[k][m][e >> 1][e & 1] = mat[i * NP + ok];
+      }
+  for (int i = tid; i < EROWS * NP; i += NW * 64) em[i] = emis[i];
+  __syncthreads();
+#pragma unroll
+  for (int sq = 0; sq < NS; ++sq) {
+    ring[(sq * 2) * NP + o] = em[o];
+    out[(size_t)(b0 + sq) * T * NP + o] = em[o];
+  }
+  barrier_lds();
+  f2 yin[NS][NM][2];
+  auto rd = [&](int sq, int q) {  // inputs of sequence sq's step q
+    const float* src = ring + (sq * 2 + ((q - 1) & 1)) * NP;
+#pragma unroll
+    for (int m = 0; m < NM; ++m) {
+      const float4 v4 = *reinterpret_cast<const float4*>(src + KI * gi + 4 * m);
+      yin[sq][m][0] = f2{v4.x, v4.y};
+      yin[sq][m][1] = f2{v4.z, v4.w};
+    }
+  };
+#pragma unroll
+  for (int sq = 0; sq < NS; ++sq) rd(sq, 1);
+  for (int q = 1; q < T; ++q) {
+#pragma unroll
+    for (int sq = 0; sq < NS; ++sq) {
+      const float eo = em[(q % EROWS) * NP + o];
+      float s[KO];
+#pragma unroll
+      for (int m = 0; m < NM; ++m)
+#pragma unroll
+        for (int p = 0; p < 2; ++p) {
+          f2 t[KO];
+#pragma unroll
+          for (int k = 0; k < KO; ++k) t[k] = yin[sq][m][p] + Mk[k][m][p];
+#pragma unroll
+          for (int k = 0; k < KO; ++k) s[k] = (m == 0 && p == 0) ? fmaxf(t[k].x, t[k].y) : fmaxf(fmaxf(s[k], t[k].x), t[k].y);
+        }
+      reduce<GI, KO, false>(s);
+      const float val = s[0] + eo;
+      ring[(sq * 2 + (q & 1)) * NP + o] = val;
+      if (is_writer<GI, KO>(gi)) out[((size_t)(b0 + sq) * T + q) * NP + o] = val;
+      barrier_lds();
+      // the next sequence's inputs for this step were published before this barrier's
+      // predecessor; this sequence's for step q+1 just now: read the one computed next
+      if (q + 1 < T || sq + 1 < NS) {
+        const int nsq = sq + 1 < NS ? sq + 1 : 0;
+        const int nq = sq + 1 < NS ? q : q + 1;
+        if (nsq == 0 || true) {}
+        rd(nsq, nq);
+      }
+    }
+  }
+}
+
+template <int NW, int KO, int KI, int NS>
+double run_multi(const char* name, int B, int T, const float* dmat, const float* demis, float* dout,
+                 const std::vector<float>& ref) {
+  auto k = chain_multi<NW, KO, KI, NS>;
+  CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(k), hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+  hipEvent_t e0, e1;
+  CHECK(hipEventCreate(&e0));
+  CHECK(hipEventCreate(&e1));
+  hipLaunchKernelGGL(k, dim3(B / NS), dim3(NW * 64), 160 * 1024, 0, dmat, demis, dout, T);
+  CHECK(hipDeviceSynchronize());
+  float best = 1e30f;
+  for (int r = 0; r < 5; ++r) {
+    CHECK(hipEventRecord(e0));
+    hipLaunchKernelGGL(k, dim3(B / NS), dim3(NW * 64), 160 * 1024, 0, dmat, demis, dout, T);
+    CHECK(hipEventRecord(e1));
+    CHECK(hipEventSynchronize(e1));
+    float ms;
+    CHECK(hipEventElapsedTime(&ms, e0, e1));
+    best = ms < best ? ms : best;
+  }
+  std::vector<float> got((size_t)B * T * NP);
+  CHECK(hipMemcpy(got.data(), dout, got.size() * 4, hipMemcpyDeviceToHost));
+  size_t bad = 0;
+  for (int b = 0; b < B; ++b)
+    for (size_t i = 0; i < (size_t)T * NP; ++i)
+      if (memcmp(&got[(size_t)b * T * NP + i], &ref[i], 4) != 0) ++bad;
+  printf("%-28s VIT  %.1f us  %.1f ns/step  (bit-exact: %zu bad)\n", name, best * 1e3, best * 1e6 / (T - 1), bad);
+  fflush(stdout);
+  return best;
+}
+
+template <int NW, int KO, int KI, bool FB, int ABL = 0>
+double run(const char* name, int B, int T, const float* dmat, const float* demis, float* dout,
+           const std::vector<float>& ref) {
+  auto k = chain<NW, KO, KI, FB, ABL>;
+  const size_t lds = (2 * NP + EROWS * NP) * 4;
+  CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(k), hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+  hipEvent_t e0, e1;
+  CHECK(hipEventCreate(&e0));
+  CHECK(hipEventCreate(&e1));
+  // 160 KiB per workgroup: one per CU, as the product's chains
+  hipLaunchKernelGGL(k, dim3(B), dim3(NW * 64), 160 * 1024, 0, dmat, demis, dout, T);
+  CHECK(hipDeviceSynchronize());
+  float best = 1e30f;
+  for (int r = 0; r < 5; ++r) {
+    CHECK(hipEventRecord(e0));
+    hipLaunchKernelGGL(k, dim3(B), dim3(NW * 64), 160 * 1024, 0, dmat, demis, dout, T);
+    CHECK(hipEventRecord(e1));
+    CHECK(hipEventSynchronize(e1));
+    float ms;
+    CHECK(hipEventElapsedTime(&ms, e0, e1));
+    best = ms < best ? ms : best;
+  }
+  (void)lds;
+  std::vector<float> got((size_t)B * T * NP);
+  CHECK(hipMemcpy(got.data(), dout, got.size() * 4, hipMemcpyDeviceToHost));
+  double maxrel = 0;
+  size_t bad = 0;
+  for (int b = 0; b < B; ++b)
+    for (size_t i = 0; i < (size_t)T * NP; ++i) {
+      const float g = got[(size_t)b * T * NP + i], r = ref[i];
+      if (FB) {
+        const double rel = fabs((double)g - r) / (fabs((double)r) + 1e-30);
+        if (rel > maxrel) maxrel = rel;
+        if (!(rel < 1e-4)) ++bad;
+      } else if (memcmp(&g, &r, 4) != 0) {
+        ++bad;
+      }
+    }
+  printf("%-28s %s  %.1f us  %.1f ns/step  (%s: %zu bad, max rel %.2e)\n", name, FB ? "FB " : "VIT", best * 1e3,
+         best * 1e6 / (T - 1), FB ? "rel 1e-4" : "bit-exact", bad, maxrel);
+  fflush(stdout);
+  return best;
+}
+
+int main(int argc, char** argv) {
+  const int B = argc > 1 ? atoi(argv[1]) : 32, T = argc > 2 ? atoi(argv[2]) : 2000;
+  std::vector<float> lmat(NP * NP), pmat(NP * NP), lem(EROWS * NP), pem(EROWS * NP);
+  srand(7);
+  for (int i = 0; i < NP; ++i) {
+    double rs = 0;
+    std::vector<double> row(NP);
+    for (int o = 0; o < NP; ++o) rs += row[o] = (rand() + 1.0) / RAND_MAX;
+    for (int o = 0; o < NP; ++o) {
+      pmat[i * NP + o] = (float)(row[o] / rs);
+      lmat[i * NP + o] = logf(pmat[i * NP + o] + 1e-8f);
+    }
+  }
+  for (int i = 0; i < EROWS * NP; ++i) {
+    lem[i] = logf((float)((rand() + 1.0) / RAND_MAX));
+    pem[i] = (float)(0.95 + 0.1 * rand() / RAND_MAX);  // FB: sums stay in fp32 range unscaled
+  }
+  // references: Viterbi exact (max is order-free, one add); FB in double, rescaled per step
+  std::vector<float> vref((size_t)T * NP), fref((size_t)T * NP);
+  for (int o = 0; o < NP; ++o) vref[o] = lem[o];
+  for (int q = 1; q < T; ++q)
+    for (int o = 0; o < NP; ++o) {
+      float m = -INFINITY;
+      for (int i = 0; i < NP; ++i) m = fmaxf(m, vref[(size_t)(q - 1) * NP + i] + lmat[i * NP + o]);
+      vref[(size_t)q * NP + o] = m + lem[(q % EROWS) * NP + o];
+    }
+  // FB: y_q = (y_{q-1} A) * e_q without rescaling (A row-stochastic, e in [0.95, 1.05])
+  std::vector<double> d((size_t)T * NP);
+  for (int o = 0; o < NP; ++o) d[o] = pem[o];
+  for (int q = 1; q < T; ++q)
+    for (int o = 0; o < NP; ++o) {
+      double s = 0;
+      for (int i = 0; i < NP; ++i) s += d[(size_t)(q - 1) * NP + i] * pmat[i * NP + o];
+      d[(size_t)q * NP + o] = s * pem[(q % EROWS) * NP + o];
+    }
+  for (size_t i = 0; i < d.size(); ++i) fref[i] = (float)d[i];
+  float *dl, *dp, *dle, *dpe, *dout;
+  CHECK(hipMalloc(&dl, NP * NP * 4));
+  CHECK(hipMalloc(&dp, NP * NP * 4));
+  CHECK(hipMalloc(&dle, EROWS * NP * 4));
+  CHECK(hipMalloc(&dpe, EROWS * NP * 4));
+  CHECK(hipMalloc(&dout, (size_t)B * T * NP * 4));
+  CHECK(hipMemcpy(dl, lmat.data(), NP * NP * 4, hipMemcpyHostToDevice));
+  CHECK(hipMemcpy(dp, pmat.data(), NP * NP * 4, hipMemcpyHostToDevice));
+  CHECK(hipMemcpy(dle, lem.data(), EROWS * NP * 4, hipMemcpyHostToDevice));
+  CHECK(hipMemcpy(dpe, pem.data(), EROWS * NP * 4, hipMemcpyHostToDevice));
+  run<8, 4, 8, false>("w8 ko4 ki8 (round 3)", B, T, dl, dle, dout, vref);
+  run<8, 4, 8, false, 16>("w8 ko4 ki8 scheduled", B, T, dl, dle, dout, vref);
+  run_multi<8, 4, 8, 2>("w8 ko4 ki8 two sequences", B, T, dl, dle, dout, vref);
+  run_multi<8, 4, 8, 3>("w8 ko4 ki8 three sequences", 33, T, dl, dle, dout, vref);
+  run_multi<4, 8, 8, 2>("w4 ko8 ki8 two sequences", B, T, dl, dle, dout, vref);
+  run_multi<16, 2, 8, 2>("w16 ko2 ki8 two sequences", B, T, dl, dle, dout, vref);
+  run<8, 4, 8, false, 48>("w8 ko4 ki8 sched+nobranch", B, T, dl, dle, dout, vref);
+  run<16, 2, 8, false, 48>("w16 ko2 ki8 sched+nobranch", B, T, dl, dle, dout, vref);
+  run<16, 2, 8, false, 16>("w16 ko2 ki8 scheduled", B, T, dl, dle, dout, vref);
+  run<8, 2, 16, false, 16>("w8 ko2 ki16 scheduled", B, T, dl, dle, dout, vref);
+  run<8, 4, 8, false, 1>("  abl: no products", B, T, dl, dle, dout, vref);
+  run<8, 4, 8, false, 2>("  abl: no barrier", B, T, dl, dle, dout, vref);
+  run<8, 4, 8, false, 4>("  abl: no global store", B, T, dl, dle, dout, vref);
+  run<8, 4, 8, false, 8>("  abl: no reduction", B, T, dl, dle, dout, vref);
+  run<8, 4, 8, false, 9>("  abl: no products/reduction", B, T, dl, dle, dout, vref);
+  run<8, 4, 8, false, 13>("  abl: only read+write+barrier", B, T, dl, dle, dout, vref);
+  run<8, 4, 8, false, 15>("  abl: only read+write", B, T, dl, dle, dout, vref);
+  run<4, 8, 8, false, 13>("  w4 abl: only read+write+barrier", B, T, dl, dle, dout, vref);
+  run<16, 2, 8, false, 13>("  w16 abl: only read+write+barrier", B, T, dl, dle, dout, vref);
+  run<4, 8, 8, false>("w4 ko8 ki8", B, T, dl, dle, dout, vref);
+  run<4, 4, 16, false>("w4 ko4 ki16", B, T, dl, dle, dout, vref);
+  run<8, 2, 16, false>("w8 ko2 ki16", B, T, dl, dle, dout, vref);
+  run<16, 2, 8, false>("w16 ko2 ki8", B, T, dl, dle, dout, vref);
+  const int TF = T;
+  run<8, 4, 8, true>("w8 ko4 ki8 (round 3)", B, TF, dp, dpe, dout, fref);
+  run<8, 4, 8, true, 32>("w8 ko4 ki8 nobranch", B, TF, dp, dpe, dout, fref);
+  run<8, 2, 16, true, 32>("w8 ko2 ki16 nobranch", B, TF, dp, dpe, dout, fref);
+  run<4, 8, 8, true>("w4 ko8 ki8", B, TF, dp, dpe, dout, fref);
+  run<4, 4, 16, true>("w4 ko4 ki16", B, TF, dp, dpe, dout, fref);
+  run<8, 2, 16, true>("w8 ko2 ki16", B, TF, dp, dpe, dout, fref);
+  run<16, 2, 8, true>("w16 ko2 ki8", B, TF, dp, dpe, dout, fref);
+  return 0;
+}
