@@ -282,7 +282,13 @@ def layer_workload(args, rank, world, dev):
         s_fb, s_vit = torch.cuda.Stream(dev), torch.cuda.Stream(dev)
         mask = ph.ops.FB_POSTERIOR | ph.ops.FB_FORWARD | ph.ops.FB_BACKWARD
 
+        split = os.environ.get("HMM355_TV_SPLIT", "") == "1" or only
+
         def step():
+            if not split:
+                # one call: the alpha and Viterbi recursions share one stream of log_A
+                # (tv_chain_av), beta beside them; the posterior, chunk-map and backtrace passes after
+                return ph.ops.tv_fb_viterbi(lo, lA, init, init, mask)
             cur = torch.cuda.current_stream(dev)
             s_fb.wait_stream(cur)
             s_vit.wait_stream(cur)
@@ -301,7 +307,8 @@ def layer_workload(args, rank, world, dev):
         # algorithmic bytes per frame: FB reads its step's matrix and emissions, writes
         # posterior/forward/backward; Viterbi reads matrix + emissions, writes delta + state
         dom, flops, bytes_ = "tv_pair", None, (8 * N * N + 24 * N + 8) * B * T
-        models = {"tv_fb": ("hbm", 2 * 4 * N * N + 4 * N), "tv_vit": ("hbm", 4 * N * N + 8 * N)}
+        models = {"tv_fb": ("hbm", 2 * 4 * N * N + 4 * N), "tv_vit": ("hbm", 4 * N * N + 8 * N),
+                  "tv_fbv": ("hbm", 2 * 4 * N * N + 12 * N)}
     elif wl == "smk":
         # SemiMarkovHMM.viterbi_decode (semi_markov.py:455-570) batched over the C5 shape
         # (the BASELINE C5 text names semi_markov.py): quad scorer + segment Viterbi + backtrace

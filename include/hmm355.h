@@ -257,6 +257,17 @@ int hmm355_tv_viterbi_f32(const float* log_obs, const float* log_A, long long a_
                           long long a_tstride, const float* init, int B, int T, int N,
                           int64_t* states, float* log_delta, void* workspace,
                           size_t workspace_bytes, void* stream);
+/* Forward-backward AND Viterbi of the same time-varying model (NeuralHMM.forward +
+ * viterbi_decode, neural.py:355-511) in one call: the alpha and Viterbi recursions run in one
+ * workgroup per sequence and read each step's matrix once (the two calls above read it three
+ * times in all).  Outputs and their bits as the two calls; no terminal vector (log_beta_T). */
+size_t hmm355_tv_fb_viterbi_workspace_bytes(int B, int T, int N);
+int hmm355_tv_fb_viterbi_f32(const float* log_obs, const float* log_A, long long a_bstride,
+                             long long a_tstride, const float* log_p0, const float* init, int B,
+                             int T, int N, unsigned out_mask, float* posterior, float* forward,
+                             float* backward, float* loglik, float* lik_ref, int64_t* states,
+                             float* log_delta, void* workspace, size_t workspace_bytes,
+                             void* stream);
 
 /* ---------------------------------------------------------------------------------
  * Explicit-duration (semi-Markov) HMM, indexed by segment END time.  Replace

@@ -28,6 +28,7 @@ EXPORTS = (
     "hmm355_hsmm_workspace_bytes", "hmm355_hsmm_viterbi_f32",
     "hmm355_tv_fb_workspace_bytes", "hmm355_tv_forward_backward_f32", "hmm355_tv_forward_backward_ex_f32",
     "hmm355_tv_viterbi_workspace_bytes", "hmm355_tv_viterbi_f32",
+    "hmm355_tv_fb_viterbi_workspace_bytes", "hmm355_tv_fb_viterbi_f32",
     "hmm355_semimarkov_workspace_bytes", "hmm355_semimarkov_quad_f32",
     "hmm355_semimarkov_viterbi_f32", "hmm355_semimarkov_forward_f32",
     "hmm355_stream_greedy_f32", "hmm355_stream_beam_f32",
@@ -78,6 +79,10 @@ def lib():
     L.hmm355_tv_forward_backward_ex_f32.restype = I
     L.hmm355_tv_viterbi_workspace_bytes.argtypes, L.hmm355_tv_viterbi_workspace_bytes.restype = [I, I, I], S
     L.hmm355_tv_viterbi_f32.argtypes = [P, P, LL, LL, P, I, I, I, P, P, P, S, P]
+    L.hmm355_tv_fb_viterbi_workspace_bytes.argtypes = [I, I, I]
+    L.hmm355_tv_fb_viterbi_workspace_bytes.restype = S
+    L.hmm355_tv_fb_viterbi_f32.argtypes = [P, P, LL, LL, P, P, I, I, I, U, P, P, P, P, P, P, P, P, S, P]
+    L.hmm355_tv_fb_viterbi_f32.restype = I
     L.hmm355_tv_viterbi_f32.restype = I
     L.hmm355_semimarkov_workspace_bytes.argtypes = [I, I, I, I]
     L.hmm355_semimarkov_workspace_bytes.restype = S

@@ -299,6 +299,47 @@ def _(log_obs, log_A, log_p0, out_mask):
     return mk(FB_POSTERIOR), mk(FB_FORWARD), mk(FB_BACKWARD), log_obs.new_empty(B), log_obs.new_empty(B)
 
 
+@torch.library.custom_op("hmm355::tv_fb_viterbi", mutates_args=())
+def tv_fb_viterbi(log_obs: Tensor, log_A: Tensor, log_p0: Tensor, init: Tensor,
+                  out_mask: int) -> Tuple[Tensor, Tensor, Tensor, Tensor, Tensor, Tensor, Tensor]:
+    """tv_forward_backward and tv_viterbi of the same model in one call
+    (hmm355_tv_fb_viterbi_f32): the alpha and Viterbi recursions share one stream of log_A.
+    Returns (posterior, forward, backward, loglik, lik_ref, states, log_delta)."""
+    nat.require_gpu(log_obs, log_A, log_p0, init)
+    log_obs, log_p0, init = _f32c(log_obs), _f32c(log_p0), _f32c(init)
+    B, T, N = log_obs.shape
+    dev = log_obs.device
+    L = nat.lib()
+    post = torch.empty((B, T, N) if out_mask & FB_POSTERIOR else _EMPTY, device=dev)
+    fwd = torch.empty((B, T, N) if out_mask & FB_FORWARD else _EMPTY, device=dev)
+    bwd = torch.empty((B, T, N) if out_mask & FB_BACKWARD else _EMPTY, device=dev)
+    loglik = torch.empty(B, device=dev)
+    lik_ref = torch.empty(B, device=dev)
+    states = torch.empty((B, T), dtype=torch.int64, device=dev)
+    delta = torch.empty((B, T, N), device=dev)
+    if B == 0:
+        return post, fwd, bwd, loglik, lik_ref, states, delta
+    A, sb, st = _tv_matrix(log_A, B, T, N)
+    ws = _workspace(L.hmm355_tv_fb_viterbi_workspace_bytes(B, T, N), dev)
+    with torch.cuda.device(dev):
+        nat.check(L.hmm355_tv_fb_viterbi_f32(
+            nat.ptr(log_obs), nat.ptr(A), sb, st, nat.ptr(log_p0), nat.ptr(init), B, T, N, out_mask,
+            nat.ptr(post) if out_mask & FB_POSTERIOR else None,
+            nat.ptr(fwd) if out_mask & FB_FORWARD else None,
+            nat.ptr(bwd) if out_mask & FB_BACKWARD else None,
+            nat.ptr(loglik), nat.ptr(lik_ref), nat.ptr(states), nat.ptr(delta), nat.ptr(ws), ws.numel(),
+            nat.stream_of(dev)))
+    return post, fwd, bwd, loglik, lik_ref, states, delta
+
+
+@tv_fb_viterbi.register_fake
+def _(log_obs, log_A, log_p0, init, out_mask):
+    B, T, N = log_obs.shape
+    mk = lambda bit: log_obs.new_empty((B, T, N) if out_mask & bit else _EMPTY)
+    return (mk(FB_POSTERIOR), mk(FB_FORWARD), mk(FB_BACKWARD), log_obs.new_empty(B), log_obs.new_empty(B),
+            log_obs.new_empty((B, T), dtype=torch.int64), log_obs.new_empty((B, T, N)))
+
+
 @torch.library.custom_op("hmm355::tv_viterbi", mutates_args=())
 def tv_viterbi(log_obs: Tensor, log_A: Tensor, init: Tensor) -> Tuple[Tensor, Tensor]:
     nat.require_gpu(log_obs, log_A, init)
