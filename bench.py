@@ -282,7 +282,10 @@ def layer_workload(args, rank, world, dev):
         s_fb, s_vit = torch.cuda.Stream(dev), torch.cuda.Stream(dev)
         mask = ph.ops.FB_POSTERIOR | ph.ops.FB_FORWARD | ph.ops.FB_BACKWARD
 
-        split = os.environ.get("HMM355_TV_SPLIT", "") == "1" or only
+        # HMM355_TV_FUSED=1: one call, alpha + Viterbi sharing one stream of log_A (tv_fbv):
+        # less HBM traffic but slower (its CU is compute-bound); the default is
+        # the two calls on two streams
+        split = os.environ.get("HMM355_TV_FUSED", "") != "1" or only
 
         def step():
             if not split:

@@ -495,9 +495,10 @@ __device__ __forceinline__ void hs_copy_lds(float* dst, const float* src, int n,
   }
 }
 
-// tables into LDS (the caller's barrier publishes them)
+// tables into LDS (the caller's barrier publishes them); copy = false: the pointers only (the
+// stitch copies the tables when it first has to walk itself, hs_walk_tables)
 template <int R>
-__device__ HsWalk hs_walk_init(const HsArgs& a, char* bsm, int b, int l) {
+__device__ HsWalk hs_walk_init(const HsArgs& a, char* bsm, int b, int l, bool copy = true) {
   HsWalk w;
   w.T = a.T;
   w.S = a.S;
@@ -511,9 +512,15 @@ __device__ HsWalk hs_walk_init(const HsArgs& a, char* bsm, int b, int l) {
   w.pcol = w.slt + a.S * a.S;
   w.rcol = w.pcol + R;
   w.rmc = w.rcol + 64 * a.Dm;
+  if (copy) {
+    hs_copy_lds(w.sdur, a.dur, a.S * a.Dm, l);
+    hs_copy_lds(w.slt, a.logT, a.S * a.S, l);
+  }
+  return w;
+}
+__device__ __forceinline__ void hs_walk_tables(const HsArgs& a, const HsWalk& w, int l) {
   hs_copy_lds(w.sdur, a.dur, a.S * a.Dm, l);
   hs_copy_lds(w.slt, a.logT, a.S * a.S, l);
-  return w;
 }
 
 // Walks from the segment (end t, state cs, duration cd, obs_sum o) towards t = 0, calling
@@ -772,7 +779,9 @@ __global__ void __launch_bounds__(64) hsmm_stitch_kernel(HsArgs a, HsChunks c) {
   extern __shared__ __attribute__((aligned(16))) char bsm[];
   const int b = blockIdx.x, l = threadIdx.x;
   const int T = a.T;
-  const HsWalk w = hs_walk_init<R>(a, bsm, b, l);
+  // the walker's tables are copied only if the stitch has to walk itself (records usually merge)
+  const HsWalk w = hs_walk_init<R>(a, bsm, b, l, false);
+  bool tables = false;
   // after the walker's tables: the first 64 records of the top kHsStage chunks, their counts
   int4* srec = reinterpret_cast<int4*>(bsm + align16(hsmm_walk_lds(a.S, a.Dm, R)));
   int* scnt = reinterpret_cast<int*>(srec + c.stage * 64);
@@ -835,6 +844,10 @@ __global__ void __launch_bounds__(64) hsmm_stitch_kernel(HsArgs a, HsChunks c) {
       bool below = false;
       const int4 e0 = l < n ? (lds ? srec[(ch - c0) * 64 + l] : recb[(size_t)ch * kHsCap + l])
                             : make_int4(-1, -1, -1, 0);
+      if (!tables) {  // (uniform: `at` comes from a ballot)
+        hs_walk_tables(a, w, l);
+        tables = true;
+      }
       hs_walk<R, SMAX>(w, l, t, cs, cd, o, lo, [&](int et, int es, int ed, float eo, int start) {
         ++serial;
         if (et < lo) {

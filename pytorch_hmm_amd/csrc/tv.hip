@@ -476,7 +476,9 @@ __device__ void tv_chain(const TvArgs& a, float* lds, int b) {
 template <int NP, bool VEC>
 __device__ void tv_chain_av(const TvArgs& fa, const TvArgs& va, float* lds, int b) {
   using G = TvGeo<NP>;
-  constexpr int PD = G::PD;
+  // one step fewer in flight than the single chains: the second recursion's registers (PD = 3
+  // at NP = 128 spilled 51 VGPRs)
+  constexpr int PD = G::PD > 4 ? 4 : (G::PD > 1 ? G::PD - 1 : 1);
   const int tid = threadIdx.x, w = tid >> 6, l = tid & 63;
   const int T = fa.T, N = fa.N;
   const int part = w / G::CB, r8 = l >> 3;
@@ -1261,7 +1263,12 @@ HMM355_API int hmm355_tv_fb_viterbi_f32(const float* log_obs, const float* log_A
   switch (NP) {
     case 64: e = launch_tv_fbv<64>(fa, fb, ta, pa, va, w, loglik, vec, st); break;
     case 128: e = launch_tv_fbv<128>(fa, fb, ta, pa, va, w, loglik, vec, st); break;
-    default: e = launch_tv_fbv<256>(fa, fb, ta, pa, va, w, loglik, vec, st); break;
+    default:
+      // NP = 256: the two recursions' registers do not fit one wave (76 VGPRs spilled), so the
+      // matrices are streamed by the separate chains, one after the other
+      e = launch_tv_fb<256>(fa, fb, pa, w, loglik, nullptr, vec, st);
+      if (e == hipSuccess) e = launch_tv_vit<256>(ta, va, vec, st);
+      break;
   }
   return e == hipSuccess ? HMM355_OK : (int)e;
 }

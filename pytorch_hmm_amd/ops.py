@@ -150,10 +150,12 @@ def viterbi(obs: Tensor, log_P: Tensor, init: Tensor, obs_mode: int,
     if B == 0:
         return states, delta, final
     ws = _workspace(L.hmm355_viterbi_workspace_bytes(B, T, N), dev)
-    # a banded plan: the chain kernel finishes the decode itself (one launch; HMM355_VIT_TAIL=0
-    # keeps the separate psi / backtrace kernels, for comparison)
+    # HMM355_VIT_TAIL=1 with a banded plan: the chain kernel finishes the decode itself (one
+    # launch instead of three).  Off by default: measured 10 us slower per op at the north-star
+    # shape (profiles/r4b_*), its composer and in-kernel backtrace cost more
+    # than the two launches they replace.
     flags = VIT_PLAN_BANDED if (plan is not None and getattr(plan, "_hmm355_banded", False)
-                                and os.environ.get("HMM355_VIT_TAIL", "1") != "0") else 0
+                                and os.environ.get("HMM355_VIT_TAIL", "0") == "1") else 0
     with torch.cuda.device(dev):
         nat.check(L.hmm355_viterbi_plan_ex_f32(
             nat.ptr(obs), obs_mode, nat.ptr(log_P), nat.ptr(init), nat.ptr(plan), flags, B, T, N,

@@ -5,7 +5,7 @@ mkdir -p gpurun_out
 timeout -k 10 400 python -u -m pytest -x -v --timeout 200 --timeout-method thread -m gpu \
   tests/test_gpu_vit_tail.py tests/test_gpu_fullsize.py tests/test_gpu_kernels.py -k "tail or fullsize or north or config3 or gmm" > gpurun_out/r4a_tests.log 2>&1 || { tail -30 gpurun_out/r4a_tests.log; exit 1; }
 tail -3 gpurun_out/r4a_tests.log
-timeout -k 10 200 python -u bench.py --steps 20 --warmup 3 --cpu-seconds 0 > gpurun_out/r4a_bench_tail.log 2>&1 || exit 1
+HMM355_VIT_TAIL=1 timeout -k 10 200 python -u bench.py --steps 20 --warmup 3 --cpu-seconds 0 > gpurun_out/r4a_bench_tail.log 2>&1 || exit 1
 HMM355_VIT_TAIL=0 timeout -k 10 200 python -u bench.py --steps 20 --warmup 3 --cpu-seconds 0 > gpurun_out/r4a_bench_notail.log 2>&1 || exit 1
 for f in gpurun_out/r4a_bench_tail.log gpurun_out/r4a_bench_notail.log; do
   python - "$f" <<'PY'

@@ -12,7 +12,7 @@ for l in open(sys.argv[1]):
 PY
 }
 HMM355_VIT_TAIL=0 run notail
-run full
-HMM355_VIT_TAIL_DIAG=2 run nocompose
-HMM355_VIT_TAIL_DIAG=12 run nowalk_noexpand
-HMM355_VIT_TAIL_DIAG=14 run none
+HMM355_VIT_TAIL=1 run full
+HMM355_VIT_TAIL=1 HMM355_VIT_TAIL_DIAG=2 run nocompose
+HMM355_VIT_TAIL=1 HMM355_VIT_TAIL_DIAG=12 run nowalk_noexpand
+HMM355_VIT_TAIL=1 HMM355_VIT_TAIL_DIAG=14 run none

@@ -404,23 +404,10 @@ int main(int argc, char** argv) {
   CHECK(hipMemcpy(dpe, pem.data(), EROWS * NP * 4, hipMemcpyHostToDevice));
   run<8, 4, 8, false>("w8 ko4 ki8 (round 3)", B, T, dl, dle, dout, vref);
   run<8, 4, 8, false, 16>("w8 ko4 ki8 scheduled", B, T, dl, dle, dout, vref);
-  run_multi<8, 4, 8, 2>("w8 ko4 ki8 two sequences", B, T, dl, dle, dout, vref);
-  run_multi<8, 4, 8, 3>("w8 ko4 ki8 three sequences", 33, T, dl, dle, dout, vref);
-  run_multi<4, 8, 8, 2>("w4 ko8 ki8 two sequences", B, T, dl, dle, dout, vref);
-  run_multi<16, 2, 8, 2>("w16 ko2 ki8 two sequences", B, T, dl, dle, dout, vref);
   run<8, 4, 8, false, 48>("w8 ko4 ki8 sched+nobranch", B, T, dl, dle, dout, vref);
   run<16, 2, 8, false, 48>("w16 ko2 ki8 sched+nobranch", B, T, dl, dle, dout, vref);
   run<16, 2, 8, false, 16>("w16 ko2 ki8 scheduled", B, T, dl, dle, dout, vref);
   run<8, 2, 16, false, 16>("w8 ko2 ki16 scheduled", B, T, dl, dle, dout, vref);
-  run<8, 4, 8, false, 1>("  abl: no products", B, T, dl, dle, dout, vref);
-  run<8, 4, 8, false, 2>("  abl: no barrier", B, T, dl, dle, dout, vref);
-  run<8, 4, 8, false, 4>("  abl: no global store", B, T, dl, dle, dout, vref);
-  run<8, 4, 8, false, 8>("  abl: no reduction", B, T, dl, dle, dout, vref);
-  run<8, 4, 8, false, 9>("  abl: no products/reduction", B, T, dl, dle, dout, vref);
-  run<8, 4, 8, false, 13>("  abl: only read+write+barrier", B, T, dl, dle, dout, vref);
-  run<8, 4, 8, false, 15>("  abl: only read+write", B, T, dl, dle, dout, vref);
-  run<4, 8, 8, false, 13>("  w4 abl: only read+write+barrier", B, T, dl, dle, dout, vref);
-  run<16, 2, 8, false, 13>("  w16 abl: only read+write+barrier", B, T, dl, dle, dout, vref);
   run<4, 8, 8, false>("w4 ko8 ki8", B, T, dl, dle, dout, vref);
   run<4, 4, 16, false>("w4 ko4 ki16", B, T, dl, dle, dout, vref);
   run<8, 2, 16, false>("w8 ko2 ki16", B, T, dl, dle, dout, vref);
