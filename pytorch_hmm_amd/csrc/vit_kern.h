@@ -145,55 +145,75 @@ __global__ void __launch_bounds__(VF<NP>::NT) vit_psi_kernel(VitArgs a) {
     return;
   }
 
+  // Dense rows.  Lane (r, c) of wave w scans the inputs i = 64*blk + 16*r + n (n = 0..15) of
+  // output o = 16*w + c: s_i = fl(delta_{t-1,i} + L[i][o]), delta_{t-1,i} broadcast from lane
+  // 16r + n of the row (one v_add_f32_dpp row_newbcast per candidate).  The first argmax
+  // (torch.max, hmm.py:164-168) in three exact passes: the maximum m over the lane's candidates
+  // and then over the four row groups (max is order-free); each lane's smallest i with s_i == m
+  // (a reverse equality scan, no value carried); the smallest such i over the row groups.  Rows
+  // stream through a three-deep register ring (loads three steps ahead, no register copies, so
+  // no VALU-write -> DPP-read padding).  i >= N or o >= N: L = -inf, so s = -inf (and the row
+  // value read for such lanes is a valid element of the row).
   const float* dbase = a.delta + (size_t)b * T * N;
   auto load_row = [&](int t, float(&yv)[C::NBLK]) {
+    const int tt = t <= t_hi ? t : t_hi;  // (ahead of the chunk end: a valid row, unused)
 #pragma unroll
     for (int blk = 0; blk < C::NBLK; ++blk) {
       const int i = 64 * blk + l;
-      const bool ok = i < N;
-      const float v = dbase[(size_t)(t - 1) * N + (ok ? i : 0)];
-      yv[blk] = ok ? v : -INFINITY;
+      yv[blk] = dbase[(size_t)(tt - 1) * N + (i < N ? i : 0)];
     }
   };
-  const int t_first = t_lo > 0 ? t_lo : 1;
-  float ycur[C::NBLK], ynext[C::NBLK];
-  if (t_first <= t_hi) load_row(t_first, ycur);
-  for (int t = t_first; t <= t_hi; ++t) {
-    if (t + 1 <= t_hi) load_row(t + 1, ynext);
-    // lane-local scan in increasing i (i = 64*blk + 16r + n): strict > keeps the first
-    float bv = row_bcast<0>(ycur[0]) + M[0][0];
-    int bk = 0;  // local index 16*blk + n
+  auto psi_row = [&](int t, const float(&yv)[C::NBLK]) {
+    float s[C::NBLK][16];
 #pragma unroll
     for (int blk = 0; blk < C::NBLK; ++blk) {
-#define PSI_STEP(n)                                                  \
-  if (blk != 0 || n != 0) {                                          \
-    const float s = row_bcast<n>(ycur[blk]) + M[blk][n];             \
-    const bool gt = s > bv;                                          \
-    bv = gt ? s : bv;                                                \
-    bk = gt ? 16 * blk + n : bk;                                     \
-  }
-      PSI_STEP(0) PSI_STEP(1) PSI_STEP(2) PSI_STEP(3) PSI_STEP(4) PSI_STEP(5) PSI_STEP(6) PSI_STEP(7)
-      PSI_STEP(8) PSI_STEP(9) PSI_STEP(10) PSI_STEP(11) PSI_STEP(12) PSI_STEP(13) PSI_STEP(14) PSI_STEP(15)
-#undef PSI_STEP
+#define PSI_ADD(n)                                                                      \
+  asm("v_add_f32_dpp %0, %1, %2 row_newbcast:" #n " row_mask:0xf bank_mask:0xf"         \
+      : "=v"(s[blk][n])                                                                 \
+      : "v"(yv[blk]), "v"(M[blk][n]));
+      PSI_ADD(0) PSI_ADD(1) PSI_ADD(2) PSI_ADD(3) PSI_ADD(4) PSI_ADD(5) PSI_ADD(6) PSI_ADD(7)
+      PSI_ADD(8) PSI_ADD(9) PSI_ADD(10) PSI_ADD(11) PSI_ADD(12) PSI_ADD(13) PSI_ADD(14) PSI_ADD(15)
+#undef PSI_ADD
     }
+    float m = fmaxf(s[0][0], s[0][1]);
+#pragma unroll
+    for (int blk = 0; blk < C::NBLK; ++blk)
+#pragma unroll
+      for (int n = (blk == 0 ? 2 : 0); n < 16; n += 2) m = fmaxf(fmaxf(m, s[blk][n]), s[blk][n + 1]);
+    m = rows_max(m);
+    int bk = 1 << 20;  // local index 16*blk + n of the first candidate equal to m (none: large)
+#pragma unroll
+    for (int blk = C::NBLK - 1; blk >= 0; --blk)
+#pragma unroll
+      for (int n = 15; n >= 0; --n) bk = s[blk][n] == m ? 16 * blk + n : bk;
     int bi = 64 * (bk >> 4) + 16 * r + (bk & 15);
-    // combine the four row groups: (value, index) lexicographic, ties -> smaller index
     {
-      float va = bv, vb = bv;
       int ia = bi, ib = bi;
-      permlane16_swap(va, vb);
       permlane16_swap_i(ia, ib);
-      argmax_combine(va, ia, vb, ib);
-      float vc = va, vd = va;
+      ia = ia < ib ? ia : ib;
       int ic = ia, id = ia;
-      permlane32_swap(vc, vd);
       permlane32_swap_i(ic, id);
-      argmax_combine(vc, ic, vd, id);
-      bi = ic;
+      bi = ic < id ? ic : id;
     }
     if (r == 0) prow[t - t_lo][o] = (uint8_t)bi;
-#pragma unroll
-    for (int blk = 0; blk < C::NBLK; ++blk) ycur[blk] = ynext[blk];
+  };
+  const int t_first = t_lo > 0 ? t_lo : 1;
+  if (t_first <= t_hi) {  // (T = 1: chunk 0 has psi_0 only)
+    float y0[C::NBLK], y1[C::NBLK], y2[C::NBLK];
+    load_row(t_first, y0);
+    load_row(t_first + 1, y1);
+    load_row(t_first + 2, y2);
+    int t = t_first;
+    for (; t + 2 <= t_hi; t += 3) {
+      psi_row(t, y0);
+      load_row(t + 3, y0);
+      psi_row(t + 1, y1);
+      load_row(t + 4, y1);
+      psi_row(t + 2, y2);
+      load_row(t + 5, y2);
+    }
+    if (t <= t_hi) psi_row(t, y0);
+    if (t + 1 <= t_hi) psi_row(t + 1, y1);
   }
   __syncthreads();
   psi_write_rows<NP>(a, prow, b, chunk, t_lo, t_hi);

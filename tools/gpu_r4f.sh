@@ -13,3 +13,9 @@ import json
 d=json.load(open("gpurun_out/prof_r4_random/summary.json"))
 for k,v in d["kernels"].items(): print(k, round(v["avg_us"],1))
 PY
+bash tools/gpu_prof.sh r4_c3 --workload c3 > gpurun_out/r4p_c3.log 2>&1 || { tail -5 gpurun_out/r4p_c3.log; exit 1; }
+python3 - <<'PY'
+import json
+d=json.load(open("gpurun_out/prof_r4_c3/summary.json"))
+for k,v in d["kernels"].items(): print(k, round(v["avg_us"],1))
+PY

@@ -101,13 +101,19 @@ __device__ __forceinline__ bool is_writer(int gi) {
 // mat[i*NP + o]: Viterbi log A; FB: A (probabilities).  emis (EROWS, NP): Viterbi log-emission,
 // FB emission.  out (B, T, NP): every row.
 // ABL (timing only, results wrong): 1 no products, 2 no barrier, 4 no global store, 8 no reduction
+// FB, as the product step (recur.h rec_run_rb): 64 the scale c = sum of the inputs reduced beside
+// the products, val = s * (rcp(c) * e), c stored by wave 0; 128 a 32-row ring flushed to global
+// memory every 16 steps (row store + exp(log x + ls) output) and the next 16 emission rows
+// loaded and staged (exp) into LDS, as rec_flush / rec_load / rec_stage
 template <int NW, int KO, int KI, bool FB, int ABL = 0>
 __global__ void __launch_bounds__(NW * 64) chain(const float* mat, const float* emis, float* out, int T) {
   constexpr int GI = NP / KI, GO = NP / KO, NM = KI / 4;
   static_assert(GI * GO == NW * 64, "layout");
   extern __shared__ float lds[];
-  float* ring = lds;              // [2][NP]
-  float* em = lds + 2 * NP;       // [EROWS][NP]
+  constexpr int RR = (ABL & 128) ? 32 : 2;  // ring rows
+  float* ring = lds;              // [RR][NP]
+  float* em = lds + RR * NP;      // [EROWS][NP]
+  float* scs = em + EROWS * NP;   // [32] scales (ABL 64)
   const int tid = threadIdx.x, b = blockIdx.x;
   const int gi = tid % GI, go = tid / GI;
   const int y = ysel<GI, KO>(gi);
@@ -133,8 +139,28 @@ __global__ void __launch_bounds__(NW * 64) chain(const float* mat, const float* 
   }
   barrier_lds();
   for (int q = 1; q < T; ++q) {
-    const float* src = ring + ((q - 1) & 1) * NP;
+    const float* src = ring + ((q - 1) & (RR - 1)) * NP;
     float eo = em[(q % EROWS) * NP + o];
+    if constexpr (ABL & 128) {
+      if ((q & 15) == 0 && q >= 32) {
+        // flush rows q-32 .. q-17 (4 floats per thread) + their exp(log x + ls) outputs
+        const int row = tid / (NP / 4), c4 = (tid % (NP / 4)) * 4;
+        const int qq = q - 32 + row;
+        const float4 v = *reinterpret_cast<const float4*>(ring + (qq & 31) * NP + c4);
+        float* dst = out + ((size_t)b * T + qq) * NP + c4;
+        *reinterpret_cast<float4*>(dst) = v;
+        const float ls = -0.01f * qq;
+        float ov[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+        for (int k = 0; k < 4; ++k) ov[k] = ls >= -110.f ? __expf(__logf(ov[k]) + ls) : 0.f;
+        *reinterpret_cast<float4*>(dst + (size_t)T * NP * 0 + 64) = make_float4(ov[0], ov[1], ov[2], ov[3]);
+        // next 16 emission rows: 4 per thread, exp, into LDS
+        const int er = (q + 16 + row) % EROWS;
+        const float4 g = *reinterpret_cast<const float4*>(emis + er * NP + c4);
+        *reinterpret_cast<float4*>(em + ((q + 32 + row) % EROWS) * NP + c4) =
+            make_float4(__expf(g.x - 1.f), __expf(g.y - 1.f), __expf(g.z - 1.f), __expf(g.w - 1.f));
+      }
+    }
     f2 yin[NM][2];
 #pragma unroll
     for (int m = 0; m < NM; ++m) {
@@ -144,21 +170,38 @@ __global__ void __launch_bounds__(NW * 64) chain(const float* mat, const float* 
     }
     keep(eo);
     float s[KO];
+    float cx = 1.f;
     if constexpr (ABL & 1) {
 #pragma unroll
       for (int k = 0; k < KO; ++k) s[k] = yin[0][0].x + yin[NM - 1][1].y;
     } else if constexpr (FB) {
       f2 acc[KO];
+      f2 ysum = f2{0.f, 0.f};
 #pragma unroll
       for (int k = 0; k < KO; ++k) acc[k] = f2{0.f, 0.f};
 #pragma unroll
       for (int m = 0; m < NM; ++m)
 #pragma unroll
-        for (int p = 0; p < 2; ++p)
+        for (int p = 0; p < 2; ++p) {
 #pragma unroll
           for (int k = 0; k < KO; ++k) acc[k] = __builtin_elementwise_fma(yin[m][p], Mk[k][m][p], acc[k]);
+          if constexpr (ABL & 64) ysum += yin[m][p];
+        }
 #pragma unroll
       for (int k = 0; k < KO; ++k) s[k] = acc[k].x + acc[k].y;
+      if constexpr (ABL & 64) {
+        static_assert(GI == 16 && KO == 4, "c reduction layout");
+        cx = ysum.x + ysum.y;
+        add_mirror(cx, cx);
+        add_mirror(s[0], s[3]);
+        add_mirror(s[1], s[2]);
+        add_hmirror(cx, cx);
+        add_hmirror(s[0], s[1]);
+        add_x3(cx, cx);
+        add_x3(s[0], s[0]);
+        add_x1(cx, cx);
+        add_x1(s[0], s[0]);
+      }
     } else if constexpr (ABL & 16) {
       // scheduled: the KO packed sums of one input pair first, then their max3 folds, so no
       // max waits on the packed add just issued; the first pair initialises the maxima
@@ -188,14 +231,19 @@ __global__ void __launch_bounds__(NW * 64) chain(const float* mat, const float* 
             s[k] = fmaxf(s[k], fmaxf(t.x, t.y));
           }
     }
-    if constexpr (!(ABL & 8)) reduce<GI, KO, FB>(s);
-    const float val = FB ? s[0] * eo : s[0] + eo;
+    if constexpr (!(ABL & 8) && !(FB && (ABL & 64))) reduce<GI, KO, FB>(s);
+    float val = FB ? s[0] * eo : s[0] + eo;
+    if constexpr (FB && (ABL & 64)) {
+      const float scale = __builtin_amdgcn_rcpf(cx);
+      if (tid < 64) scs[(q - 1) & 31] = cx;
+      val = s[0] * (scale * eo);
+    }
     if constexpr (ABL & 32) {
       // every lane of an output's group holds the same value: all write it, no branch (and no
       // per-step global store: the product flushes rows every 16 steps)
-      ring[(q & 1) * NP + o] = val;
+      ring[(q & (RR - 1)) * NP + o] = val;
     } else if (wr) {
-      ring[(q & 1) * NP + o] = val;
+      ring[(q & (RR - 1)) * NP + o] = val;
       if constexpr (!(ABL & 4)) ob[(size_t)q * NP + o] = val;
     }
     if constexpr (ABL & 2)
@@ -316,7 +364,7 @@ template <int NW, int KO, int KI, bool FB, int ABL = 0>
 double run(const char* name, int B, int T, const float* dmat, const float* demis, float* dout,
            const std::vector<float>& ref) {
   auto k = chain<NW, KO, KI, FB, ABL>;
-  const size_t lds = (2 * NP + EROWS * NP) * 4;
+  const size_t lds = (32 * NP + EROWS * NP + 32) * 4;
   CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(k), hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
   hipEvent_t e0, e1;
   CHECK(hipEventCreate(&e0));
@@ -402,23 +450,12 @@ int main(int argc, char** argv) {
   CHECK(hipMemcpy(dp, pmat.data(), NP * NP * 4, hipMemcpyHostToDevice));
   CHECK(hipMemcpy(dle, lem.data(), EROWS * NP * 4, hipMemcpyHostToDevice));
   CHECK(hipMemcpy(dpe, pem.data(), EROWS * NP * 4, hipMemcpyHostToDevice));
-  run<8, 4, 8, false>("w8 ko4 ki8 (round 3)", B, T, dl, dle, dout, vref);
-  run<8, 4, 8, false, 16>("w8 ko4 ki8 scheduled", B, T, dl, dle, dout, vref);
   run<8, 4, 8, false, 48>("w8 ko4 ki8 sched+nobranch", B, T, dl, dle, dout, vref);
-  run<16, 2, 8, false, 48>("w16 ko2 ki8 sched+nobranch", B, T, dl, dle, dout, vref);
-  run<16, 2, 8, false, 16>("w16 ko2 ki8 scheduled", B, T, dl, dle, dout, vref);
-  run<8, 2, 16, false, 16>("w8 ko2 ki16 scheduled", B, T, dl, dle, dout, vref);
-  run<4, 8, 8, false>("w4 ko8 ki8", B, T, dl, dle, dout, vref);
-  run<4, 4, 16, false>("w4 ko4 ki16", B, T, dl, dle, dout, vref);
-  run<8, 2, 16, false>("w8 ko2 ki16", B, T, dl, dle, dout, vref);
-  run<16, 2, 8, false>("w16 ko2 ki8", B, T, dl, dle, dout, vref);
+  run<8, 4, 8, false, 48 | 128>("  + flush/stage blocks", B, T, dl, dle, dout, vref);
   const int TF = T;
-  run<8, 4, 8, true>("w8 ko4 ki8 (round 3)", B, TF, dp, dpe, dout, fref);
   run<8, 4, 8, true, 32>("w8 ko4 ki8 nobranch", B, TF, dp, dpe, dout, fref);
-  run<8, 2, 16, true, 32>("w8 ko2 ki16 nobranch", B, TF, dp, dpe, dout, fref);
-  run<4, 8, 8, true>("w4 ko8 ki8", B, TF, dp, dpe, dout, fref);
-  run<4, 4, 16, true>("w4 ko4 ki16", B, TF, dp, dpe, dout, fref);
-  run<8, 2, 16, true>("w8 ko2 ki16", B, TF, dp, dpe, dout, fref);
-  run<16, 2, 8, true>("w16 ko2 ki8", B, TF, dp, dpe, dout, fref);
+  run<8, 4, 8, true, 32 | 64>("  + c reduction, rcp", B, TF, dp, dpe, dout, fref);
+  run<8, 4, 8, true, 32 | 128>("  + flush/stage blocks", B, TF, dp, dpe, dout, fref);
+  run<8, 4, 8, true, 32 | 64 | 128>("  + both (product step)", B, TF, dp, dpe, dout, fref);
   return 0;
 }
