@@ -39,21 +39,24 @@ constexpr int kGmmSub = 16;     // frames per LDS LSE tile
 // so D is bounded only by the workspace (frames * D * 8 bytes for the fp64 frame tiles)
 constexpr int kGmmDMax = 8192;
 
+// one block per component p < PP (PP: P padded to the scorers' component groups; the pad
+// components get w = mw = 0 and are never written out)
 __global__ void gmm_prep_kernel(const float* __restrict__ means, const float* __restrict__ log_vars,
                                 const float* __restrict__ log_w, double* __restrict__ pw,
-                                double* __restrict__ pmw, double* __restrict__ cst, int P, int D, int DP) {
+                                double* __restrict__ pmw, double* __restrict__ cst, int P, int PP, int D,
+                                int DP) {
   const int p = blockIdx.x;
-  if (p >= P) return;
+  if (p >= PP) return;
   for (int d = threadIdx.x; d < DP; d += blockDim.x) {
     double w = 0.0, mw = 0.0;
-    if (d < D) {
+    if (d < D && p < P) {
       w = exp(-0.5 * (double)log_vars[(size_t)p * D + d]);
       mw = -(double)means[(size_t)p * D + d] * w;
     }
-    pw[(size_t)d * P + p] = w;
-    pmw[(size_t)d * P + p] = mw;
+    pw[(size_t)d * PP + p] = w;
+    pmw[(size_t)d * PP + p] = mw;
   }
-  if (threadIdx.x == 0) {
+  if (threadIdx.x == 0 && p < P) {
     double s = 0.0;
     for (int d = 0; d < D; ++d) s += (double)log_vars[(size_t)p * D + d];
     cst[2 * p + 0] = s + (double)D * 1.8378770664093453;  // D*log(2*pi)
@@ -83,7 +86,7 @@ __global__ void __launch_bounds__(kGmmThreads) gmm_score_kernel(const double* __
                                                                const double* __restrict__ pmw,
                                                                const double* __restrict__ cst,
                                                                float* __restrict__ out, int nframes, int NDC,
-                                                               int S, int C, int mix_lse) {
+                                                               int S, int C, int PP, int mix_lse) {
   __shared__ double tile[kGmmSub][kGmmThreads];
   const int tid = threadIdx.x;
   const int nt = blockDim.x;        // 64..256: sized to S*C by the host (a lane per component)
@@ -128,8 +131,8 @@ __global__ void __launch_bounds__(kGmmThreads) gmm_score_kernel(const double* __
     double w[kGmmDc], mw[kGmmDc];
 #pragma unroll
     for (int k = 0; k < kGmmDc; ++k) {
-      w[k] = pw[(size_t)(dc * kGmmDc + k) * P + p];
-      mw[k] = pmw[(size_t)(dc * kGmmDc + k) * P + p];
+      w[k] = pw[(size_t)(dc * kGmmDc + k) * PP + p];
+      mw[k] = pmw[(size_t)(dc * kGmmDc + k) * PP + p];
     }
 #pragma unroll
     for (int f = 0; f < kGmmFrames; ++f) {
@@ -177,20 +180,222 @@ __global__ void __launch_bounds__(kGmmThreads) gmm_score_kernel(const double* __
   }
 }
 
+// ---- the scorer for C in {1, 2, 4} (every BASELINE layer: C = 4 at config 3, C = 1 for the
+// Gaussian and HSMM layers).
+//
+// gmm_score_kernel above reads one broadcast ds_read_b128 (2 dims of a frame) per 4 fp64 FMAs of
+// its one component per lane: 4 LDS cycles per 8 issue cycles per SIMD, so the CU's shared LDS
+// (4 SIMDs) is the bound at half the FMA rate (302 us at config 3 = 0.44 of fp64 peak).  Here a
+// lane owns 4 components (p = g0 + 4*cl + j) and 16 frames (64 fp64 accumulators): each
+// broadcast x read feeds 16 FMAs, and each component's parameters, read once per dim pair from
+// LDS, feed 16 frames.  Per dim pair and lane: 8 parameter reads + 16 x reads for 256 FMAs.
+// Frame groups (FG): the 64 lanes of a wave are FG groups of 64/FG component lanes, group fg
+// taking frames fg*16 .. fg*16+15 of the wave's block (small P: 64 components per wave at FG = 4).
+// The NW waves of a workgroup take consecutive frame blocks and share one staged copy of the
+// parameters.  The fp32 frames are converted to fp64 while staged (no separate pass).
+// Arithmetic per (frame, component): z = fma(x_d, w_d, mw_d), q = fma(z, z, q) for d = 0, 1, ...
+// in order, then the LSE over the state's components, exactly as gmm_score_kernel: same bits.
+constexpr int kG4Dc = 8;   // dims per staged chunk
+
+template <int FG, int NW, int kG4Nf>  // frame groups per wave, waves, frames per lane
+struct G4 {
+  static constexpr int CL = 64 / FG;            // component lanes per frame group
+  static constexpr int CG = 4 * CL;             // components per workgroup
+  static constexpr int FW = FG * kG4Nf;         // frames per wave
+  static constexpr int FT = NW * FW;            // frames per workgroup
+  static constexpr int NT = NW * 64;
+  // x tile row offset (doubles): 16-frame blocks padded by 2 doubles, so the FG groups' broadcast
+  // reads (one frame each) fall in different banks
+  static constexpr int NF = kG4Nf;
+  static constexpr int XROW = kG4Nf * kG4Dc + 2;
+  static constexpr int XS = (FT / kG4Nf) * XROW;
+  static constexpr int PS = 2 * kG4Dc * 2 * CL;   // double2 per parameter buffer: [array][dim][half][cl]
+  static constexpr int PV = (2 * kG4Dc * CG / 2 + NT - 1) / NT;  // double2 staged per thread
+  static constexpr int XV = (FT * kG4Dc + NT - 1) / NT;          // floats staged per thread
+};
+
+template <int FG, int NW, int kG4Nf>
+__global__ void __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(kG4Nf >= 16 ? 2 : 3))) gmm_score4_kernel(const float* __restrict__ x,
+                                                             const double* __restrict__ pw,
+                                                             const double* __restrict__ pmw,
+                                                             const double* __restrict__ cst,
+                                                             float* __restrict__ out, int nframes, int D,
+                                                             int NDC, int S, int C, int P, int PP,
+                                                             int mix_lse) {
+  using G = G4<FG, NW, kG4Nf>;
+  __shared__ double2 ps[2][G::PS];
+  __shared__ double xs[2][G::XS];
+  const int tid = threadIdx.x, w = tid >> 6, l = tid & 63;
+  const int fg = l / G::CL, cl = l % G::CL;
+  const int g0 = blockIdx.y * G::CG;
+  const size_t f0 = (size_t)blockIdx.x * G::FT;
+  const int fblk = w * FG + fg;  // this lane's 16-frame block in the tile
+
+  // staging registers: parameters (a = array, k = dim, c2 = component pair) and frames
+  double2 pre_p[G::PV];
+  float pre_x[G::XV];
+  auto fetch = [&](int dc) {
+#pragma unroll
+    for (int r = 0; r < G::PV; ++r) {
+      const int i = tid + r * G::NT;
+      const int a = i / (kG4Dc * G::CG / 2), rem = i % (kG4Dc * G::CG / 2);
+      const int k = rem / (G::CG / 2), c2 = rem % (G::CG / 2);
+      const double* src = a ? pmw : pw;
+      // PP (the padded stride) is a multiple of CG: every pair is in bounds and 16-B aligned
+      pre_p[r] = i < 2 * kG4Dc * G::CG / 2
+                     ? *reinterpret_cast<const double2*>(src + (size_t)(dc * kG4Dc + k) * PP + g0 + 2 * c2)
+                     : make_double2(0.0, 0.0);
+    }
+#pragma unroll
+    for (int r = 0; r < G::XV; ++r) {
+      const int i = tid + r * G::NT;
+      const int f = i / kG4Dc, k = i % kG4Dc;
+      const size_t frame = f0 + f;
+      const int d = dc * kG4Dc + k;
+      pre_x[r] = (i < G::FT * kG4Dc && frame < (size_t)nframes && d < D) ? x[frame * D + d] : 0.f;
+    }
+  };
+  auto stage = [&](int buf) {
+#pragma unroll
+    for (int r = 0; r < G::PV; ++r) {
+      const int i = tid + r * G::NT;
+      if (i < 2 * kG4Dc * G::CG / 2) {
+        const int a = i / (kG4Dc * G::CG / 2), rem = i % (kG4Dc * G::CG / 2);
+        const int k = rem / (G::CG / 2), c2 = rem % (G::CG / 2);
+        ps[buf][((a * kG4Dc + k) * 2 + (c2 & 1)) * G::CL + (c2 >> 1)] = pre_p[r];
+      }
+    }
+#pragma unroll
+    for (int r = 0; r < G::XV; ++r) {
+      const int i = tid + r * G::NT;
+      if (i < G::FT * kG4Dc) {
+        const int f = i / kG4Dc, k = i % kG4Dc;
+        xs[buf][(f / kG4Nf) * G::XROW + (f % kG4Nf) * kG4Dc + k] = (double)pre_x[r];
+      }
+    }
+  };
+
+  double q[4][kG4Nf];
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+#pragma unroll
+    for (int f = 0; f < kG4Nf; ++f) q[j][f] = 0.0;
+
+  fetch(0);
+  stage(0);
+  __syncthreads();
+  for (int dc = 0; dc < NDC; ++dc) {
+    const int buf = dc & 1;
+    if (dc + 1 < NDC) fetch(dc + 1);
+    const double2* pb = ps[buf];
+    const double* xb = xs[buf] + fblk * G::XROW;
+#pragma unroll 1
+    for (int kp = 0; kp < kG4Dc / 2; ++kp) {  // (not unrolled: each pair's 16 parameters stay live alone)
+      double wv[2][4], mv[2][4];
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          const double2 a = pb[((0 * kG4Dc + 2 * kp + kk) * 2 + h) * G::CL + cl];
+          const double2 b = pb[((1 * kG4Dc + 2 * kp + kk) * 2 + h) * G::CL + cl];
+          wv[kk][2 * h] = a.x; wv[kk][2 * h + 1] = a.y;
+          mv[kk][2 * h] = b.x; mv[kk][2 * h + 1] = b.y;
+        }
+#pragma unroll
+      for (int f = 0; f < kG4Nf; ++f) {
+        const double2 xv = *reinterpret_cast<const double2*>(xb + f * kG4Dc + 2 * kp);  // broadcast per group
+#pragma unroll
+        for (int kk = 0; kk < 2; ++kk) {
+          const double xd = kk ? xv.y : xv.x;
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const double z = fma(xd, wv[kk][j], mv[kk][j]);
+            q[j][f] = fma(z, z, q[j][f]);
+          }
+        }
+      }
+    }
+    if (dc + 1 < NDC) {
+      stage(buf ^ 1);  // the other buffer: its last readers passed the barrier that ended chunk dc - 1
+      __syncthreads();
+    }
+  }
+
+  // scores, then the LSE over each state's components (lane-local: C divides 4)
+  const size_t fbase = f0 + (size_t)fblk * kG4Nf;
+  const int pl = g0 + 4 * cl;  // first component of this lane
+  double kp4[4], lw4[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int p = pl + j < P ? pl + j : 0;
+    kp4[j] = cst[2 * p];
+    lw4[j] = cst[2 * p + 1];
+  }
+#pragma unroll
+  for (int f = 0; f < kG4Nf; ++f) {
+    const size_t frame = fbase + f;
+    if (frame >= (size_t)nframes) break;
+    double v[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) v[j] = -0.5 * (q[j][f] + kp4[j]) + lw4[j];
+    for (int j0 = 0; j0 < 4; j0 += C) {
+      const int p0 = pl + j0;
+      if (p0 >= P) break;
+      double r;
+      if (!mix_lse) {
+        r = v[j0];
+      } else {
+        double m = -INFINITY;
+        for (int cc = 0; cc < C; ++cc) m = fmax(m, v[j0 + cc]);
+        if (isinf(m)) m = 0.0;  // mixture_gaussian.py:144
+        float e = 0.f;
+        for (int cc = 0; cc < C; ++cc) e += expf((float)(v[j0 + cc] - m));
+        r = (double)logf(fmaxf(e, 1e-8f)) + m;  // :149-153
+      }
+      out[frame * S + p0 / C] = (float)r;
+    }
+  }
+}
+
+template <int FG, int NW, int NF>
+static hipError_t launch_g4(const float* x, const double* pw, const double* pmw, const double* cst, float* out,
+                            int nframes, int D, int NDC, int S, int C, int P, int PP, int mix_lse, hipStream_t st) {
+  using G = G4<FG, NW, NF>;
+  dim3 grid((unsigned)(((size_t)nframes + G::FT - 1) / G::FT), (unsigned)((P + G::CG - 1) / G::CG));
+  hipLaunchKernelGGL((gmm_score4_kernel<FG, NW, NF>), grid, dim3(G::NT), 0, st, x, pw, pmw, cst, out, nframes, D, NDC,
+                     S, C, P, PP, mix_lse);
+  return hipGetLastError();
+}
+
 struct GmmWs {
   double *pw, *pmw, *cst, *xt;
 };
+// the v2 scorer (gmm_score4_kernel) serves C in {1, 2, 4}; others take gmm_score_kernel
+static bool gmm_v2(int C) { return C == 1 || C == 2 || C == 4; }
+// components per v2 workgroup for P components (G4<FG, NW>::CG of the launch below)
+static int gmm_v2_group(size_t P) { return P > 128 ? 256 : (P > 64 ? 128 : 64); }
+// the configuration index of HMM355_GMM_CFG (diagnostic; -1 = default) and whether the first
+// scorer runs (it needs the fp64 frame tiles in the workspace: the size query and the launch
+// read the same variable)
+static int gmm_cfg() {
+  const char* ev = getenv("HMM355_GMM_CFG");
+  return ev ? atoi(ev) : -1;
+}
+static bool gmm_use_v1(int C) { return !gmm_v2(C) || gmm_cfg() == 0; }
 static size_t gmm_ws_layout(int B, int T, int D, int S, int C, char* base, GmmWs* w) {
   const size_t P = (size_t)S * C;
+  const size_t CG = gmm_v2_group(P);
+  const size_t PP = (P + CG - 1) / CG * CG;  // padded stride of the [d][PP] parameter tables
   const size_t NDC = (D + kGmmDc - 1) / kGmmDc, DP = NDC * kGmmDc;
   const size_t nframes = (size_t)B * T;
   const size_t ntiles = (nframes + kGmmFrames - 1) / kGmmFrames;
   size_t off = 0;
   auto take = [&](size_t bytes) { const size_t o = off; off += align_up(bytes, 256); return o; };
-  const size_t ow = take(P * DP * sizeof(double));
-  const size_t om = take(P * DP * sizeof(double));
+  const size_t ow = take(PP * DP * sizeof(double));
+  const size_t om = take(PP * DP * sizeof(double));
   const size_t oc = take(P * 2 * sizeof(double));
-  const size_t ox = take(ntiles * NDC * kGmmFrames * kGmmDc * sizeof(double));
+  // fp64 frame tiles: the first scorer only (v2 converts while staging)
+  const size_t ox = take(gmm_use_v1(C) ? ntiles * NDC * kGmmFrames * kGmmDc * sizeof(double) : 0);
   if (w && base) {
     w->pw = reinterpret_cast<double*>(base + ow);
     w->pmw = reinterpret_cast<double*>(base + om);
@@ -223,13 +428,28 @@ HMM355_API int hmm355_gmm_diag_logprob_f32(const float* x, const float* means, c
   gmm_ws_layout(B, T, D, S, C, static_cast<char*>(workspace), &w);
   const int NDC = (D + kGmmDc - 1) / kGmmDc, DP = NDC * kGmmDc;
   const int P = S * C;
+  const int CG = gmm_v2_group(P), PP = (P + CG - 1) / CG * CG;
   const int nframes = B * T;
   const size_t ntiles = ((size_t)nframes + kGmmFrames - 1) / kGmmFrames;
   hipStream_t st = static_cast<hipStream_t>(stream);
-  hipLaunchKernelGGL(gmm_prep_kernel, dim3(P), dim3(64), 0, st, means, log_vars, log_w, w.pw, w.pmw, w.cst, P, D,
-                     DP);
+  hipLaunchKernelGGL(gmm_prep_kernel, dim3(PP), dim3(64), 0, st, means, log_vars, log_w, w.pw, w.pmw, w.cst, P, PP,
+                     D, DP);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return (int)e;
+  const int cfg = gmm_cfg();  // diagnostic: 0 = the first scorer, 1.. = v2 shapes
+  if (!gmm_use_v1(C)) {
+    static_assert(G4<1, 4, 16>::CG == 256 && G4<2, 2, 16>::CG == 128 && G4<4, 2, 16>::CG == 64, "gmm_v2_group");
+#define G4L(fg, nw, nf) launch_g4<fg, nw, nf>(x, w.pw, w.pmw, w.cst, out, nframes, D, NDC, S, C, P, PP, mix_lse, st)
+    if (CG == 256) {
+      e = cfg == 2 ? G4L(1, 4, 8) : cfg == 3 ? G4L(1, 2, 16) : cfg == 4 ? G4L(1, 1, 16) : G4L(1, 4, 16);
+    } else if (CG == 128) {
+      e = cfg == 2 ? G4L(2, 2, 8) : cfg == 3 ? G4L(2, 1, 8) : G4L(2, 2, 16);
+    } else {
+      e = cfg == 2 ? G4L(4, 2, 8) : cfg == 3 ? G4L(4, 1, 4) : cfg == 4 ? G4L(4, 2, 4) : G4L(4, 2, 16);
+    }
+#undef G4L
+    return e == hipSuccess ? HMM355_OK : (int)e;
+  }
   const size_t total = ntiles * NDC * kGmmFrames * kGmmDc;
   size_t blocks = (total + 255) / 256;
   blocks = blocks < 8192 ? blocks : 8192;
@@ -242,7 +462,7 @@ HMM355_API int hmm355_gmm_diag_logprob_f32(const float* x, const float* means, c
   const int spb = nt / C;
   dim3 grid((unsigned)ntiles, (S + spb - 1) / spb);
   hipLaunchKernelGGL(gmm_score_kernel, grid, dim3(nt), 0, st, w.xt, w.pw, w.pmw, w.cst, out, nframes, NDC,
-                     S, C, mix_lse);
+                     S, C, PP, mix_lse);
   e = hipGetLastError();
   return e == hipSuccess ? HMM355_OK : (int)e;
 }

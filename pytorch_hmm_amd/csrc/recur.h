@@ -127,6 +127,45 @@ HMM355_DPP_RED(red_max_q3210, "v_max_f32_dpp", "quad_perm:[3,2,1,0]")
 HMM355_DPP_RED(red_max_q1032, "v_max_f32_dpp", "quad_perm:[1,0,3,2]")
 #undef HMM355_DPP_RED
 
+// The reduce-scatter of the four output partials of rec_run_rb over the 16 lanes of a row
+// (mirror, half mirror, two quad permutations: slot 0 of every lane of quad x ends with output
+// 4g + x), written as one block with only the wait states the DPP-read hazard needs (a DPP
+// source written by one of the two previous VALU instructions: 2 wait states).  The separate
+// helpers above pad every DPP op with "s_nop 1"; here the forward-backward form interleaves the
+// all-reduce of the scale c with the outputs' tree, so most reads are two instructions away
+// from their writes (tools/mb_dense.hip: 297 -> 279 ns per FB step).  Same operations in the same
+// order as the helpers: identical bits.
+__device__ __forceinline__ void red4_add_with_c(float& s0, float& s1, float s2, float s3, float& c) {
+  asm("s_nop 1\n\t"
+      "v_add_f32_dpp %2, %2, %2 row_mirror row_mask:0xf bank_mask:0xf\n\t"
+      "v_add_f32_dpp %0, %3, %0 row_mirror row_mask:0xf bank_mask:0xf\n\t"
+      "v_add_f32_dpp %1, %4, %1 row_mirror row_mask:0xf bank_mask:0xf\n\t"
+      "v_add_f32_dpp %2, %2, %2 row_half_mirror row_mask:0xf bank_mask:0xf\n\t"
+      "s_nop 0\n\t"
+      "v_add_f32_dpp %0, %1, %0 row_half_mirror row_mask:0xf bank_mask:0xf\n\t"
+      "v_add_f32_dpp %2, %2, %2 quad_perm:[3,2,1,0] row_mask:0xf bank_mask:0xf\n\t"
+      "s_nop 0\n\t"
+      "v_add_f32_dpp %0, %0, %0 quad_perm:[3,2,1,0] row_mask:0xf bank_mask:0xf\n\t"
+      "v_add_f32_dpp %2, %2, %2 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n\t"
+      "s_nop 0\n\t"
+      "v_add_f32_dpp %0, %0, %0 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf"
+      : "+v"(s0), "+v"(s1), "+v"(c)
+      : "v"(s3), "v"(s2));
+}
+__device__ __forceinline__ void red4_max(float& s0, float& s1, float s2, float s3) {
+  asm("s_nop 1\n\t"
+      "v_max_f32_dpp %0, %2, %0 row_mirror row_mask:0xf bank_mask:0xf\n\t"
+      "v_max_f32_dpp %1, %3, %1 row_mirror row_mask:0xf bank_mask:0xf\n\t"
+      "s_nop 0\n\t"
+      "v_max_f32_dpp %0, %1, %0 row_half_mirror row_mask:0xf bank_mask:0xf\n\t"
+      "s_nop 1\n\t"
+      "v_max_f32_dpp %0, %0, %0 quad_perm:[3,2,1,0] row_mask:0xf bank_mask:0xf\n\t"
+      "s_nop 1\n\t"
+      "v_max_f32_dpp %0, %0, %0 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf"
+      : "+v"(s0), "+v"(s1)
+      : "v"(s3), "v"(s2));
+}
+
 // Window term of slot offset DD in {-1, +1} for state vector v (state 64*blk + lane), weights
 // w: Viterbi -> t = v(s + DD) + w (neutral -inf past the ends); FB -> acc += v(s + DD) * w.
 template <int NB, bool FB, int DD>
@@ -915,15 +954,7 @@ __device__ __forceinline__ void rec_run_rb(const RecArgs& a, float* lds, int b) 
         s0 = acc[0].x + acc[0].y; s1 = acc[1].x + acc[1].y;
         s2 = acc[2].x + acc[2].y; s3 = acc[3].x + acc[3].y;
         // the two reductions interleaved (issue is in order within a wave)
-        red_add_mirror(cx, cx);
-        red_add_mirror(s0, s3);
-        red_add_mirror(s1, s2);
-        red_add_hmirror(cx, cx);
-        red_add_hmirror(s0, s1);
-        red_add_q3210(cx, cx);
-        red_add_q3210(s0, s0);
-        red_add_q1032(cx, cx);
-        red_add_q1032(s0, s0);
+        red4_add_with_c(s0, s1, s2, s3, cx);
         cs = cx;
       } else {
         // the four packed sums of one input pair first, then their max3 folds: no max waits on
@@ -942,11 +973,7 @@ __device__ __forceinline__ void rec_run_rb(const RecArgs& a, float* lds, int b) 
               mx[k] = (m == 0 && p == 0) ? fmaxf(t[k].x, t[k].y) : fmaxf(fmaxf(mx[k], t[k].x), t[k].y);
           }
         s0 = mx[0]; s1 = mx[1]; s2 = mx[2]; s3 = mx[3];
-        red_max_mirror(s0, s3);
-        red_max_mirror(s1, s2);
-        red_max_hmirror(s0, s1);
-        red_max_q3210(s0, s0);
-        red_max_q1032(s0, s0);
+        red4_max(s0, s1, s2, s3);
       }
       if (kStamp) { keep(s0); mark(1); }
       float val, pval = 0.f;

@@ -4,8 +4,8 @@ set -o pipefail
 mkdir -p gpurun_out
 run() {
   tag=$1; shift
-  timeout -k 10 300 python -u bench.py --steps 20 --warmup 3 --cpu-seconds 0 "$@" > gpurun_out/r4e_$tag.log 2>&1 || exit 1
-  python - gpurun_out/r4e_$tag.log <<'PY'
+  timeout -k 10 300 python -u bench.py --steps 20 --warmup 3 --cpu-seconds 0 "$@" > gpurun_out/r4g_$tag.log 2>&1 || exit 1
+  python - gpurun_out/r4g_$tag.log <<'PY'
 import json,sys
 for l in open(sys.argv[1]):
     if l.startswith("{"):
@@ -15,3 +15,4 @@ PY
 run random --transition random
 run c3 --workload c3
 run c2 --workload c2
+run c5 --workload c5

@@ -138,6 +138,7 @@ __global__ void __launch_bounds__(NW * 64) chain(const float* mat, const float* 
     ob[o] = v0;
   }
   barrier_lds();
+  float4 gpre = make_float4(0.f, 0.f, 0.f, 0.f);
   for (int q = 1; q < T; ++q) {
     const float* src = ring + ((q - 1) & (RR - 1)) * NP;
     float eo = em[(q % EROWS) * NP + o];
@@ -154,9 +155,16 @@ __global__ void __launch_bounds__(NW * 64) chain(const float* mat, const float* 
 #pragma unroll
         for (int k = 0; k < 4; ++k) ov[k] = ls >= -110.f ? __expf(__logf(ov[k]) + ls) : 0.f;
         *reinterpret_cast<float4*>(dst + (size_t)T * NP * 0 + 64) = make_float4(ov[0], ov[1], ov[2], ov[3]);
-        // next 16 emission rows: 4 per thread, exp, into LDS
+        // next 16 emission rows: 4 per thread, exp, into LDS (1024: loaded a block ahead, as
+        // the product's rec_load / rec_stage)
         const int er = (q + 16 + row) % EROWS;
-        const float4 g = *reinterpret_cast<const float4*>(emis + er * NP + c4);
+        float4 g;
+        if constexpr (ABL & 1024) {
+          g = gpre;
+          gpre = *reinterpret_cast<const float4*>(emis + ((q + 32 + row) % EROWS) * NP + c4);
+        } else {
+          g = *reinterpret_cast<const float4*>(emis + er * NP + c4);
+        }
         *reinterpret_cast<float4*>(em + ((q + 32 + row) % EROWS) * NP + c4) =
             make_float4(__expf(g.x - 1.f), __expf(g.y - 1.f), __expf(g.z - 1.f), __expf(g.w - 1.f));
       }
@@ -192,15 +200,35 @@ __global__ void __launch_bounds__(NW * 64) chain(const float* mat, const float* 
       if constexpr (ABL & 64) {
         static_assert(GI == 16 && KO == 4, "c reduction layout");
         cx = ysum.x + ysum.y;
-        add_mirror(cx, cx);
-        add_mirror(s[0], s[3]);
-        add_mirror(s[1], s[2]);
-        add_hmirror(cx, cx);
-        add_hmirror(s[0], s[1]);
-        add_x3(cx, cx);
-        add_x3(s[0], s[0]);
-        add_x1(cx, cx);
-        add_x1(s[0], s[0]);
+        if constexpr (ABL & 256) {
+          // the two reductions as one block with only the wait states the DPP-read hazard needs
+          // (a DPP source written by one of the two previous VALU instructions)
+          asm("s_nop 1\n\t"
+              "v_add_f32_dpp %2, %2, %2 row_mirror row_mask:0xf bank_mask:0xf\n\t"
+              "v_add_f32_dpp %0, %3, %0 row_mirror row_mask:0xf bank_mask:0xf\n\t"
+              "v_add_f32_dpp %1, %4, %1 row_mirror row_mask:0xf bank_mask:0xf\n\t"
+              "v_add_f32_dpp %2, %2, %2 row_half_mirror row_mask:0xf bank_mask:0xf\n\t"
+              "s_nop 0\n\t"
+              "v_add_f32_dpp %0, %1, %0 row_half_mirror row_mask:0xf bank_mask:0xf\n\t"
+              "v_add_f32_dpp %2, %2, %2 quad_perm:[3,2,1,0] row_mask:0xf bank_mask:0xf\n\t"
+              "s_nop 0\n\t"
+              "v_add_f32_dpp %0, %0, %0 quad_perm:[3,2,1,0] row_mask:0xf bank_mask:0xf\n\t"
+              "v_add_f32_dpp %2, %2, %2 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n\t"
+              "s_nop 0\n\t"
+              "v_add_f32_dpp %0, %0, %0 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf"
+              : "+v"(s[0]), "+v"(s[1]), "+v"(cx)
+              : "v"(s[3]), "v"(s[2]));
+        } else {
+          add_mirror(cx, cx);
+          add_mirror(s[0], s[3]);
+          add_mirror(s[1], s[2]);
+          add_hmirror(cx, cx);
+          add_hmirror(s[0], s[1]);
+          add_x3(cx, cx);
+          add_x3(s[0], s[0]);
+          add_x1(cx, cx);
+          add_x1(s[0], s[0]);
+        }
       }
     } else if constexpr (ABL & 16) {
       // scheduled: the KO packed sums of one input pair first, then their max3 folds, so no
@@ -231,7 +259,20 @@ __global__ void __launch_bounds__(NW * 64) chain(const float* mat, const float* 
             s[k] = fmaxf(s[k], fmaxf(t.x, t.y));
           }
     }
-    if constexpr (!(ABL & 8) && !(FB && (ABL & 64))) reduce<GI, KO, FB>(s);
+    if constexpr (!FB && (ABL & 512)) {
+      static_assert(GI == 16 && KO == 4, "layout");
+      asm("s_nop 1\n\t"
+          "v_max_f32_dpp %0, %2, %0 row_mirror row_mask:0xf bank_mask:0xf\n\t"
+          "v_max_f32_dpp %1, %3, %1 row_mirror row_mask:0xf bank_mask:0xf\n\t"
+          "s_nop 0\n\t"
+          "v_max_f32_dpp %0, %1, %0 row_half_mirror row_mask:0xf bank_mask:0xf\n\t"
+          "s_nop 1\n\t"
+          "v_max_f32_dpp %0, %0, %0 quad_perm:[3,2,1,0] row_mask:0xf bank_mask:0xf\n\t"
+          "s_nop 1\n\t"
+          "v_max_f32_dpp %0, %0, %0 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf"
+          : "+v"(s[0]), "+v"(s[1])
+          : "v"(s[3]), "v"(s[2]));
+    } else if constexpr (!(ABL & 8) && !(FB && (ABL & 64))) reduce<GI, KO, FB>(s);
     float val = FB ? s[0] * eo : s[0] + eo;
     if constexpr (FB && (ABL & 64)) {
       const float scale = __builtin_amdgcn_rcpf(cx);
@@ -452,10 +493,16 @@ int main(int argc, char** argv) {
   CHECK(hipMemcpy(dpe, pem.data(), EROWS * NP * 4, hipMemcpyHostToDevice));
   run<8, 4, 8, false, 48>("w8 ko4 ki8 sched+nobranch", B, T, dl, dle, dout, vref);
   run<8, 4, 8, false, 48 | 128>("  + flush/stage blocks", B, T, dl, dle, dout, vref);
+  run<8, 4, 8, false, 48 | 512>("  fewer nops", B, T, dl, dle, dout, vref);
+  run<8, 4, 8, false, 48 | 128 | 1024>("  flush/stage, prefetched", B, T, dl, dle, dout, vref);
   const int TF = T;
   run<8, 4, 8, true, 32>("w8 ko4 ki8 nobranch", B, TF, dp, dpe, dout, fref);
   run<8, 4, 8, true, 32 | 64>("  + c reduction, rcp", B, TF, dp, dpe, dout, fref);
   run<8, 4, 8, true, 32 | 128>("  + flush/stage blocks", B, TF, dp, dpe, dout, fref);
   run<8, 4, 8, true, 32 | 64 | 128>("  + both (product step)", B, TF, dp, dpe, dout, fref);
+  run<8, 4, 8, true, 32 | 64 | 256>("  c reduction, fewer nops", B, TF, dp, dpe, dout, fref);
+  run<8, 4, 8, true, 32 | 64 | 128 | 256>("  product step, fewer nops", B, TF, dp, dpe, dout, fref);
+  run<8, 4, 8, true, 32 | 128 | 1024>("  flush/stage, prefetched", B, TF, dp, dpe, dout, fref);
+  run<8, 4, 8, true, 32 | 64 | 128 | 256 | 1024>("  product, fewer nops, prefetch", B, TF, dp, dpe, dout, fref);
   return 0;
 }
