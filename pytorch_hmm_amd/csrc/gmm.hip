@@ -185,7 +185,7 @@ __global__ void __launch_bounds__(kGmmThreads) gmm_score_kernel(const double* __
 //
 // gmm_score_kernel above reads one broadcast ds_read_b128 (2 dims of a frame) per 4 fp64 FMAs of
 // its one component per lane: 4 LDS cycles per 8 issue cycles per SIMD, so the CU's shared LDS
-// (4 SIMDs) is the bound at half the FMA rate (302 us at config 3 = 0.44 of fp64 peak).  Here a
+// (4 SIMDs) is the bound (376 us per call at config 3, 28 TFLOP/s fp64).  Here a
 // lane owns 4 components (p = g0 + 4*cl + j) and 16 frames (64 fp64 accumulators): each
 // broadcast x read feeds 16 FMAs, and each component's parameters, read once per dim pair from
 // LDS, feed 16 frames.  Per dim pair and lane: 8 parameter reads + 16 x reads for 256 FMAs.
@@ -231,21 +231,26 @@ __global__ void __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(kG
   const size_t f0 = (size_t)blockIdx.x * G::FT;
   const int fblk = w * FG + fg;  // this lane's 16-frame block in the tile
 
-  // staging registers: parameters (a = array, k = dim, c2 = component pair) and frames
-  double2 pre_p[G::PV];
-  float pre_x[G::XV];
-  auto fetch = [&](int dc) {
-#pragma unroll
-    for (int r = 0; r < G::PV; ++r) {
-      const int i = tid + r * G::NT;
-      const int a = i / (kG4Dc * G::CG / 2), rem = i % (kG4Dc * G::CG / 2);
-      const int k = rem / (G::CG / 2), c2 = rem % (G::CG / 2);
-      const double* src = a ? pmw : pw;
+  // Parameters go global -> LDS directly (global_load_lds_dwordx4: no staging registers, no
+  // LDS stores): one wave instruction fills 64 consecutive double2 of the buffer, element
+  // e = ((a*8 + k)*2 + h)*CL + cl holding components g0 + 4cl + 2h, +1 of array a at dim k.
+  // The frames go through registers (fp32 -> fp64 on the way into LDS), loaded when chunk dc
+  // starts; the parameters of chunk dc + 1 are issued when its reads end.  __syncthreads (which
+  // waits for vmcnt(0)) publishes both.
+  constexpr int PI = G::PS / 64;  // wave instructions per parameter buffer
+  auto fetch_params = [&](int dc, int buf) {
+    for (int i = w; i < PI; i += NW) {
+      const int e = i * 64 + l;
+      const int cle = e % G::CL, rest = e / G::CL;
+      const int h = rest & 1, k = (rest >> 1) % kG4Dc, a = rest / (2 * kG4Dc);
+      const double* src = (a ? pmw : pw) + (size_t)(dc * kG4Dc + k) * PP + g0 + 4 * cle + 2 * h;
       // PP (the padded stride) is a multiple of CG: every pair is in bounds and 16-B aligned
-      pre_p[r] = i < 2 * kG4Dc * G::CG / 2
-                     ? *reinterpret_cast<const double2*>(src + (size_t)(dc * kG4Dc + k) * PP + g0 + 2 * c2)
-                     : make_double2(0.0, 0.0);
+      __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(src),
+                                       reinterpret_cast<void*>(&ps[buf][i * 64]), 16, 0, 0);
     }
+  };
+  float pre_x[G::XV];
+  auto fetch_x = [&](int dc) {
 #pragma unroll
     for (int r = 0; r < G::XV; ++r) {
       const int i = tid + r * G::NT;
@@ -255,16 +260,7 @@ __global__ void __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(kG
       pre_x[r] = (i < G::FT * kG4Dc && frame < (size_t)nframes && d < D) ? x[frame * D + d] : 0.f;
     }
   };
-  auto stage = [&](int buf) {
-#pragma unroll
-    for (int r = 0; r < G::PV; ++r) {
-      const int i = tid + r * G::NT;
-      if (i < 2 * kG4Dc * G::CG / 2) {
-        const int a = i / (kG4Dc * G::CG / 2), rem = i % (kG4Dc * G::CG / 2);
-        const int k = rem / (G::CG / 2), c2 = rem % (G::CG / 2);
-        ps[buf][((a * kG4Dc + k) * 2 + (c2 & 1)) * G::CL + (c2 >> 1)] = pre_p[r];
-      }
-    }
+  auto stage_x = [&](int buf) {
 #pragma unroll
     for (int r = 0; r < G::XV; ++r) {
       const int i = tid + r * G::NT;
@@ -281,12 +277,15 @@ __global__ void __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(kG
 #pragma unroll
     for (int f = 0; f < kG4Nf; ++f) q[j][f] = 0.0;
 
-  fetch(0);
-  stage(0);
+  fetch_params(0, 0);
+  fetch_x(0);
+  stage_x(0);
   __syncthreads();
   for (int dc = 0; dc < NDC; ++dc) {
     const int buf = dc & 1;
-    if (dc + 1 < NDC) fetch(dc + 1);
+    // the frames of chunk dc + 1 into registers now; its parameters (LDS-DMA) after this chunk's
+    // reads: an LDS-DMA in flight makes the compiler wait for it before every LDS read
+    if (dc + 1 < NDC) fetch_x(dc + 1);
     const double2* pb = ps[buf];
     const double* xb = xs[buf] + fblk * G::XROW;
 #pragma unroll 1
@@ -301,22 +300,28 @@ __global__ void __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(kG
           wv[kk][2 * h] = a.x; wv[kk][2 * h + 1] = a.y;
           mv[kk][2 * h] = b.x; mv[kk][2 * h + 1] = b.y;
         }
+      // frame f's two dims read one frame ahead; its 8 z values formed before their squares
+      // are accumulated (no FMA waits on the one just issued)
+      double2 xn = *reinterpret_cast<const double2*>(xb + 2 * kp);  // broadcast per group
 #pragma unroll
       for (int f = 0; f < kG4Nf; ++f) {
-        const double2 xv = *reinterpret_cast<const double2*>(xb + f * kG4Dc + 2 * kp);  // broadcast per group
+        const double2 xv = xn;
+        if (f + 1 < kG4Nf) xn = *reinterpret_cast<const double2*>(xb + (f + 1) * kG4Dc + 2 * kp);
+        double z[2][4];
 #pragma unroll
-        for (int kk = 0; kk < 2; ++kk) {
-          const double xd = kk ? xv.y : xv.x;
+        for (int kk = 0; kk < 2; ++kk)
 #pragma unroll
-          for (int j = 0; j < 4; ++j) {
-            const double z = fma(xd, wv[kk][j], mv[kk][j]);
-            q[j][f] = fma(z, z, q[j][f]);
-          }
-        }
+          for (int j = 0; j < 4; ++j) z[kk][j] = fma(kk ? xv.y : xv.x, wv[kk][j], mv[kk][j]);
+#pragma unroll
+        for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) q[j][f] = fma(z[kk][j], z[kk][j], q[j][f]);
       }
     }
     if (dc + 1 < NDC) {
-      stage(buf ^ 1);  // the other buffer: its last readers passed the barrier that ended chunk dc - 1
+      // the other buffers' last readers passed the barrier that ended chunk dc - 1
+      fetch_params(dc + 1, buf ^ 1);
+      stage_x(buf ^ 1);
       __syncthreads();
     }
   }
@@ -440,12 +445,14 @@ HMM355_API int hmm355_gmm_diag_logprob_f32(const float* x, const float* means, c
   if (!gmm_use_v1(C)) {
     static_assert(G4<1, 4, 16>::CG == 256 && G4<2, 2, 16>::CG == 128 && G4<4, 2, 16>::CG == 64, "gmm_v2_group");
 #define G4L(fg, nw, nf) launch_g4<fg, nw, nf>(x, w.pw, w.pmw, w.cst, out, nframes, D, NDC, S, C, P, PP, mix_lse, st)
+    // defaults from tools/time_gmm.py (profiles/r4h_gmm2.log): config 3 (P = 512) 326 us with
+    // 16 frames per lane; P = 64 (configs 2, 5) 57 / 34 us with 4 (the work is small: more waves)
     if (CG == 256) {
       e = cfg == 2 ? G4L(1, 4, 8) : cfg == 3 ? G4L(1, 2, 16) : cfg == 4 ? G4L(1, 1, 16) : G4L(1, 4, 16);
     } else if (CG == 128) {
-      e = cfg == 2 ? G4L(2, 2, 8) : cfg == 3 ? G4L(2, 1, 8) : G4L(2, 2, 16);
+      e = cfg == 2 ? G4L(2, 2, 16) : cfg == 3 ? G4L(2, 1, 8) : G4L(2, 2, 8);
     } else {
-      e = cfg == 2 ? G4L(4, 2, 8) : cfg == 3 ? G4L(4, 1, 4) : cfg == 4 ? G4L(4, 2, 4) : G4L(4, 2, 16);
+      e = cfg == 2 ? G4L(4, 2, 8) : cfg == 3 ? G4L(4, 1, 4) : cfg == 4 ? G4L(4, 2, 16) : G4L(4, 2, 4);
     }
 #undef G4L
     return e == hipSuccess ? HMM355_OK : (int)e;
