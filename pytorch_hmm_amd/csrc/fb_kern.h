@@ -9,7 +9,7 @@ namespace hmm355 {
 
 
 template <int NP>
-__global__ void __launch_bounds__(RC<NP>::NT) fb_recur_kernel(RecArgs fa, RecArgs fb) {
+__global__ void __launch_bounds__(kFbNT<NP>) fb_recur_kernel(RecArgs fa, RecArgs fb) {
   extern __shared__ __attribute__((aligned(16))) float lds[];
   const int b = blockIdx.x >> 1;
   if (blockIdx.x & 1) {
@@ -27,7 +27,7 @@ hipError_t launch_fb(const RecArgs& fa, const RecArgs& fb, const PostArgs& pa, b
     e = launch_band_prep(fa.mat, fa.N, const_cast<BandDesc*>(fa.band), st);
     if (e != hipSuccess) return e;
   }
-  hipLaunchKernelGGL(fb_recur_kernel<NP>, dim3(2 * fa.B), dim3(RC<NP>::NT), kExclusiveLds, st, fa, fb);
+  hipLaunchKernelGGL(fb_recur_kernel<NP>, dim3(2 * fa.B), dim3(kFbNT<NP>), kExclusiveLds, st, fa, fb);
   e = hipGetLastError();
   if (e != hipSuccess) return e;
   const size_t rows = (size_t)pa.B * pa.T;

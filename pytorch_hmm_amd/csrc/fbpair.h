@@ -98,14 +98,17 @@ __device__ __forceinline__ void band_chain_dispatch(const RecArgs& a, float* lds
 template <int NP>
 __device__ __forceinline__ void fb_pair_dense(const PairArgs& p, float* lds, int b) {
   constexpr int K = NP / 64;
-  if ((int)(threadIdx.x >> 6) >= RC<NP>::NW) return;  // rec_run uses NW waves (ended waves skip barriers)
+  // rec_run_rb's NW chain waves and NH block-work helpers (ended waves skip barriers)
+  constexpr int NWD = kRbHelpers<NP>::NT / kWave;
+  static_assert(kRbHelpers<NP>::NT <= PairL<NP>::NT, "the pair launch holds the dense chain's helpers");
+  if ((int)(threadIdx.x >> 6) >= NWD) return;
   rec_run_rb<NP, kFbAlpha>(p.fa, lds, b);
   __syncthreads();
   rec_run_rb<NP, kFbBeta>(p.fb, lds, b);
   __syncthreads();
   const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
   const int T = p.fa.T, N = p.fa.N;
-  for (int t = w; t < T; t += RC<NP>::NW) {
+  for (int t = w; t < T; t += NWD) {
     const size_t row = (size_t)b * T + t;
     float u[K], v[K], mu = 0.f, mv = 0.f;
 #pragma unroll

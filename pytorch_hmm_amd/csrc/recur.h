@@ -64,6 +64,18 @@ struct RC {
   static_assert(OFF_GMAP * 4 <= kExclusiveLds, "fused Viterbi LDS layout too large");
 };
 
+// threads of a launch that may run the register-blocked dense chain (rec_run_rb, NP <= 128):
+// its NW chain waves plus NH block-work helper waves (rec_rb_helper)
+template <int NP>
+struct kRbHelpers {
+  static constexpr int NH = NP <= 128 ? RC<NP>::NW / 2 : 0;
+  static constexpr int NT = RC<NP>::NT + NH * kWave;
+};
+// the forward-backward chain kernel's threads: the dense chain's helpers included (the banded
+// chains use the first RC<NP>::NT and the rest end at once, rec_dispatch)
+template <int NP>
+constexpr int kFbNT = kRbHelpers<NP>::NT;
+
 // Sum over all 64 lanes with DPP only (row sums, then row_bcast:15 / row_bcast:31), read
 // from lane 63: wave-uniform.
 __device__ __forceinline__ float wave_sum_bcast(float x) {
@@ -275,7 +287,8 @@ constexpr bool kVitFused = RC<NP>::NW >= 6;
 // staging helpers and two psi waves on each of SIMDs 1..3); the dense chains use the first
 // RC<NP>::NW waves and the rest exit at once
 template <int NP>
-constexpr int kVitNT = kVitFused<NP> ? 1024 : RC<NP>::NT;
+constexpr int kVitNT = kVitFused<NP> ? (1024 > kRbHelpers<NP>::NT ? 1024 : kRbHelpers<NP>::NT)
+                                     : kRbHelpers<NP>::NT;
 
 template <int KIND>
 __device__ __forceinline__ int rec_tau(int q, int T) {
@@ -827,6 +840,89 @@ __device__ __forceinline__ void rec_run_bc(const RecArgs& a, float* lds, int b) 
 }
 
 // ---------------------------------------------------------------------------------------
+// Dense chain helpers (round 4).  The per-16-step block work of the register-blocked chain --
+// the next block's emission staging (exp / log), the global loads two blocks ahead, the log-scale
+// scan and the flush of the rows two blocks back (rows + the exp(log x + LS) output) -- costs the
+// chain waves ~55 ns per step when they do it themselves between two steps
+// (tools/mb_dense.hip: 229 -> 285 ns per FB step, 267 -> 325 Viterbi, prefetched), since every
+// wave waits at the next barrier for the slowest.  kRbHelpers<NP>::NH extra waves (launched
+// beside the NW chain waves) do it instead, one item per step, each item small enough to finish
+// inside the step they share a barrier with:
+//   item 0, 1    stage block kb + 1, column slices 2h, 2h + 1 (from registers loaded a block ago)
+//   item 2, 3    load block kb + 2 (clamped), the same slices
+//   item 4       the log-scale scan of block kb - 2 (every helper keeps its own running base;
+//                the last one writes LS)
+//   item 5, 6    flush block kb - 2, rows 0..7 and 8..15
+// Barriers: the helpers pass exactly the chain's barriers (two before the loop, one per step,
+// one after), so the s_barrier counts of all waves agree.  The last two blocks are flushed by
+// the helpers after the loop, and the FB log-likelihood (which needs the running base) is
+// written by the last helper.
+constexpr int kRbItems = 7;
+
+template <int NP, int KIND>
+__device__ __forceinline__ void rec_rb_helper(const RecArgs& a, float* lds, int b) {
+  using C = RC<NP>;
+  constexpr int NH = kRbHelpers<NP>::NH;
+  const int tid = threadIdx.x;
+  const int h = (tid >> 6) - C::NW, l = tid & 63, th = tid - C::NT;
+  const int T = a.T;
+  const int nblocks = (T + 15) / 16;
+  // register sets: [set = block & 1][slice 0/1][5]
+  float er[2][2][5];
+  if (KIND == kVit) rec_logt_fill<NP>(lds, l);
+  if (nblocks > 1) {
+    rec_load<NP, KIND>(a, b, 1, 2 * h, l, er[1][0]);
+    rec_load<NP, KIND>(a, b, 1, 2 * h + 1, l, er[1][1]);
+  }
+  lds_barrier();  // (the chain's: block 0 staged)
+  lds_barrier();  // (the chain's: row 0 written)
+  double base = (KIND == kFbBeta && a.bscale) ? (double)a.bscale[b] : 0.0;
+  float lsv = 0.f;
+  // item it of block kb; `set` = kb & 1 as a template-free pair of branches over er[0] / er[1]
+  auto item = [&](int kb, int it, float(&cur)[2][5], float(&nxt)[2][5]) {
+    // cur: block kb + 1's rows (loaded a block ago); nxt: block kb + 2's (loaded now)
+    switch (it) {
+      case 0: if (kb + 1 < nblocks) rec_stage<NP, KIND>(a, lds, kb + 1, 2 * h, l, cur[0]); break;
+      case 1: if (kb + 1 < nblocks) rec_stage<NP, KIND>(a, lds, kb + 1, 2 * h + 1, l, cur[1]); break;
+      case 2: rec_load<NP, KIND>(a, b, kb + 2 < nblocks ? kb + 2 : nblocks - 1, 2 * h, l, nxt[0]); break;
+      case 3: rec_load<NP, KIND>(a, b, kb + 2 < nblocks ? kb + 2 : nblocks - 1, 2 * h + 1, l, nxt[1]); break;
+      case 4: if (kb >= 2) lsv = rec_ls_scan<NP, KIND>(a, lds, b, kb - 2, base, h == NH - 1); break;
+      case 5: if (kb >= 2) rec_flush<NP, KIND>(a, lds, b, kb - 2, th, lsv); break;
+      case 6: if (kb >= 2) rec_flush<NP, KIND>(a, lds, b, kb - 2, th + NH * kWave, lsv); break;
+      default: break;
+    }
+  };
+  auto run_block = [&](int kb, float(&cur)[2][5], float(&nxt)[2][5]) {
+    const int q0 = kb * 16 < 1 ? 1 : kb * 16;
+    const int q1 = (kb + 1) * 16 < T ? (kb + 1) * 16 : T;
+    int it = 0;
+    for (int q = q0; q < q1; ++q, ++it) {
+      if (it < kRbItems) item(kb, it, cur, nxt);
+      step_barrier();
+    }
+    for (; it < kRbItems; ++it) item(kb, it, cur, nxt);  // (a short last block)
+  };
+  // block kb stages block kb + 1 from set (kb + 1) & 1 and loads block kb + 2 into set kb & 1
+  for (int k = 0; k < nblocks; k += 2) {
+    run_block(k, er[1], er[0]);
+    if (k + 1 < nblocks) run_block(k + 1, er[0], er[1]);
+  }
+  lds_barrier();  // (the chain's: the last rows and c_{T-1} written)
+  static_assert(2 * NH * kWave == C::NT, "two flush passes cover the block");
+  if (nblocks >= 2) {
+    lsv = rec_ls_scan<NP, KIND>(a, lds, b, nblocks - 2, base, h == NH - 1);
+    rec_flush<NP, KIND>(a, lds, b, nblocks - 2, th, lsv);
+    rec_flush<NP, KIND>(a, lds, b, nblocks - 2, th + NH * kWave, lsv);
+  }
+  lsv = rec_ls_scan<NP, KIND>(a, lds, b, nblocks - 1, base, h == NH - 1);
+  rec_flush<NP, KIND>(a, lds, b, nblocks - 1, th, lsv);
+  rec_flush<NP, KIND>(a, lds, b, nblocks - 1, th + NH * kWave, lsv);
+  if (KIND == kFbAlpha && a.loglik && h == NH - 1 && l == 0) {
+    a.loglik[b] = (float)(base + (double)__logf(lds[C::OFF_SC + 64 * ((T - 1) & (C::RING - 1))]));
+  }
+}
+
+// ---------------------------------------------------------------------------------------
 // Dense chain, register-blocked form (round 3; every NP).  rec_run_bc gives each lane ONE
 // output and 16 inputs per 64-block, so every step moves NP * NP * 4 bytes out of LDS
 // (64 KiB at NP = 128: 64 ds_read_b128 = 256 LDS-array cycles, the largest term of its
@@ -856,6 +952,12 @@ __device__ __forceinline__ void rec_run_rb(const RecArgs& a, float* lds, int b) 
   constexpr int NM = NP / 64;  // float4 input blocks per lane
   typedef float f2 __attribute__((ext_vector_type(2)));
   const int tid = threadIdx.x;
+  if (tid >= C::NT) {  // the block-work helpers (kRbHelpers)
+    rec_rb_helper<NP, KIND>(a, lds, b);
+    return;
+  }
+  // the chain waves issue first: a helper takes the SIMD only while they wait (LDS, barrier)
+  __builtin_amdgcn_s_setprio(2);
   const int w = tid >> 6, l = tid & 63, r = l >> 4, c = l & 15;
   const int g = 4 * w + r;      // output group
   const int x = c >> 2;         // register slot k holds output 4g + (k ^ x)
@@ -881,12 +983,13 @@ __device__ __forceinline__ void rec_run_rb(const RecArgs& a, float* lds, int b) 
       }
 
   const int nblocks = (T + 15) / 16;
-  float er0[5], er1[5];
-  if (KIND == kVit) rec_logt_fill<NP>(lds, l);
-  rec_load<NP, KIND>(a, b, 0, w, l, er0);
-  rec_stage<NP, KIND>(a, lds, 0, w, l, er0);
-  if (nblocks > 1) rec_load<NP, KIND>(a, b, 1, w, l, er1);
-  lds_barrier();
+  {
+    float er0[5];
+    if (KIND == kVit) rec_logt_fill<NP>(lds, l);
+    rec_load<NP, KIND>(a, b, 0, w, l, er0);
+    rec_stage<NP, KIND>(a, lds, 0, w, l, er0);
+  }
+  lds_barrier();  // (block 1 on: the helpers stage)
 
   auto emis = [&](int rho, int idx) { return lds[C::OFF_EMIS + (((rho >> 4) % 3) * 16 + (rho & 15)) * NP + idx]; };
   const bool writer = (c & 3) == 0;
@@ -903,7 +1006,6 @@ __device__ __forceinline__ void rec_run_rb(const RecArgs& a, float* lds, int b) 
   }
   lds_barrier();
 
-  double base = (KIND == kFbBeta && a.bscale) ? (double)a.bscale[b] : 0.0;
   unsigned long long st_acc[4] = {0, 0, 0, 0}, st_prev = 0, st_t0 = 0, st_steps = 0;
   long long rt0 = 0;
   if (kStamp) { st_t0 = stamp(); st_prev = st_t0; rt0 = __builtin_amdgcn_s_memrealtime(); }
@@ -911,10 +1013,7 @@ __device__ __forceinline__ void rec_run_rb(const RecArgs& a, float* lds, int b) 
     if (kStamp) { const unsigned long long t = stamp(); st_acc[k] += t - st_prev; st_prev = t; }
   };
 
-  auto run_block = [&](int kb, float(&ernext)[5], float(&erfree)[5]) {
-    rec_stage<NP, KIND>(a, lds, kb + 1, w, l, ernext);
-    rec_load<NP, KIND>(a, b, kb + 2 < nblocks ? kb + 2 : nblocks - 1, w, l, erfree);
-    if (kb >= 2) rec_flush<NP, KIND>(a, lds, b, kb - 2, tid, rec_ls_scan<NP, KIND>(a, lds, b, kb - 2, base, w == C::NW - 1));
+  auto run_block = [&](int kb) {
     const int q0 = kb * 16 < 1 ? 1 : kb * 16;
     const int q1 = (kb + 1) * 16 < T ? (kb + 1) * 16 : T;
     for (int q = q0; q < q1; ++q) {
@@ -995,10 +1094,7 @@ __device__ __forceinline__ void rec_run_rb(const RecArgs& a, float* lds, int b) 
       step_barrier();
     }
   };
-  for (int k = 0; k < nblocks; k += 2) {
-    run_block(k, er1, er0);
-    if (k + 1 < nblocks) run_block(k + 1, er0, er1);
-  }
+  for (int k = 0; k < nblocks; ++k) run_block(k);
   if (kStamp && (tid & 63) == 0) {
     const unsigned long long t1 = stamp();
     const long long rt1 = __builtin_amdgcn_s_memrealtime();
@@ -1013,13 +1109,7 @@ __device__ __forceinline__ void rec_run_rb(const RecArgs& a, float* lds, int b) 
     const float cs = wave_sum_bcast(ys);
     if (l == 0) lds[C::OFF_SC + 64 * ((T - 1) & (C::RING - 1))] = cs;  // c_{T-1} (loglik only)
   }
-  lds_barrier();
-  if (nblocks >= 2)
-    rec_flush<NP, KIND>(a, lds, b, nblocks - 2, tid, rec_ls_scan<NP, KIND>(a, lds, b, nblocks - 2, base, w == C::NW - 1));
-  rec_flush<NP, KIND>(a, lds, b, nblocks - 1, tid, rec_ls_scan<NP, KIND>(a, lds, b, nblocks - 1, base, w == C::NW - 1));
-  if (KIND == kFbAlpha && a.loglik && tid == C::NT - 64) {
-    a.loglik[b] = (float)(base + (double)__logf(lds[C::OFF_SC + 64 * ((T - 1) & (C::RING - 1))]));
-  }
+  lds_barrier();  // the last blocks' flush and the log-likelihood: the helpers
 }
 
 // The banded chain wave (wave 0 of rec_band; waves 0 and 1 of the forward-backward pair
@@ -1703,7 +1793,11 @@ __device__ __forceinline__ int rec_band_code(const RecArgs& a) {
 
 template <int NP, int KIND>
 __device__ __forceinline__ void rec_dispatch(const RecArgs& a, float* lds, int b) {
-  switch (rec_band_code<KIND, NP>(a)) {
+  const int code = rec_band_code<KIND, NP>(a);
+  // the banded chains are written for RC<NP>::NT threads (the fused Viterbi form for 1024)
+  constexpr int kBandNT = (KIND == kVit && kVitFused<NP>) ? 1024 : RC<NP>::NT;
+  if (code != 0 && threadIdx.x >= kBandNT) return;
+  switch (code) {
     case 2: rec_band<NP, KIND, 2>(a, lds, b, a.band); break;
     case 4: rec_band<NP, KIND, 4>(a, lds, b, a.band); break;
     case 8: rec_band<NP, KIND, 8>(a, lds, b, a.band); break;
@@ -1723,14 +1817,18 @@ __device__ __forceinline__ void rec_dispatch(const RecArgs& a, float* lds, int b
           if (threadIdx.x == 0 && a.final_score) a.final_score[b] = __builtin_nanf("");
         }
       }
-      if (threadIdx.x >= RC<NP>::NT) return;  // (a wider Viterbi launch: waves beyond NW end here)
       // (diagnostic ablation bits: 1 << 25 the round-2 register-operand chain (NP <= 128),
       // 1 << 24 the DPP-broadcast chain)
       // (NP = 256 keeps the DPP-broadcast chain: 16 waves leave 128 VGPRs a lane, too few for
       // the register-blocked slices)
-      if constexpr (NP <= 128 && !(kAbl & (3 << 24))) rec_run_rb<NP, KIND>(a, lds, b);
-      else if constexpr (NP <= 128 && !(kAbl & (1 << 24))) rec_run_bc<NP, KIND>(a, lds, b);
-      else rec_run<NP, KIND>(a, lds, b);
+      if constexpr (NP <= 128 && !(kAbl & (3 << 24))) {
+        if (threadIdx.x >= kRbHelpers<NP>::NT) return;  // (waves beyond the chain and its helpers)
+        rec_run_rb<NP, KIND>(a, lds, b);
+      } else {
+        if (threadIdx.x >= RC<NP>::NT) return;
+        if constexpr (NP <= 128 && !(kAbl & (1 << 24))) rec_run_bc<NP, KIND>(a, lds, b);
+        else rec_run<NP, KIND>(a, lds, b);
+      }
       break;
   }
 }
