@@ -54,7 +54,7 @@ def parse():
     p.add_argument("--cpu-seconds", type=float, default=12.0, help="bounded CPU-baseline budget (0 = skip)")
     p.add_argument("--no-graph", action="store_true",
                    help="launch every step eagerly instead of replaying one captured HIP graph")
-    p.add_argument("--transition", default="left_to_right", choices=["left_to_right", "ergodic", "random"],
+    p.add_argument("--transition", default="left_to_right", choices=["left_to_right", "ergodic", "random", "trained"],
                    help="transition matrix of the workload (BASELINE: left_to_right 0.7; SURVEY §8(d) also "
                         "names create_transition_matrix(N,'ergodic'); 'random' = a dense learned-style "
                         "matrix softmax(randn), which takes the dense chains)")
@@ -671,6 +671,24 @@ def main():
     elif args.transition == "random":
         gp = torch.Generator().manual_seed(4321)
         hmm = ph.HMMPyTorch(torch.softmax(torch.randn(N, N, generator=gp), dim=-1))
+    elif args.transition == "trained":
+        # a trained layer's tables (hmm_layer.py:61-89): HMMLayer(N) after three Adam steps
+        # (lr 1e-3) on compute_loss over random scores at T = 8 (no saturation, so every
+        # logit moves): no structural zeros are left and the dense chains run
+        torch.manual_seed(0)
+        layer = ph.HMMLayer(N).to(dev)
+        opt = torch.optim.Adam(layer.parameters(), lr=1e-3)
+        gt = torch.Generator(device=dev).manual_seed(0)
+        layer.train()
+        for _ in range(3):
+            loss = layer.compute_loss(torch.randn(4, 8, N, device=dev, generator=gt))
+            opt.zero_grad()
+            loss.backward()
+            opt.step()
+        layer.eval()
+        with torch.no_grad():
+            layer(torch.randn(1, 2, N, device=dev, generator=gt))   # later-call tables
+        hmm = layer._hmm
     else:
         hmm = ph.HMMPyTorch(ph.create_left_to_right_matrix(N, 0.7))
     if args.strong:
@@ -739,7 +757,8 @@ def main():
     ms_per_step = elapsed / args.steps * 1e3
 
     tdesc = {"left_to_right": "left_to_right(0.7)", "ergodic": "ergodic",
-             "random": "random dense softmax(randn(N,N))"}[args.transition]
+             "random": "random dense softmax(randn(N,N))",
+             "trained": "trained HMMLayer(N) tables (3 Adam steps)"}[args.transition]
     # roofline of the dominant op, algorithmic bytes per SURVEY.md §8(d)
     pair = plan is not None and getattr(plan, "_hmm355_banded", False) and ops._use_pair(B, dev)
     if fb_ms >= vit_ms:

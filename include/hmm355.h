@@ -141,6 +141,13 @@ int hmm355_viterbi_plan_f32(const float* obs, int obs_mode, const float* log_P, 
  * T <= 262144; otherwise the flag is ignored.  Passing the flag with a plan that is not banded
  * is a caller error: the states come back as -1 and the final score as NaN. */
 #define HMM355_VIT_PLAN_BANDED 0x1u
+/* HMM355_VIT_PLAN_DENSE: the caller read hmm355_plan_banded(plan) == 0.  Then, for N <= 128, the
+ * argmax pointers of each 64-step chunk are computed while the chain still runs, by workgroups
+ * of the chain's own launch on the CUs the chain leaves idle (they follow the rows the chain
+ * has flushed; a chunk they did not finish is computed by the pass after the chain, so the
+ * result never depends on their timing).  Without the flag the pointers are computed after the
+ * chain.  The flag with a banded plan only costs the idle launch. */
+#define HMM355_VIT_PLAN_DENSE 0x2u
 int hmm355_viterbi_plan_ex_f32(const float* obs, int obs_mode, const float* log_P, const float* init,
                                const void* plan, unsigned flags, int B, int T, int N, int64_t* states,
                                float* log_delta, float* final_score, void* workspace,

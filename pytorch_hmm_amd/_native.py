@@ -16,6 +16,7 @@ OBS_LOG = 1
 FB_POSTERIOR = 1
 FB_PAIR = 0x100
 VIT_PLAN_BANDED = 0x1  # HMM355_VIT_PLAN_BANDED
+VIT_PLAN_DENSE = 0x2  # HMM355_VIT_PLAN_DENSE
 FB_FORWARD = 2
 FB_BACKWARD = 4
 

@@ -168,6 +168,11 @@ struct VitArgs {
   int B, T, N, obs_mode, nchunks;
   const BandDesc* band;  // banded decomposition (band.h) or null
   int vdiag;             // diagnostic bits for RecArgs::vtail (timing only)
+  // psi followers (HMM355_VIT_PLAN_DENSE): workgroups beside the chain, their progress and
+  // finished-chunk words (RecArgs::prog / done), zeroed before each launch
+  int nfollow;
+  int* prog;
+  uint8_t* done;
 };
 
 // chunk map: G[j] = state at t_lo - 1 given state j at t_hi (psi rows of the chunk in LDS)

@@ -70,6 +70,7 @@ template <int NP>
 struct kRbHelpers {
   static constexpr int NH = NP <= 128 ? RC<NP>::NW / 2 : 0;
   static constexpr int NT = RC<NP>::NT + NH * kWave;
+  static_assert(NH <= 8, "kProgSlots");
 };
 // the forward-backward chain kernel's threads: the dense chain's helpers included (the banded
 // chains use the first RC<NP>::NT and the rest end at once, rec_dispatch)
@@ -275,7 +276,13 @@ struct RecArgs {
   float* final_score;    // (B) max of the last trellis row, or null
   int nchunks;
   int vtail;
+  // Viterbi, dense chain with psi followers (HMM355_VIT_PLAN_DENSE, vit_kern.h): the helpers
+  // publish the blocks they have flushed in prog[b * kProgSlots + h]; the follower workgroups
+  // (blockIdx >= B) mark the chunks they finished in done[b * nchunks + c]
+  int* prog;
+  uint8_t* done;
 };
+constexpr int kProgSlots = 8;  // >= kRbHelpers<NP>::NH
 
 // The banded Viterbi chain computes the argmax pointers psi itself (helper waves on the idle
 // SIMDs, from the delta rows still in its LDS ring), so the psi pass only composes the
@@ -853,11 +860,18 @@ __device__ __forceinline__ void rec_run_bc(const RecArgs& a, float* lds, int b) 
 //   item 4       the log-scale scan of block kb - 2 (every helper keeps its own running base;
 //                the last one writes LS)
 //   item 5, 6    flush block kb - 2, rows 0..7 and 8..15
+//   item 7       (Viterbi with psi followers) publish the flushed blocks, once per chunk
 // Barriers: the helpers pass exactly the chain's barriers (two before the loop, one per step,
 // one after), so the s_barrier counts of all waves agree.  The last two blocks are flushed by
 // the helpers after the loop, and the FB log-likelihood (which needs the running base) is
 // written by the last helper.
-constexpr int kRbItems = 7;
+// items per block: 7 (FB), 8 (Viterbi: the psi followers' publish); HMM355_RB_ITEMS_FB is a
+// diagnostic override
+#ifndef HMM355_RB_ITEMS_FB
+#define HMM355_RB_ITEMS_FB 7
+#endif
+template <int KIND>
+constexpr int kRbItems = KIND == kVit ? 8 : HMM355_RB_ITEMS_FB;
 
 template <int NP, int KIND>
 __device__ __forceinline__ void rec_rb_helper(const RecArgs& a, float* lds, int b) {
@@ -878,6 +892,22 @@ __device__ __forceinline__ void rec_rb_helper(const RecArgs& a, float* lds, int 
   lds_barrier();  // (the chain's: row 0 written)
   double base = (KIND == kFbBeta && a.bscale) ? (double)a.bscale[b] : 0.0;
   float lsv = 0.f;
+  // psi followers (Viterbi, vit_kern.h): the count of flushed blocks, published once per 64-step
+  // chunk.  Every helper waits for its own flush stores (a workgroup-scope release: vmcnt(0), no
+  // cache maintenance) before the step barrier; one lane of helper 0 then, after the barrier,
+  // makes them visible to the other XCDs (an agent-scope release: this XCD's L2 written back)
+  // and stores the count.  Agent-scope releases are L2-wide: per block and helper they slowed
+  // the whole chip (Viterbi op 0.77 -> 1.79 ms), so there is one per chunk and sequence.
+  const bool follow = KIND == kVit && a.prog;
+  auto flushed = [&]() {
+    if (follow) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+  };
+  auto publish = [&](int blocks) {
+    if (follow && h == 0 && l == 0) {
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+      __hip_atomic_store(a.prog + (size_t)b * kProgSlots, blocks, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  };
   // item it of block kb; `set` = kb & 1 as a template-free pair of branches over er[0] / er[1]
   auto item = [&](int kb, int it, float(&cur)[2][5], float(&nxt)[2][5]) {
     // cur: block kb + 1's rows (loaded a block ago); nxt: block kb + 2's (loaded now)
@@ -888,7 +918,15 @@ __device__ __forceinline__ void rec_rb_helper(const RecArgs& a, float* lds, int 
       case 3: rec_load<NP, KIND>(a, b, kb + 2 < nblocks ? kb + 2 : nblocks - 1, 2 * h + 1, l, nxt[1]); break;
       case 4: if (kb >= 2) lsv = rec_ls_scan<NP, KIND>(a, lds, b, kb - 2, base, h == NH - 1); break;
       case 5: if (kb >= 2) rec_flush<NP, KIND>(a, lds, b, kb - 2, th, lsv); break;
-      case 6: if (kb >= 2) rec_flush<NP, KIND>(a, lds, b, kb - 2, th + NH * kWave, lsv); break;
+      case 6:
+        if (kb >= 2) {
+          rec_flush<NP, KIND>(a, lds, b, kb - 2, th + NH * kWave, lsv);
+          flushed();
+        }
+        break;
+      case 7:  // (after the barrier that follows every helper's flush of block kb - 2)
+        if (kb >= 2 && ((kb - 1) & 3) == 0) publish(kb - 1);  // blocks 0 .. kb - 2 are out
+        break;
       default: break;
     }
   };
@@ -897,10 +935,10 @@ __device__ __forceinline__ void rec_rb_helper(const RecArgs& a, float* lds, int 
     const int q1 = (kb + 1) * 16 < T ? (kb + 1) * 16 : T;
     int it = 0;
     for (int q = q0; q < q1; ++q, ++it) {
-      if (it < kRbItems) item(kb, it, cur, nxt);
+      if (it < kRbItems<KIND>) item(kb, it, cur, nxt);
       step_barrier();
     }
-    for (; it < kRbItems; ++it) item(kb, it, cur, nxt);  // (a short last block)
+    for (; it < kRbItems<KIND>; ++it) item(kb, it, cur, nxt);  // (a short last block)
   };
   // block kb stages block kb + 1 from set (kb + 1) & 1 and loads block kb + 2 into set kb & 1
   for (int k = 0; k < nblocks; k += 2) {
@@ -917,6 +955,11 @@ __device__ __forceinline__ void rec_rb_helper(const RecArgs& a, float* lds, int 
   lsv = rec_ls_scan<NP, KIND>(a, lds, b, nblocks - 1, base, h == NH - 1);
   rec_flush<NP, KIND>(a, lds, b, nblocks - 1, th, lsv);
   rec_flush<NP, KIND>(a, lds, b, nblocks - 1, th + NH * kWave, lsv);
+  if (follow) {
+    flushed();
+    __syncthreads();  // (the chain waves have ended: the helpers alone)
+    publish(nblocks);
+  }
   if (KIND == kFbAlpha && a.loglik && h == NH - 1 && l == 0) {
     a.loglik[b] = (float)(base + (double)__logf(lds[C::OFF_SC + 64 * ((T - 1) & (C::RING - 1))]));
   }

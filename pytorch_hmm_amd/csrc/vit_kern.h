@@ -8,8 +8,15 @@ namespace hmm355 {
 
 
 template <int NP>
+__device__ __forceinline__ void vit_psi_follow(const RecArgs& ra, float* lds);
+
+template <int NP>
 __global__ void __launch_bounds__(kVitNT<NP>) vit_fwd_kernel(RecArgs ra) {
   extern __shared__ __attribute__((aligned(16))) float lds[];
+  if ((int)blockIdx.x >= ra.B) {  // psi followers (HMM355_VIT_PLAN_DENSE)
+    if constexpr (NP <= 128) vit_psi_follow<NP>(ra, lds);
+    return;
+  }
   rec_dispatch<NP, kVit>(ra, lds, blockIdx.x);
 }
 
@@ -99,34 +106,15 @@ __device__ __forceinline__ void psi_band_rows(const VitArgs& a, uint8_t (*prow)[
   }
 }
 
+// ---- dense psi rows (every non-banded matrix: config 3, every trained layer)
+// The matrix slice of lane (r, c) of wave w: M[blk][n] = L[i][o], i = 64*blk + 16*r + n,
+// o = 16*w + c (-inf outside N x N).
 template <int NP>
-__global__ void __launch_bounds__(VF<NP>::NT) vit_psi_kernel(VitArgs a) {
-  using C = VF<NP>;
-  static_assert(kPsiChunk == kChunk, "chunk length shared with the fused banded chain");
-  __shared__ __attribute__((aligned(16))) uint8_t prow[kChunk][NP];
-  const int chunk = blockIdx.x, b = blockIdx.y;
-  const int tid = threadIdx.x;
-  if (kVitFused<NP> && a.band && a.band->wc <= kBandMax) {
-    // the banded chain's helpers wrote the psi rows (recur.h kVitFused): compose the map only
-    if (chunk == 0) return;
-    const int t_lo = chunk * kChunk;
-    const int t_hi = (t_lo + kChunk < a.T ? t_lo + kChunk : a.T) - 1;
-    const uint8_t* psrc = a.psi + ((size_t)b * a.T + t_lo) * NP;
-    for (int idx = tid; idx < (t_hi - t_lo + 1) * NP / 16; idx += C::NT)
-      *reinterpret_cast<uint4*>(&prow[0][0] + idx * 16) = *reinterpret_cast<const uint4*>(psrc + idx * 16);
-    __syncthreads();
-    compose_chunk_map<NP>(a, prow, b, chunk, t_lo, t_hi);
-    return;
-  }
-  const int w = tid >> 6, l = tid & 63, r = l >> 4, c = l & 15;
-  const int o = 16 * w + c;
-  const int T = a.T, N = a.N;
-  const int t_lo = chunk * kChunk;
-  const int t_hi = (t_lo + kChunk < T ? t_lo + kChunk : T) - 1;
-
-  float M[C::NBLK][16];
+__device__ __forceinline__ void psi_dense_matrix(const VitArgs& a, float (&M)[VF<NP>::NBLK][16]) {
+  const int tid = threadIdx.x, w = tid >> 6, l = tid & 63, r = l >> 4, c = l & 15;
+  const int o = 16 * w + c, N = a.N;
 #pragma unroll
-  for (int blk = 0; blk < C::NBLK; ++blk)
+  for (int blk = 0; blk < VF<NP>::NBLK; ++blk)
 #pragma unroll
     for (int n = 0; n < 16; ++n) {
       const int i = 64 * blk + 16 * r + n;
@@ -134,26 +122,28 @@ __global__ void __launch_bounds__(VF<NP>::NT) vit_psi_kernel(VitArgs a) {
       const float v = a.log_P[ok ? (size_t)i * N + o : 0];
       M[blk][n] = ok ? v : -INFINITY;
     }
-  if (t_lo == 0 && tid < NP) prow[0][tid] = 0;  // psi_0 (hmm.py:156 zeros)
-  if (a.band && a.band->wc <= kBandMax) {
-    __shared__ float rowM[kChunk];
-    __shared__ int rowI[kChunk];
-    extern __shared__ __attribute__((aligned(16))) float drows[];  // [kChunk][NP] (dynamic)
-    psi_band_rows<NP>(a, prow, rowM, rowI, drows, b, t_lo, t_hi);
-    __syncthreads();
-    psi_write_rows<NP>(a, prow, b, chunk, t_lo, t_hi);
-    return;
-  }
+}
 
-  // Dense rows.  Lane (r, c) of wave w scans the inputs i = 64*blk + 16*r + n (n = 0..15) of
-  // output o = 16*w + c: s_i = fl(delta_{t-1,i} + L[i][o]), delta_{t-1,i} broadcast from lane
-  // 16r + n of the row (one v_add_f32_dpp row_newbcast per candidate).  The first argmax
-  // (torch.max, hmm.py:164-168) in three exact passes: the maximum m over the lane's candidates
-  // and then over the four row groups (max is order-free); each lane's smallest i with s_i == m
-  // (a reverse equality scan, no value carried); the smallest such i over the row groups.  Rows
-  // stream through a three-deep register ring (loads three steps ahead, no register copies, so
-  // no VALU-write -> DPP-read padding).  i >= N or o >= N: L = -inf, so s = -inf (and the row
-  // value read for such lanes is a valid element of the row).
+// Dense rows of one chunk into prow, then to HBM with the chunk map.  Lane (r, c) of wave w
+// scans the inputs i = 64*blk + 16*r + n (n = 0..15) of output o = 16*w + c:
+// s_i = fl(delta_{t-1,i} + L[i][o]), delta_{t-1,i} broadcast from lane 16r + n of the row (one
+// v_add_f32_dpp row_newbcast per candidate).  The first argmax (torch.max, hmm.py:164-168) in
+// three exact passes: the maximum m over the lane's candidates and then over the four row
+// groups (max is order-free); each lane's smallest i with s_i == m (a reverse equality scan, no
+// value carried); the smallest such i over the row groups.  Rows stream through a three-deep
+// register ring (loads three steps ahead, no register copies, so no VALU-write -> DPP-read
+// padding).  i >= N or o >= N: L = -inf, so s = -inf (and the row value read for such lanes is
+// a valid element of the row).
+template <int NP>
+__device__ __forceinline__ void psi_dense_chunk(const VitArgs& a, uint8_t (*prow)[NP],
+                                                const float (&M)[VF<NP>::NBLK][16], int b, int chunk) {
+  using C = VF<NP>;
+  const int tid = threadIdx.x, w = tid >> 6, l = tid & 63, r = l >> 4, c = l & 15;
+  const int o = 16 * w + c;
+  const int T = a.T, N = a.N;
+  const int t_lo = chunk * kChunk;
+  const int t_hi = (t_lo + kChunk < T ? t_lo + kChunk : T) - 1;
+  if (t_lo == 0 && tid < NP) prow[0][tid] = 0;  // psi_0 (hmm.py:156 zeros)
   const float* dbase = a.delta + (size_t)b * T * N;
   auto load_row = [&](int t, float(&yv)[C::NBLK]) {
     const int tt = t <= t_hi ? t : t_hi;  // (ahead of the chunk end: a valid row, unused)
@@ -220,6 +210,103 @@ __global__ void __launch_bounds__(VF<NP>::NT) vit_psi_kernel(VitArgs a) {
 }
 
 template <int NP>
+__global__ void __launch_bounds__(VF<NP>::NT) vit_psi_kernel(VitArgs a) {
+  using C = VF<NP>;
+  static_assert(kPsiChunk == kChunk, "chunk length shared with the fused banded chain");
+  __shared__ __attribute__((aligned(16))) uint8_t prow[kChunk][NP];
+  const int chunk = blockIdx.x, b = blockIdx.y;
+  const int tid = threadIdx.x;
+  const bool banded = a.band && a.band->wc <= kBandMax;
+  if (kVitFused<NP> && banded) {
+    // the banded chain's helpers wrote the psi rows (recur.h kVitFused): compose the map only
+    if (chunk == 0) return;
+    const int t_lo = chunk * kChunk;
+    const int t_hi = (t_lo + kChunk < a.T ? t_lo + kChunk : a.T) - 1;
+    const uint8_t* psrc = a.psi + ((size_t)b * a.T + t_lo) * NP;
+    for (int idx = tid; idx < (t_hi - t_lo + 1) * NP / 16; idx += C::NT)
+      *reinterpret_cast<uint4*>(&prow[0][0] + idx * 16) = *reinterpret_cast<const uint4*>(psrc + idx * 16);
+    __syncthreads();
+    compose_chunk_map<NP>(a, prow, b, chunk, t_lo, t_hi);
+    return;
+  }
+  if (!banded && a.done && a.done[(size_t)b * a.nchunks + chunk]) return;  // a follower did it
+  if (banded) {
+    const int t_lo = chunk * kChunk;
+    const int t_hi = (t_lo + kChunk < a.T ? t_lo + kChunk : a.T) - 1;
+    if (t_lo == 0 && tid < NP) prow[0][tid] = 0;  // psi_0 (hmm.py:156 zeros)
+    __shared__ float rowM[kChunk];
+    __shared__ int rowI[kChunk];
+    extern __shared__ __attribute__((aligned(16))) float drows[];  // [kChunk][NP] (dynamic)
+    psi_band_rows<NP>(a, prow, rowM, rowI, drows, b, t_lo, t_hi);
+    __syncthreads();
+    psi_write_rows<NP>(a, prow, b, chunk, t_lo, t_hi);
+    return;
+  }
+  float M[C::NBLK][16];
+  psi_dense_matrix<NP>(a, M);
+  psi_dense_chunk<NP>(a, prow, M, b, chunk);
+}
+
+// ---- psi followers (HMM355_VIT_PLAN_DENSE; RecArgs::prog): workgroups blockIdx >= B of the
+// chain's own launch.  Workgroups are dispatched in index order, so the B chain workgroups own
+// their CUs before any follower is placed, and a follower waiting for rows can never keep a
+// chain from starting.  Each follower takes the tasks (chunk, sequence) chunk-major with a
+// stride of the follower count, waits until that sequence's chain has published the blocks
+// holding the chunk's rows (rec_rb_helper: once per chunk; acquire at agent scope, then a
+// workgroup barrier), computes the chunk's psi rows and map exactly as the pass after the chain does,
+// and marks the chunk done.  A wait is bounded (kFollowWait ticks of the 100 MHz real-time
+// counter): a chunk not reached in time is left to the pass after the chain, which computes
+// every chunk not marked done, so the result never depends on the followers' timing.
+constexpr long long kFollowWait = 20000000;  // 200 ms
+
+template <int NP>
+__device__ __forceinline__ void vit_psi_follow(const RecArgs& ra, float* lds) {
+  using C = VF<NP>;
+  if (rec_band_code<kVit, NP>(ra) != 0) return;  // banded: the psi pass after the chain
+  if (threadIdx.x >= C::NT) return;              // the dense psi layout's waves
+  const VitArgs a{ra.obs, ra.mat, ra.init, ra.rows, ra.final_score, ra.states, ra.psi, ra.G,
+                  ra.B, ra.T, ra.N, ra.obs_mode, ra.nchunks, ra.band, 0, 0, ra.prog, ra.done};
+  uint8_t(*prow)[NP] = reinterpret_cast<uint8_t(*)[NP]>(lds);
+  int* ok_slot = reinterpret_cast<int*>(lds + kChunk * NP / 4);
+  float M[C::NBLK][16];
+  psi_dense_matrix<NP>(a, M);
+  const int nf = (int)gridDim.x - a.B;
+  const int ntask = a.B * a.nchunks;
+  for (int task = (int)blockIdx.x - a.B; task < ntask; task += nf) {
+    const int chunk = task / a.B, b = task - chunk * a.B;
+    const int t_lo = chunk * kChunk;
+    const int t_hi = (t_lo + kChunk < a.T ? t_lo + kChunk : a.T) - 1;
+    // rows t_first - 1 .. t_hi - 1 are read: blocks 0 .. (t_hi - 1) / 16 must be out
+    const int need = t_hi >= 1 ? ((t_hi - 1) >> 4) + 1 : 0;
+    if (threadIdx.x == 0) {
+      int ok = 1;
+      const long long t0 = __builtin_amdgcn_s_memrealtime();
+      // relaxed polls (no cache maintenance per poll), one agent-scope acquire once the count
+      // is there (it invalidates this XCD's caches: once per task, not per poll)
+      for (;;) {
+        const int have = __hip_atomic_load(a.prog + (size_t)b * kProgSlots, __ATOMIC_RELAXED,
+                                           __HIP_MEMORY_SCOPE_AGENT);
+        if (have >= need) break;
+        if (__builtin_amdgcn_s_memrealtime() - t0 > kFollowWait) {
+          ok = 0;
+          break;
+        }
+        __builtin_amdgcn_s_sleep(16);
+      }
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      *ok_slot = ok;
+    }
+    __syncthreads();
+    const int ok = *ok_slot;
+    __syncthreads();  // (ok_slot is rewritten by the next task's wait)
+    if (!ok) continue;
+    psi_dense_chunk<NP>(a, prow, M, b, chunk);
+    __syncthreads();  // (prow is rewritten by the next task; the rows and map are issued)
+    if (threadIdx.x == 0) a.done[(size_t)b * a.nchunks + chunk] = 1;
+  }
+}
+
+template <int NP>
 hipError_t launch_vit(const VitArgs& va, bool prep, bool tail, hipStream_t sm) {
   hipError_t e = allow_lds(vit_fwd_kernel<NP>, kExclusiveLds);  // own the CU (recur.h)
   if (e != hipSuccess) return e;
@@ -236,13 +323,28 @@ hipError_t launch_vit(const VitArgs& va, bool prep, bool tail, hipStream_t sm) {
     ra.nchunks = va.nchunks;
     ra.vtail = 1 | va.vdiag;
   }
-  hipLaunchKernelGGL(vit_fwd_kernel<NP>, dim3(va.B), dim3(kVitNT<NP>), kExclusiveLds, sm, ra);
+  // psi followers beside a dense chain (NP <= 128: the chain with block-work helpers publishes)
+  const int nfollow = (!tail && NP <= 128 && va.prog && va.done) ? va.nfollow : 0;
+  if (nfollow > 0) {
+    e = hipMemsetAsync(va.prog, 0, (size_t)va.B * kProgSlots * sizeof(int), sm);
+    if (e == hipSuccess) e = hipMemsetAsync(va.done, 0, (size_t)va.B * va.nchunks, sm);
+    if (e != hipSuccess) return e;
+    ra.G = va.G;
+    ra.states = va.states;
+    ra.final_score = va.final_score;
+    ra.nchunks = va.nchunks;
+    ra.prog = va.prog;
+    ra.done = va.done;
+  }
+  hipLaunchKernelGGL(vit_fwd_kernel<NP>, dim3(va.B + nfollow), dim3(kVitNT<NP>), kExclusiveLds, sm, ra);
   e = hipGetLastError();
   if (e != hipSuccess) return e;
   if (tail) return hipSuccess;
   // banded psi stages the chunk's delta rows in LDS (dynamic, kChunk x NP floats)
   const size_t psi_lds = va.band ? (size_t)kChunk * NP * sizeof(float) : 0;
-  hipLaunchKernelGGL(vit_psi_kernel<NP>, dim3(va.nchunks, va.B), dim3(VF<NP>::NT), psi_lds, sm, va);
+  VitArgs vp = va;
+  if (nfollow == 0) vp.done = nullptr;  // (no followers: every chunk here)
+  hipLaunchKernelGGL(vit_psi_kernel<NP>, dim3(va.nchunks, va.B), dim3(VF<NP>::NT), psi_lds, sm, vp);
   e = hipGetLastError();
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL(vit_backtrace_kernel<NP>, dim3(va.nchunks, va.B), dim3(64), 0, sm, va);

@@ -45,7 +45,23 @@ HMM355_API size_t hmm355_viterbi_workspace_bytes(int B, int T, int N) {
   if (B < 0 || T < 1 || N < 1 || N > 256) return 0;
   const size_t NP = pad_states(N);
   const size_t nc = (T + kChunk - 1) / kChunk;
-  return align_up((size_t)B * T * NP, 256) + align_up((size_t)B * nc * NP, 256) + align_up(sizeof(BandDesc), 256);
+  // psi rows, chunk maps, the plan-less band descriptor, the psi followers' progress and done words
+  return align_up((size_t)B * T * NP, 256) + align_up((size_t)B * nc * NP, 256) + align_up(sizeof(BandDesc), 256) +
+         align_up((size_t)B * kProgSlots * sizeof(int), 256) + align_up((size_t)B * nc, 256);
+}
+
+// CUs of the current device (cached per device): the psi followers take the ones the chain
+// leaves, at most one workgroup per CU (the launch owns a CU's LDS)
+static int device_cus() {
+  static int cus[64] = {0};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 0;
+  if (cus[dev] == 0) {
+    int n = 0;
+    if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) n = 0;
+    cus[dev] = n > 0 ? n : -1;
+  }
+  return cus[dev] > 0 ? cus[dev] : 0;
 }
 
 HMM355_API int hmm355_viterbi_plan_ex_f32(const float* obs, int obs_mode, const float* log_P, const float* init,
@@ -65,6 +81,8 @@ HMM355_API int hmm355_viterbi_plan_ex_f32(const float* obs, int obs_mode, const 
   uint8_t* psi = static_cast<uint8_t*>(workspace);
   uint8_t* G = psi + align_up((size_t)B * T * NP, 256);
   uint8_t* bandp = G + align_up((size_t)B * nc * NP, 256);
+  int* prog = reinterpret_cast<int*>(bandp + align_up(sizeof(BandDesc), 256));
+  uint8_t* done = reinterpret_cast<uint8_t*>(prog) + align_up((size_t)B * kProgSlots * sizeof(int), 256);
   BandDesc* band = use_band() ? (plan ? static_cast<BandDesc*>(const_cast<void*>(plan))
                                       : reinterpret_cast<BandDesc*>(bandp))
                                : nullptr;
@@ -80,6 +98,14 @@ HMM355_API int hmm355_viterbi_plan_ex_f32(const float* obs, int obs_mode, const 
   // (HMM355_VIT_TAIL_DIAG: diagnostic bits of RecArgs::vtail, timing only -- results are wrong)
   const char* diag = getenv("HMM355_VIT_TAIL_DIAG");
   va.vdiag = diag ? (atoi(diag) & ~1) : 0;
+  // psi followers: the caller's word that the plan is dense, N <= 128, and CUs beside the chain
+  if ((flags & HMM355_VIT_PLAN_DENSE) && plan && NP <= 128 && !tail) {
+    const long room = (long)device_cus() - B;
+    const long tasks = (long)B * nc;
+    va.nfollow = (int)(room < tasks ? (room > 0 ? room : 0) : tasks);
+    va.prog = prog;
+    va.done = done;
+  }
   hipError_t e;
   switch (NP) {
     case 64: e = launch_vit<64>(va, plan == nullptr, false, sm); break;

@@ -28,6 +28,8 @@ OBS_LOG = nat.OBS_LOG
 FB_POSTERIOR = nat.FB_POSTERIOR
 FB_PAIR = nat.FB_PAIR
 VIT_PLAN_BANDED = nat.VIT_PLAN_BANDED
+VIT_PLAN_DENSE = nat.VIT_PLAN_DENSE
+_VIT_FOLLOW_DEFAULT = "0"  # psi followers for dense plans (off until measured faster)
 FB_FORWARD = nat.FB_FORWARD
 FB_BACKWARD = nat.FB_BACKWARD
 
@@ -156,6 +158,11 @@ def viterbi(obs: Tensor, log_P: Tensor, init: Tensor, obs_mode: int,
     # than the two launches they replace.
     flags = VIT_PLAN_BANDED if (plan is not None and getattr(plan, "_hmm355_banded", False)
                                 and os.environ.get("HMM355_VIT_TAIL", "0") == "1") else 0
+    # a dense plan: the argmax pointers computed beside the chain, on the CUs it leaves
+    # (HMM355_VIT_FOLLOW; _VIT_FOLLOW_DEFAULT: DESIGN.md round 4 item 15)
+    if (plan is not None and not getattr(plan, "_hmm355_banded", True)
+            and os.environ.get("HMM355_VIT_FOLLOW", _VIT_FOLLOW_DEFAULT) != "0"):
+        flags |= VIT_PLAN_DENSE
     with torch.cuda.device(dev):
         nat.check(L.hmm355_viterbi_plan_ex_f32(
             nat.ptr(obs), obs_mode, nat.ptr(log_P), nat.ptr(init), nat.ptr(plan), flags, B, T, N,

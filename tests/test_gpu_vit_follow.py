@@ -1,0 +1,104 @@
+"""GPU: psi followers (HMM355_VIT_PLAN_DENSE; csrc/vit_kern.h vit_psi_follow) -- the argmax
+pointers of a dense chain computed beside it by extra workgroups of the chain's launch, which
+follow the rows the chain's helpers publish.  Checked bit-exact against the C oracle
+(hmm.py:154-184) with the followers on and off, at chunk edges, with a batch larger than the
+CUs left for followers, and with the flag given for a banded plan (the followers step aside)."""
+import ctypes
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import hmm_oracle as O
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def _dense(N, seed):
+    rng = np.random.default_rng(seed)
+    return torch.from_numpy(rng.random((N, N), dtype=np.float32))
+
+
+def _run(lo, lP, lp0, plan, follow, monkeypatch, mode=None):
+    from pytorch_hmm_amd import ops
+    monkeypatch.setenv("HMM355_VIT_FOLLOW", "1" if follow else "0")
+    x = torch.from_numpy(lo).to(DEV)
+    s, d, f = ops.viterbi(x, lP.to(DEV), lp0.to(DEV), ops.OBS_LOG if mode is None else mode, plan)
+    torch.cuda.synchronize()
+    return s.cpu().numpy(), d.cpu().numpy(), f.cpu().numpy()
+
+
+@pytest.mark.parametrize("N", [128, 100, 64, 37])
+@pytest.mark.parametrize("T", [1, 2, 63, 64, 65, 129, 1000])
+def test_followers_vs_c_oracle(N, T, monkeypatch):
+    from pytorch_hmm_amd import ops
+    lP, lp0 = O.hmm_params(_dense(N, N + T))
+    plan = ops.make_plan(lP.to(DEV))
+    assert not plan._hmm355_banded
+    rng = np.random.default_rng(T)
+    B = 5
+    lo = np.log(rng.random((B, T, N), dtype=np.float32) + np.float32(1e-3)).astype(np.float32)
+    cs, cd, _ = O.c_viterbi(lo, lP.numpy(), lp0.numpy())
+    for follow in (True, False):  # (HMM355_VIT_FOLLOW overrides the default either way)
+        s, d, f = _run(lo, lP, lp0, plan, follow, monkeypatch)
+        assert np.array_equal(d, cd), follow
+        assert np.array_equal(s, cs), follow
+        assert np.array_equal(f, cd[:, -1].max(-1)), follow
+
+
+def test_followers_tie_heavy_and_large_batch(monkeypatch):
+    """Coarse emissions (many equal trellis values: the first index on ties) and B = 300, more
+    sequences than CUs: no room for followers, the pass after the chain does every chunk."""
+    from pytorch_hmm_amd import ops
+    N = 128
+    lP, lp0 = O.hmm_params(_dense(N, 3))
+    plan = ops.make_plan(lP.to(DEV))
+    for B, T in ((8, 2000), (300, 130)):
+        rng = np.random.default_rng(B)
+        lo = np.round(-(rng.random((B, T, N)) * 4), 0).astype(np.float32)
+        cs, cd, _ = O.c_viterbi(lo, lP.numpy(), lp0.numpy())
+        s, d, _ = _run(lo, lP, lp0, plan, True, monkeypatch)
+        assert np.array_equal(d, cd) and np.array_equal(s, cs), B
+
+
+def test_dense_flag_with_banded_plan(monkeypatch):
+    """The flag with a banded plan: the followers see a banded chain and leave; the psi pass
+    after the chain does its usual work."""
+    import pytorch_hmm_amd._native as nat
+    from pytorch_hmm_amd import ops
+    N, B, T = 128, 3, 300
+    lP, lp0 = O.hmm_params(O.left_to_right_matrix(N, 0.7))
+    lPd = lP.to(DEV)
+    plan = ops.make_plan(lPd)
+    assert plan._hmm355_banded
+    rng = np.random.default_rng(1)
+    lo = np.log(rng.random((B, T, N), dtype=np.float32) + np.float32(1e-3)).astype(np.float32)
+    obs = torch.from_numpy(lo).to(DEV)
+    L = nat.lib()
+    states = torch.zeros(B, T, dtype=torch.int64, device=DEV)
+    delta = torch.empty(B, T, N, device=DEV)
+    final = torch.zeros(B, device=DEV)
+    ws = torch.empty(L.hmm355_viterbi_workspace_bytes(B, T, N), dtype=torch.uint8, device=DEV)
+    p = lambda t: ctypes.c_void_p(t.data_ptr())
+    rc = L.hmm355_viterbi_plan_ex_f32(p(obs), ops.OBS_LOG, p(lPd), p(lp0.to(DEV)), p(plan), nat.VIT_PLAN_DENSE,
+                                      B, T, N, p(states), p(delta), p(final), p(ws), ws.numel(),
+                                      nat.stream_of(torch.device(DEV, 0)))
+    assert rc == 0
+    torch.cuda.synchronize()
+    cs, cd, _ = O.c_viterbi(lo, lP.numpy(), lp0.numpy())
+    assert np.array_equal(delta.cpu().numpy(), cd) and np.array_equal(states.cpu().numpy(), cs)
+
+
+def test_followers_obs_prob(monkeypatch):
+    """OBS_PROB (the chain's helpers take log(x + 1e-8)): followers on and off agree."""
+    from pytorch_hmm_amd import ops
+    N, B, T = 128, 6, 777
+    lP, lp0 = O.hmm_params(_dense(N, 11))
+    plan = ops.make_plan(lP.to(DEV))
+    g = torch.Generator().manual_seed(2)
+    x = torch.softmax(torch.randn(B, T, N, generator=g), -1).numpy()
+    a = _run(x, lP, lp0, plan, True, monkeypatch, ops.OBS_PROB)
+    b = _run(x, lP, lp0, plan, False, monkeypatch, ops.OBS_PROB)
+    for u, v in zip(a, b):
+        assert np.array_equal(u, v)
