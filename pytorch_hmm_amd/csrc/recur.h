@@ -860,18 +860,16 @@ __device__ __forceinline__ void rec_run_bc(const RecArgs& a, float* lds, int b) 
 //   item 4       the log-scale scan of block kb - 2 (every helper keeps its own running base;
 //                the last one writes LS)
 //   item 5, 6    flush block kb - 2, rows 0..7 and 8..15
-//   item 7       (Viterbi with psi followers) publish the flushed blocks, once per chunk
+//   (Viterbi with psi followers: item 0 also publishes the blocks flushed a block earlier,
+//   once per chunk)
 // Barriers: the helpers pass exactly the chain's barriers (two before the loop, one per step,
 // one after), so the s_barrier counts of all waves agree.  The last two blocks are flushed by
 // the helpers after the loop, and the FB log-likelihood (which needs the running base) is
 // written by the last helper.
-// items per block: 7 (FB), 8 (Viterbi: the psi followers' publish); HMM355_RB_ITEMS_FB is a
-// diagnostic override
-#ifndef HMM355_RB_ITEMS_FB
-#define HMM355_RB_ITEMS_FB 7
-#endif
+// items per block.  (An eighth, empty item per block measured 58 ns per step slower on the
+// dense FB chain, 828 -> 944 us per op, profiles/r4k_ops.log: the publish rides on item 0.)
 template <int KIND>
-constexpr int kRbItems = KIND == kVit ? 8 : HMM355_RB_ITEMS_FB;
+constexpr int kRbItems = 7;
 
 template <int NP, int KIND>
 __device__ __forceinline__ void rec_rb_helper(const RecArgs& a, float* lds, int b) {
@@ -912,7 +910,12 @@ __device__ __forceinline__ void rec_rb_helper(const RecArgs& a, float* lds, int 
   auto item = [&](int kb, int it, float(&cur)[2][5], float(&nxt)[2][5]) {
     // cur: block kb + 1's rows (loaded a block ago); nxt: block kb + 2's (loaded now)
     switch (it) {
-      case 0: if (kb + 1 < nblocks) rec_stage<NP, KIND>(a, lds, kb + 1, 2 * h, l, cur[0]); break;
+      case 0:
+        if (kb + 1 < nblocks) rec_stage<NP, KIND>(a, lds, kb + 1, 2 * h, l, cur[0]);
+        // (Viterbi with psi followers) blocks 0 .. kb - 3 were flushed in block kb - 1, before
+        // the barriers since: publish them once per chunk
+        if (kb >= 3 && ((kb - 2) & 3) == 0) publish(kb - 2);
+        break;
       case 1: if (kb + 1 < nblocks) rec_stage<NP, KIND>(a, lds, kb + 1, 2 * h + 1, l, cur[1]); break;
       case 2: rec_load<NP, KIND>(a, b, kb + 2 < nblocks ? kb + 2 : nblocks - 1, 2 * h, l, nxt[0]); break;
       case 3: rec_load<NP, KIND>(a, b, kb + 2 < nblocks ? kb + 2 : nblocks - 1, 2 * h + 1, l, nxt[1]); break;
@@ -923,9 +926,6 @@ __device__ __forceinline__ void rec_rb_helper(const RecArgs& a, float* lds, int 
           rec_flush<NP, KIND>(a, lds, b, kb - 2, th + NH * kWave, lsv);
           flushed();
         }
-        break;
-      case 7:  // (after the barrier that follows every helper's flush of block kb - 2)
-        if (kb >= 2 && ((kb - 1) & 3) == 0) publish(kb - 1);  // blocks 0 .. kb - 2 are out
         break;
       default: break;
     }
