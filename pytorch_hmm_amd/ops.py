@@ -29,7 +29,7 @@ FB_POSTERIOR = nat.FB_POSTERIOR
 FB_PAIR = nat.FB_PAIR
 VIT_PLAN_BANDED = nat.VIT_PLAN_BANDED
 VIT_PLAN_DENSE = nat.VIT_PLAN_DENSE
-_VIT_FOLLOW_DEFAULT = "0"  # psi followers for dense plans (off until measured faster)
+_VIT_FOLLOW_DEFAULT = "1"  # psi followers for dense plans (config 3: 65.2 -> 68.2 M frames/s)
 FB_FORWARD = nat.FB_FORWARD
 FB_BACKWARD = nat.FB_BACKWARD
 
