@@ -214,7 +214,7 @@ struct G4 {
   static constexpr int XV = (FT * kG4Dc + NT - 1) / NT;          // floats staged per thread
 };
 
-template <int FG, int NW, int kG4Nf>
+template <int FG, int NW, int kG4Nf, bool REGP = false>
 __global__ void __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(kG4Nf >= 16 ? 2 : 3))) gmm_score4_kernel(const float* __restrict__ x,
                                                              const double* __restrict__ pw,
                                                              const double* __restrict__ pmw,
@@ -249,6 +249,27 @@ __global__ void __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(kG
                                        reinterpret_cast<void*>(&ps[buf][i * 64]), 16, 0, 0);
     }
   };
+  // (REGP, diagnostic: the parameters through registers, loaded with the frames when a chunk
+  // starts and stored to LDS when its reads end -- no LDS-DMA in flight during the reads)
+  constexpr int PV = REGP ? (2 * kG4Dc * G::CG / 2 + G::NT - 1) / G::NT : 1;
+  double2 pre_p[PV];
+  auto fetch_preg = [&](int dc) {
+#pragma unroll
+    for (int r = 0; r < PV; ++r) {
+      const int e = tid + r * G::NT;
+      const int cle = e % G::CL, rest = e / G::CL;
+      const int h = rest & 1, k = (rest >> 1) % kG4Dc, a = rest / (2 * kG4Dc);
+      const double* src = (a ? pmw : pw) + (size_t)(dc * kG4Dc + k) * PP + g0 + 4 * cle + 2 * h;
+      pre_p[r] = e < G::PS ? *reinterpret_cast<const double2*>(src) : make_double2(0.0, 0.0);
+    }
+  };
+  auto stage_preg = [&](int buf) {
+#pragma unroll
+    for (int r = 0; r < PV; ++r) {
+      const int e = tid + r * G::NT;
+      if (e < G::PS) ps[buf][e] = pre_p[r];
+    }
+  };
   float pre_x[G::XV];
   auto fetch_x = [&](int dc) {
 #pragma unroll
@@ -277,7 +298,12 @@ __global__ void __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(kG
 #pragma unroll
     for (int f = 0; f < kG4Nf; ++f) q[j][f] = 0.0;
 
-  fetch_params(0, 0);
+  if constexpr (REGP) {
+    fetch_preg(0);
+    stage_preg(0);
+  } else {
+    fetch_params(0, 0);
+  }
   fetch_x(0);
   stage_x(0);
   __syncthreads();
@@ -285,7 +311,10 @@ __global__ void __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(kG
     const int buf = dc & 1;
     // the frames of chunk dc + 1 into registers now; its parameters (LDS-DMA) after this chunk's
     // reads: an LDS-DMA in flight makes the compiler wait for it before every LDS read
-    if (dc + 1 < NDC) fetch_x(dc + 1);
+    if (dc + 1 < NDC) {
+      fetch_x(dc + 1);
+      if constexpr (REGP) fetch_preg(dc + 1);
+    }
     const double2* pb = ps[buf];
     const double* xb = xs[buf] + fblk * G::XROW;
 #pragma unroll 1
@@ -320,7 +349,8 @@ __global__ void __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(kG
     }
     if (dc + 1 < NDC) {
       // the other buffers' last readers passed the barrier that ended chunk dc - 1
-      fetch_params(dc + 1, buf ^ 1);
+      if constexpr (REGP) stage_preg(buf ^ 1);
+      else fetch_params(dc + 1, buf ^ 1);
       stage_x(buf ^ 1);
       __syncthreads();
     }
@@ -362,12 +392,12 @@ __global__ void __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(kG
   }
 }
 
-template <int FG, int NW, int NF>
+template <int FG, int NW, int NF, bool REGP = false>
 static hipError_t launch_g4(const float* x, const double* pw, const double* pmw, const double* cst, float* out,
                             int nframes, int D, int NDC, int S, int C, int P, int PP, int mix_lse, hipStream_t st) {
   using G = G4<FG, NW, NF>;
   dim3 grid((unsigned)(((size_t)nframes + G::FT - 1) / G::FT), (unsigned)((P + G::CG - 1) / G::CG));
-  hipLaunchKernelGGL((gmm_score4_kernel<FG, NW, NF>), grid, dim3(G::NT), 0, st, x, pw, pmw, cst, out, nframes, D, NDC,
+  hipLaunchKernelGGL((gmm_score4_kernel<FG, NW, NF, REGP>), grid, dim3(G::NT), 0, st, x, pw, pmw, cst, out, nframes, D, NDC,
                      S, C, P, PP, mix_lse);
   return hipGetLastError();
 }
@@ -448,11 +478,15 @@ HMM355_API int hmm355_gmm_diag_logprob_f32(const float* x, const float* means, c
     // defaults from tools/time_gmm.py (profiles/r4h_gmm2.log): config 3 (P = 512) 326 us with
     // 16 frames per lane; P = 64 (configs 2, 5) 57 / 34 us with 4 (the work is small: more waves)
     if (CG == 256) {
-      e = cfg == 2 ? G4L(1, 4, 8) : cfg == 3 ? G4L(1, 2, 16) : cfg == 4 ? G4L(1, 1, 16) : G4L(1, 4, 16);
+      e = cfg == 2 ? G4L(1, 4, 8) : cfg == 3 ? G4L(1, 2, 16) : cfg == 4 ? G4L(1, 1, 16)
+        : cfg == 5 ? launch_g4<1, 4, 16, true>(x, w.pw, w.pmw, w.cst, out, nframes, D, NDC, S, C, P, PP, mix_lse, st)
+                   : G4L(1, 4, 16);
     } else if (CG == 128) {
       e = cfg == 2 ? G4L(2, 2, 16) : cfg == 3 ? G4L(2, 1, 8) : G4L(2, 2, 8);
     } else {
-      e = cfg == 2 ? G4L(4, 2, 8) : cfg == 3 ? G4L(4, 1, 4) : cfg == 4 ? G4L(4, 2, 16) : G4L(4, 2, 4);
+      e = cfg == 2 ? G4L(4, 2, 8) : cfg == 3 ? G4L(4, 1, 4) : cfg == 4 ? G4L(4, 2, 16)
+        : cfg == 5 ? launch_g4<4, 2, 4, true>(x, w.pw, w.pmw, w.cst, out, nframes, D, NDC, S, C, P, PP, mix_lse, st)
+                   : G4L(4, 2, 4);
     }
 #undef G4L
     return e == hipSuccess ? HMM355_OK : (int)e;

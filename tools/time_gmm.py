@@ -18,7 +18,7 @@ for name, (B, T, D, S, C) in shapes.items():
     lv = torch.randn(S, C, D, device=dev, generator=g) * 0.3
     lw = torch.log_softmax(torch.randn(S, C, device=dev, generator=g), -1)
     ref = None
-    for cfg in ("0", "1", "2", "3", "4"):
+    for cfg in ("0", "1", "2", "3", "4", "5"):
         os.environ["HMM355_GMM_CFG"] = cfg
         out = ops.gmm_diag_logprob(x, mu, lv, lw, 1 if C > 1 else 0)
         torch.cuda.synchronize()
