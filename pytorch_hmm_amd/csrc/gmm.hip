@@ -231,12 +231,13 @@ __global__ void __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(kG
   const size_t f0 = (size_t)blockIdx.x * G::FT;
   const int fblk = w * FG + fg;  // this lane's 16-frame block in the tile
 
-  // Parameters go global -> LDS directly (global_load_lds_dwordx4: no staging registers, no
-  // LDS stores): one wave instruction fills 64 consecutive double2 of the buffer, element
-  // e = ((a*8 + k)*2 + h)*CL + cl holding components g0 + 4cl + 2h, +1 of array a at dim k.
-  // The frames go through registers (fp32 -> fp64 on the way into LDS), loaded when chunk dc
-  // starts; the parameters of chunk dc + 1 are issued when its reads end.  __syncthreads (which
-  // waits for vmcnt(0)) publishes both.
+  // Parameter buffer element e = ((a*8 + k)*2 + h)*CL + cl holds components g0 + 4cl + 2h, +1
+  // of array a at dim k.  REGP (the default): the parameters and the frames (fp32 -> fp64 on
+  // the way into LDS) of chunk dc + 1 are loaded into registers when chunk dc starts and stored
+  // to the other LDS buffers when its reads end.  Otherwise the parameters go global -> LDS
+  // directly (global_load_lds_dwordx4, one wave instruction per 64 consecutive double2), issued
+  // when the chunk's reads end: an LDS-DMA in flight makes the compiler wait for it before every
+  // LDS read, so it cannot overlap them (4-7 % slower).  __syncthreads publishes both.
   constexpr int PI = G::PS / 64;  // wave instructions per parameter buffer
   auto fetch_params = [&](int dc, int buf) {
     for (int i = w; i < PI; i += NW) {
@@ -475,19 +476,22 @@ HMM355_API int hmm355_gmm_diag_logprob_f32(const float* x, const float* means, c
   if (!gmm_use_v1(C)) {
     static_assert(G4<1, 4, 16>::CG == 256 && G4<2, 2, 16>::CG == 128 && G4<4, 2, 16>::CG == 64, "gmm_v2_group");
 #define G4L(fg, nw, nf) launch_g4<fg, nw, nf>(x, w.pw, w.pmw, w.cst, out, nframes, D, NDC, S, C, P, PP, mix_lse, st)
-    // defaults from tools/time_gmm.py (profiles/r4h_gmm2.log): config 3 (P = 512) 326 us with
+    // shapes from tools/time_gmm.py (profiles/r4h_gmm2.log): config 3 (P = 512) 326 us with
     // 16 frames per lane; P = 64 (configs 2, 5) 57 / 34 us with 4 (the work is small: more waves)
+    // (round 4, profiles/r4m_gmm_regp.log: the parameters staged through registers, config 5
+    // below and the default, beat the LDS-DMA staging, config 1, by 4-7 %: 311 / 54 / 31 us per
+    // call at configs 3 / 2 / 5; identical bits)
+#define G4R(fg, nw, nf) launch_g4<fg, nw, nf, true>(x, w.pw, w.pmw, w.cst, out, nframes, D, NDC, S, C, P, PP, mix_lse, st)
     if (CG == 256) {
-      e = cfg == 2 ? G4L(1, 4, 8) : cfg == 3 ? G4L(1, 2, 16) : cfg == 4 ? G4L(1, 1, 16)
-        : cfg == 5 ? launch_g4<1, 4, 16, true>(x, w.pw, w.pmw, w.cst, out, nframes, D, NDC, S, C, P, PP, mix_lse, st)
-                   : G4L(1, 4, 16);
+      e = cfg == 1 ? G4L(1, 4, 16) : cfg == 2 ? G4L(1, 4, 8) : cfg == 3 ? G4L(1, 2, 16) : cfg == 4 ? G4L(1, 1, 16)
+                   : G4R(1, 4, 16);
     } else if (CG == 128) {
-      e = cfg == 2 ? G4L(2, 2, 16) : cfg == 3 ? G4L(2, 1, 8) : G4L(2, 2, 8);
+      e = cfg == 1 ? G4L(2, 2, 8) : cfg == 2 ? G4L(2, 2, 16) : cfg == 3 ? G4L(2, 1, 8) : G4R(2, 2, 8);
     } else {
-      e = cfg == 2 ? G4L(4, 2, 8) : cfg == 3 ? G4L(4, 1, 4) : cfg == 4 ? G4L(4, 2, 16)
-        : cfg == 5 ? launch_g4<4, 2, 4, true>(x, w.pw, w.pmw, w.cst, out, nframes, D, NDC, S, C, P, PP, mix_lse, st)
-                   : G4L(4, 2, 4);
+      e = cfg == 1 ? G4L(4, 2, 4) : cfg == 2 ? G4L(4, 2, 8) : cfg == 3 ? G4L(4, 1, 4) : cfg == 4 ? G4L(4, 2, 16)
+                   : G4R(4, 2, 4);
     }
+#undef G4R
 #undef G4L
     return e == hipSuccess ? HMM355_OK : (int)e;
   }
