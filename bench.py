@@ -429,8 +429,9 @@ def layer_workload(args, rank, world, dev):
             kroof = {"note": f"torch.profiler unavailable: {type(exc).__name__}"}
     if kroof is not None and "frac" in kroof:
         roof = kroof
-        if roof.get("bound") == "hbm":
-            roof["traffic"], roof["traffic_source"] = profiled_kernel_traffic(roof.get("kernel"), desc)
+        # the committed PMC bytes of the same kernel (for a VALU-bound kernel too: HBM bytes far
+        # above its algorithmic bytes would still be the first thing to fix)
+        roof["traffic"], roof["traffic_source"] = profiled_kernel_traffic(roof.get("kernel"), desc)
     elif flops is not None:
         achieved = flops / (step_ms * 1e-3) / 1e12
         roof = {"bound": "valu", "kernel": dom, "achieved": achieved, "peak": VALU_PEAK_TFLOPS, "unit": "TFLOP/s",
