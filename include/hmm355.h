@@ -78,8 +78,12 @@ size_t hmm355_fb_workspace_bytes(int B, int T, int N);
  *              (pytorch_hmm_amd/autograd.py; replaces the reference's autograd through
  *              hmm.py:89-101 for compute_likelihood / HMMLayer.compute_loss, hmm_layer.py:144-173).
  * Workspace layout (256-B aligned pieces, in order): U (B,T,NP) scaled alpha rows | V
- * (B,T,NP) scaled beta rows | LA (B,T) | LB (B,T) | ... ; alpha_t = U_t exp(LA_t),
- * beta_t = V_t exp(LB_t), NP = N padded to 64/128/256.  With obs_mode == HMM355_OBS_LOG
+ * (B,T,NP) scaled beta rows | LA (B,T) | LB (B,T) | BandDesc (hmm355_plan_bytes(N)) |
+ * (B,NP) | (B) | (B,T) | CA (B,T) | CB (B,T); alpha_t = U_t exp(LA_t), beta_t = V_t exp(LB_t),
+ * NP = N padded to 64/128/256.  CA / CB are the steps' normalisers by time:
+ * U_{t+1} = (A^T U_t) e_{t+1} / CA_t  (t <= T-2)  and  V_{t-1} = A (e_t V_t) / CB_t  (t >= 1),
+ * A = exp(log_P) -- the chains do not normalise every row to sum 1 (the dense chain applies a
+ * scale predicted a step ahead), so an adjoint takes its step factors from CA / CB.  With obs_mode == HMM355_OBS_LOG
  * the chains use the shifted emissions e_t = exp(obs_t - M_t), M_t = max_j obs_t[j] (a row
  * without a finite maximum: M_t = 0), and LA / LB carry the shifts, so log-emissions far
  * below -87 do not underflow; U and V are the rows of that shifted recursion. */

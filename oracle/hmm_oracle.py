@@ -209,20 +209,31 @@ def _mix_lse(x, dim):
     return _safe_log(s) + m.squeeze(dim)
 
 
-def mixture_log_probs(x, mixture_weights_logits, means, log_vars, t_chunk=None):
-    """mixture_gaussian.py:157-214 (diag).  t_chunk evaluates the (B,T,S,C,D) broadcast in
-    slices of T (identical per-element ops; bounds host memory at full size)."""
+def mixture_log_probs(x, mixture_weights_logits, means, log_vars, t_chunk=None, covariance_type="diag"):
+    """mixture_gaussian.py:157-214 (diag :200-214, tied :242-253, spherical :255-269).  t_chunk
+    evaluates the (B,T,S,C,D) broadcast in slices of T (identical per-element ops; bounds host
+    memory at full size)."""
     B, T, D = x.shape
     log_w = _safe_log(F.softmax(mixture_weights_logits, dim=-1))
     var = torch.exp(log_vars)
-    const = torch.sum(log_vars, dim=-1).unsqueeze(0).unsqueeze(0)
     outs = []
     step = T if not t_chunk else t_chunk
     for t0 in range(0, T, step):
         xe = x[:, t0:t0 + step].unsqueeze(2).unsqueeze(3)
         diff = xe - means.unsqueeze(0).unsqueeze(0)
-        comp = -0.5 * (torch.sum(diff ** 2 / var.unsqueeze(0).unsqueeze(0), dim=-1) + const
-                       + D * math.log(2 * math.pi))
+        if covariance_type == "diag":
+            const = torch.sum(log_vars, dim=-1).unsqueeze(0).unsqueeze(0)
+            comp = -0.5 * (torch.sum(diff ** 2 / var.unsqueeze(0).unsqueeze(0), dim=-1) + const
+                           + D * math.log(2 * math.pi))
+        elif covariance_type == "tied":
+            comp = -0.5 * (torch.sum(diff ** 2 / var.unsqueeze(0).unsqueeze(0).unsqueeze(0).unsqueeze(0), dim=-1)
+                           + torch.sum(log_vars) + D * math.log(2 * math.pi))
+        elif covariance_type == "spherical":
+            ve = var.unsqueeze(0).unsqueeze(0).unsqueeze(-1)
+            comp = -0.5 * (torch.sum(diff ** 2, dim=-1) / ve.squeeze(-1)
+                           + D * log_vars.unsqueeze(0).unsqueeze(0) + D * math.log(2 * math.pi))
+        else:
+            raise ValueError(covariance_type)
         outs.append(_mix_lse(comp + log_w.unsqueeze(0).unsqueeze(0), dim=-1))
     return torch.cat(outs, dim=1)
 

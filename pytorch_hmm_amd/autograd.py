@@ -60,16 +60,22 @@ def _run_fb(obs, log_P, log_p0, obs_mode, log_beta_T=None, posterior=False, out_
             mask, nat.ptr(post), nat.ptr(fwd), nat.ptr(bwd), nat.ptr(loglik), nat.ptr(lik_ref),
             nat.ptr(ws), ws.numel(), nat.stream_of(dev)))
     rows = B * T
-    # workspace layout: U | V (B,T,NP) then LA | LB (B,T), pieces 256-B aligned (hmm355.h)
+    # workspace layout (hmm355.h): U | V (B,T,NP) | LA | LB (B,T) | BandDesc | (B,NP) | (B) |
+    # (B,T) | CA | CB (B,T), pieces 256-B aligned
+    al = lambda n: ((n + 255) // 256) * 256
     fl = ws.view(torch.float32)
     U = fl[: rows * NP].view(B, T, NP)[..., :N]
     V = fl[rows * NP: 2 * rows * NP].view(B, T, NP)[..., :N]
-    off = ((2 * rows * NP * 4 + 255) // 256) * 256 // 4
+    off = al(2 * rows * NP * 4) // 4
     LA = fl[off: off + rows].view(B, T)
     LB = fl[off + rows: off + 2 * rows].view(B, T)
+    offc = (al(2 * rows * NP * 4) + al(2 * rows * 4) + al(L.hmm355_plan_bytes(N)) + al(B * NP * 4) + al(B * 4)
+            + al(rows * 4)) // 4
+    CA = fl[offc: offc + rows].view(B, T)
+    CB = fl[offc + rows: offc + 2 * rows].view(B, T)
     if out_mask is not None:
-        return (post, fwd, bwd), loglik, lik_ref, U, V, LA, LB
-    return post, loglik, lik_ref, U, V, LA, LB
+        return (post, fwd, bwd), loglik, lik_ref, U, V, LA, LB, CA, CB
+    return post, loglik, lik_ref, U, V, LA, LB, CA, CB
 
 
 def _staged_emissions(obs, obs_mode):
@@ -90,7 +96,7 @@ class SequenceLogLik(torch.autograd.Function):
     def forward(ctx, obs, log_P, log_p0, obs_mode, kind):
         nat.require_gpu(obs, log_P, log_p0)
         obs_c, lP, l0 = (t.detach().to(torch.float32).contiguous() for t in (obs, log_P, log_p0))
-        _, loglik, lik_ref, _, _, _, _ = _run_fb(obs_c, lP, l0, obs_mode)
+        _, loglik, lik_ref, *_ = _run_fb(obs_c, lP, l0, obs_mode)
         ctx.save_for_backward(obs_c, lP, l0)
         ctx.obs_mode, ctx.kind = obs_mode, kind
         return lik_ref if kind == "ref" else loglik
@@ -99,7 +105,7 @@ class SequenceLogLik(torch.autograd.Function):
     def backward(ctx, gout):
         obs, lP, l0 = ctx.saved_tensors
         B, T, N = obs.shape
-        _, _, _, U, _, LA, _ = _run_fb(obs, lP, l0, ctx.obs_mode)
+        _, _, _, U, _, LA, _, _, _ = _run_fb(obs, lP, l0, ctx.obs_mode)
         a_last = torch.log(U[:, -1]) + LA[:, -1:]                 # log alpha_{T-1}  (B,N)
         if ctx.kind == "ref":
             f = torch.exp(a_last)                                 # the reference's forward[:, -1]
@@ -111,7 +117,7 @@ class SequenceLogLik(torch.autograd.Function):
             g = torch.softmax(a_last, dim=-1)
             log_mu = torch.zeros_like(a_last)
         G = g.sum(-1) * gout                                      # (B,)
-        post, _, _, U, V, _, _ = _run_fb(obs, lP, l0, ctx.obs_mode, log_beta_T=log_mu.contiguous(),
+        post, _, _, U, V, _, _, CA, _ = _run_fb(obs, lP, l0, ctx.obs_mode, log_beta_T=log_mu.contiguous(),
                                          posterior=True)
         grad_lo = G[:, None, None] * post
         if ctx.obs_mode == nat.OBS_PROB:
@@ -127,7 +133,7 @@ class SequenceLogLik(torch.autograd.Function):
         grad_l0 = (G[:, None] * post[:, 0]).sum(0)
         grad_lP = None
         if T > 1 and ctx.needs_input_grad[1]:
-            c = U.sum(-1)                                         # c_t = sum_j u_t(j)   (B,T)
+            c = CA                                                # U_{t+1} = A^T U_t e_{t+1} / c_t
             S = (U * V).sum(-1)                                   # (B,T)
             X = U[:, :-1] / (c[:, :-1] * S[:, 1:]).unsqueeze(-1) * G[:, None, None]
             Y = e[:, 1:] * V[:, 1:]
@@ -223,11 +229,13 @@ class TvSequenceLogLik(torch.autograd.Function):
         return grad_lo, grad_A, grad_l0, None
 
 
-def _adjoint_sources(U, V, E, post, fwd, bwd, gp, gf, gb):
+def _adjoint_sources(U, V, E, post, fwd, bwd, gp, gf, gb, CA=None, CB=None):
     """Per-step sources and scales of the two adjoint chains (ForwardBackwardFn's docstring):
     srcW = v (Gp - <gamma, Gp>) / sum(u v) + Gf exp(LA), srcZ = u (Gp - <gamma, Gp>) / sum(u v)
     + Gb exp(LB) (Gf exp(LA) = Gf forward / u), Fw_t = 1 / sum u_t, Fz_t = 1 / sum v_t E_t
-    (t >= 1).  Formed in fp64 from the stored fp32 rows, returned as contiguous fp32."""
+    (t >= 1).  Formed in fp64 from the stored fp32 rows, returned as contiguous fp32.  The step
+    factors are the chains' own normalisers CA / CB (hmm355.h; the dense chain's rows do not sum
+    to 1, so they are not the row sums there)."""
     B, T, N = U.shape
     U64, V64 = U.double(), V.double()
     Suv = (U64 * V64).sum(-1, keepdim=True)
@@ -245,10 +253,14 @@ def _adjoint_sources(U, V, E, post, fwd, bwd, gp, gf, gb):
     if gb is not None:
         srcZ += torch.where(V64 > 0, gb.double() * bwd.double() / torch.where(V64 > 0, V64, torch.ones_like(V64)),
                             torch.zeros_like(V64))
-    Fw = (1.0 / U64.sum(-1)).float().contiguous()                              # 1/c_t
-    Fz = torch.zeros(B, T, device=U.device)
+    Fw = torch.zeros(B, T, device=U.device)                                    # 1/c_t (t <= T-2)
+    Fz = torch.zeros(B, T, device=U.device)                                    # 1/c'_{t-1} (t >= 1)
     if T > 1:
-        Fz[:, 1:] = (1.0 / (V64[:, 1:] * E[:, 1:].double()).sum(-1)).float()   # 1/c'_{t-1}
+        # (CA / CB None: chains that normalise every step exactly, c_t = sum u_t -- csrc/tv.hip)
+        ca = CA[:, :-1].double() if CA is not None else U64[:, :-1].sum(-1)
+        cb = CB[:, 1:].double() if CB is not None else (V64[:, 1:] * E[:, 1:].double()).sum(-1)
+        Fw[:, :-1] = (1.0 / ca).float()
+        Fz[:, 1:] = (1.0 / cb).float()
     return srcW.float().contiguous(), Fw, srcZ.float().contiguous(), Fz
 
 
@@ -265,8 +277,10 @@ class ForwardBackwardFn(torch.autograd.Function):
         k_t = gamma_t (Gp_t - <gamma_t, Gp_t>) + Gb_t exp(b_t)     (of b_t).
     The total adjoint of a_t is alpha_t * W_t e^{-LA_t}, W the forward recursion's adjoint in
     alpha's scaling, and that of b_t is beta_t * Z_t e^{-LB_t}:
-        W_{t-1} = h_{t-1} / u_{t-1} + (1/c_{t-1}) A (E_t W_t),          c_t = sum u_t
-        Z_{t+1} = k_{t+1} / v_{t+1} + (1/c'_t) E_{t+1} (A^T Z_t),       c'_t = sum v_{t+1} E_{t+1}
+        W_{t-1} = h_{t-1} / u_{t-1} + (1/c_{t-1}) A (E_t W_t),          c_t = CA_t
+        Z_{t+1} = k_{t+1} / v_{t+1} + (1/c'_t) E_{t+1} (A^T Z_t),       c'_t = CB_{t+1}
+    with c, c' the chains' step normalisers (u_{t+1} = A^T u_t E_{t+1} / c_t, v_t = A E_{t+1}
+    v_{t+1} / c'_t; hmm355.h workspace CA / CB)
     (hmm355_fb_adjoint_f32), where h/u = v (Gp - <.,.>) / sum(u v) + Gf exp(LA) and
     k/v = u (Gp - <.,.>) / sum(u v) + Gb exp(LB) are O(1) (no division by a vanishing u or v).
     Then, with P = Z - k/v the propagated part of Z,
@@ -280,9 +294,10 @@ class ForwardBackwardFn(torch.autograd.Function):
     def forward(ctx, obs, log_P, log_p0, obs_mode, out_mask, plan=None):
         nat.require_gpu(obs, log_P, log_p0)
         obs_c, lP, l0 = (t.detach().to(torch.float32).contiguous() for t in (obs, log_P, log_p0))
-        outs, _, _, U, V, _, _ = _run_fb(obs_c, lP, l0, obs_mode, out_mask=out_mask | nat.FB_POSTERIOR, plan=plan)
+        outs, _, _, U, V, _, _, CA, CB = _run_fb(obs_c, lP, l0, obs_mode, out_mask=out_mask | nat.FB_POSTERIOR,
+                                                 plan=plan)
         post, fwd, bwd = outs
-        ctx.save_for_backward(obs_c, lP, l0, U, V, post, fwd, bwd)
+        ctx.save_for_backward(obs_c, lP, l0, U, V, post, fwd, bwd, CA, CB)
         ctx.obs_mode, ctx.out_mask = obs_mode, out_mask
         ctx.set_materialize_grads(False)   # outputs the loss does not use arrive as None
         res = tuple(o for bit, o in ((nat.FB_POSTERIOR, post), (nat.FB_FORWARD, fwd), (nat.FB_BACKWARD, bwd))
@@ -291,14 +306,14 @@ class ForwardBackwardFn(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, *grads):
-        obs, lP, l0, U, V, post, fwd, bwd = ctx.saved_tensors
+        obs, lP, l0, U, V, post, fwd, bwd, CA, CB = ctx.saved_tensors
         B, T, N = obs.shape
         returned = [k for bit, k in ((nat.FB_POSTERIOR, "p"), (nat.FB_FORWARD, "f"), (nat.FB_BACKWARD, "b"))
                     if ctx.out_mask & bit]
         got = dict(zip(returned, grads))
         gp, gf, gb = got.get("p"), got.get("f"), got.get("b")
         E = _staged_emissions(obs, ctx.obs_mode).contiguous()
-        srcW, Fw, srcZ, Fz = _adjoint_sources(U, V, E, post, fwd, bwd, gp, gf, gb)
+        srcW, Fw, srcZ, Fz = _adjoint_sources(U, V, E, post, fwd, bwd, gp, gf, gb, CA, CB)
         W = torch.empty(B, T, N, device=obs.device)
         P = torch.empty(B, T, N, device=obs.device)
         L = nat.lib()

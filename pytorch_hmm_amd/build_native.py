@@ -29,12 +29,18 @@ def _hipcc():
     raise RuntimeError("hipcc not found")
 
 
-def build(force=False, verbose=False, defines=(), out=None):
+# the sources of the forward-backward / Viterbi entry points alone (diagnostic A/B builds, tools/ab.py)
+RECURSION_SOURCES = ["capi.hip", "fb.hip", "fb_np64.hip", "fb_np128.hip", "fb_np256.hip", "viterbi.hip",
+                     "vit_np64.hip", "vit_np128.hip", "vit_np256.hip"]
+
+
+def build(force=False, verbose=False, defines=(), out=None, sources=None):
     """Compile csrc/*.hip into `out` (default pytorch_hmm_amd/lib/libhmm355.so).
-    `defines` (e.g. ["HMM355_ABL=2"]) are for diagnostic builds only."""
+    `defines` (e.g. ["HMM355_ABL=2"]) and `sources` (a subset of SOURCES) are for diagnostic
+    builds only."""
     lib = out or LIB
     os.makedirs(os.path.dirname(lib), exist_ok=True)
-    srcs = [s for s in SOURCES if os.path.exists(os.path.join(CSRC, s))]
+    srcs = [s for s in (sources or SOURCES) if os.path.exists(os.path.join(CSRC, s))]
     # every header the sources include (csrc/*.h and the public header) is a dependency
     deps = ([os.path.join(CSRC, s) for s in srcs] + sorted(glob.glob(os.path.join(CSRC, "*.h"))) +
             [os.path.join(HERE, "..", "include", "hmm355.h"), os.path.abspath(__file__)])

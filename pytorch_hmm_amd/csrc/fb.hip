@@ -52,9 +52,9 @@ __global__ void __launch_bounds__(256) row_max_kernel(const float* __restrict__ 
 
 // Workspace layout (documented in include/hmm355.h for adjoint callers):
 //   U (B,T,NP) | V (B,T,NP) | LA (B,T) | LB (B,T) | BandDesc | beta init (B,NP) | its scale (B)
-//   | row maxima M (B,T) (OBS_LOG)
+//   | row maxima M (B,T) (OBS_LOG) | CA (B,T) | CB (B,T) (each step's normaliser, recur.h RecArgs::cs)
 struct FbWs {
-  float *U, *V, *LA, *LB, *binit, *bscale, *rmax;
+  float *U, *V, *LA, *LB, *binit, *bscale, *rmax, *CA, *CB;
   BandDesc* band;
 };
 static size_t fb_ws_layout(int B, int T, int N, char* base, FbWs* w) {
@@ -68,6 +68,7 @@ static size_t fb_ws_layout(int B, int T, int N, char* base, FbWs* w) {
   const size_t oI = take((size_t)B * NP * sizeof(float));
   const size_t oS = take((size_t)B * sizeof(float));
   const size_t oM = take(rows * sizeof(float));
+  const size_t oC = take(2 * rows * sizeof(float));
   if (w && base) {
     w->U = reinterpret_cast<float*>(base + oU);
     w->V = w->U + rows * NP;
@@ -77,6 +78,8 @@ static size_t fb_ws_layout(int B, int T, int N, char* base, FbWs* w) {
     w->binit = reinterpret_cast<float*>(base + oI);
     w->bscale = reinterpret_cast<float*>(base + oS);
     w->rmax = reinterpret_cast<float*>(base + oM);
+    w->CA = reinterpret_cast<float*>(base + oC);
+    w->CB = w->CA + rows;
   }
   return off;
 }
@@ -154,6 +157,8 @@ HMM355_API int hmm355_forward_backward_plan_f32(const float* obs, int obs_mode, 
   }
   RecArgs fa{obs, log_P, log_p0, w.U, w.LA, loglik, B, T, N, obs_mode, NP, band, nullptr, nullptr, nullptr, rmax, nullptr};
   RecArgs fb{obs, log_P, log_p0, w.V, w.LB, nullptr, B, T, N, obs_mode, NP, band, binit, bscale, nullptr, rmax, nullptr};
+  fa.cs = w.CA;  // each step's normaliser, by time (the adjoint's step factors, autograd.py)
+  fb.cs = w.CB;
   hipStream_t st0 = static_cast<hipStream_t>(stream);
   if ((out_mask & HMM355_FB_PAIR) && plan && band && NP <= 128 && !log_beta_T &&
       (size_t)T * NP * sizeof(float) < ((size_t)1 << 31)) {

@@ -846,6 +846,7 @@ __global__ void __launch_bounds__(64) hsmm_stitch_kernel(HsArgs a, HsChunks c) {
                             : make_int4(-1, -1, -1, 0);
       if (!tables) {  // (uniform: `at` comes from a ballot)
         hs_walk_tables(a, w, l);
+        __syncthreads();  // every lane reads entries other lanes wrote
         tables = true;
       }
       hs_walk<R, SMAX>(w, l, t, cs, cd, o, lo, [&](int et, int es, int ed, float eo, int start) {

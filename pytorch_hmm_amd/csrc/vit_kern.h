@@ -254,10 +254,14 @@ __global__ void __launch_bounds__(VF<NP>::NT) vit_psi_kernel(VitArgs a) {
 // stride of the follower count, waits until that sequence's chain has published the blocks
 // holding the chunk's rows (rec_rb_helper: once per chunk; acquire at agent scope, then a
 // workgroup barrier), computes the chunk's psi rows and map exactly as the pass after the chain does,
-// and marks the chunk done.  A wait is bounded (kFollowWait ticks of the 100 MHz real-time
-// counter): a chunk not reached in time is left to the pass after the chain, which computes
-// every chunk not marked done, so the result never depends on the followers' timing.
-constexpr long long kFollowWait = 20000000;  // 200 ms
+// and marks the chunk done.  Waits are bounded by ONE stall budget per launch: the clock
+// restarts whenever the awaited sequence's count moves, and a follower that sees no progress
+// for kFollowStall ticks of the 100 MHz real-time counter (2 ms: a published 64-step chunk
+// takes ~20-30 us) gives up ALL its remaining tasks.  A chain held back behind other work on
+// its XCD therefore costs each follower at most 2 ms of polling, never 2 ms per task.  Chunks a
+// follower does not finish are left to the pass after the chain, which computes every chunk
+// not marked done, so the result never depends on the followers' timing.
+constexpr long long kFollowStall = 200000;  // 2 ms
 
 template <int NP>
 __device__ __forceinline__ void vit_psi_follow(const RecArgs& ra, float* lds) {
@@ -272,6 +276,8 @@ __device__ __forceinline__ void vit_psi_follow(const RecArgs& ra, float* lds) {
   psi_dense_matrix<NP>(a, M);
   const int nf = (int)gridDim.x - a.B;
   const int ntask = a.B * a.nchunks;
+  int last_have = -1;
+  long long t0 = __builtin_amdgcn_s_memrealtime();
   for (int task = (int)blockIdx.x - a.B; task < ntask; task += nf) {
     const int chunk = task / a.B, b = task - chunk * a.B;
     const int t_lo = chunk * kChunk;
@@ -280,14 +286,17 @@ __device__ __forceinline__ void vit_psi_follow(const RecArgs& ra, float* lds) {
     const int need = t_hi >= 1 ? ((t_hi - 1) >> 4) + 1 : 0;
     if (threadIdx.x == 0) {
       int ok = 1;
-      const long long t0 = __builtin_amdgcn_s_memrealtime();
       // relaxed polls (no cache maintenance per poll), one agent-scope acquire once the count
       // is there (it invalidates this XCD's caches: once per task, not per poll)
       for (;;) {
         const int have = __hip_atomic_load(a.prog + (size_t)b * kProgSlots, __ATOMIC_RELAXED,
                                            __HIP_MEMORY_SCOPE_AGENT);
         if (have >= need) break;
-        if (__builtin_amdgcn_s_memrealtime() - t0 > kFollowWait) {
+        const long long now = __builtin_amdgcn_s_memrealtime();
+        if (have != last_have) {  // progress (or a new sequence): restart the stall clock
+          last_have = have;
+          t0 = now;
+        } else if (now - t0 > kFollowStall) {
           ok = 0;
           break;
         }
@@ -299,7 +308,7 @@ __device__ __forceinline__ void vit_psi_follow(const RecArgs& ra, float* lds) {
     __syncthreads();
     const int ok = *ok_slot;
     __syncthreads();  // (ok_slot is rewritten by the next task's wait)
-    if (!ok) continue;
+    if (!ok) return;  // stalled: every remaining task goes to the pass after the chain
     psi_dense_chunk<NP>(a, prow, M, b, chunk);
     __syncthreads();  // (prow is rewritten by the next task; the rows and map are issued)
     if (threadIdx.x == 0) a.done[(size_t)b * a.nchunks + chunk] = 1;

@@ -52,6 +52,8 @@ HMM355_API size_t hmm355_viterbi_workspace_bytes(int B, int T, int N) {
 
 // CUs of the current device (cached per device): the psi followers take the ones the chain
 // leaves, at most one workgroup per CU (the launch owns a CU's LDS)
+static constexpr int kFollowPerSeq = 2;
+
 static int device_cus() {
   static int cus[64] = {0};
   int dev = 0;
@@ -95,14 +97,23 @@ HMM355_API int hmm355_viterbi_plan_ex_f32(const float* obs, int obs_mode, const 
   // banded (the caller read it once per plan, hmm355_plan_banded); its tail keeps at most
   // 4096 chunk end states in LDS (T <= 262144)
   const bool tail = (flags & HMM355_VIT_PLAN_BANDED) && plan && band && NP >= 128 && nc <= 4096;
-  // (HMM355_VIT_TAIL_DIAG: diagnostic bits of RecArgs::vtail, timing only -- results are wrong)
+#ifdef HMM355_DIAG
+  // (HMM355_VIT_TAIL_DIAG: diagnostic bits of RecArgs::vtail, timing only -- results are wrong;
+  // read only in diagnostic builds, build_native.build(defines=["HMM355_DIAG"]))
   const char* diag = getenv("HMM355_VIT_TAIL_DIAG");
   va.vdiag = diag ? (atoi(diag) & ~1) : 0;
-  // psi followers: the caller's word that the plan is dense, N <= 128, and CUs beside the chain
+#endif
+  // psi followers: the caller's word that the plan is dense, N <= 128, and CUs beside the chain.
+  // A chain publishes a 64-step chunk every ~17 us (dense step ~270 ns) and a follower takes
+  // ~25-30 us per chunk, so two followers per sequence keep up; more would only hold CUs (each
+  // owns one: the launch asks for the CU's whole LDS) that a concurrent op on another stream
+  // could use.  With nfollow = 2B follower f serves sequence f mod B, every other chunk.
   if ((flags & HMM355_VIT_PLAN_DENSE) && plan && NP <= 128 && !tail) {
     const long room = (long)device_cus() - B;
     const long tasks = (long)B * nc;
-    va.nfollow = (int)(room < tasks ? (room > 0 ? room : 0) : tasks);
+    long nf = room < tasks ? room : tasks;
+    if (nf > (long)kFollowPerSeq * B) nf = (long)kFollowPerSeq * B;
+    va.nfollow = (int)(nf > 0 ? nf : 0);
     va.prog = prog;
     va.done = done;
   }

@@ -62,9 +62,13 @@ class HMMPyTorch(HMM):
                 or lp.requires_grad or l0.requires_grad):
             lpd = lp if lp.device == dev else lp.to(dev)
             l0d = l0 if l0.device == dev else l0.to(dev)
-            plan = ops.make_plan(lpd.detach()) if dev.type == "cuda" else None
+            # A plan re-formed every call (log_P requires grad: a training step changes it)
+            # skips the host read of its structure, so a training forward never waits on the
+            # device (ops.make_plan read_banded=False).
+            grad = lp.requires_grad or l0.requires_grad
+            plan = ops.make_plan(lpd.detach(), read_banded=not grad) if dev.type == "cuda" else None
             hit = (lp, l0, (lp._version, l0._version), lpd, l0d, plan)
-            if not (lp.requires_grad or l0.requires_grad):
+            if not grad:
                 cache[str(dev)] = hit
         return hit[3], hit[4], hit[5]
 

@@ -160,7 +160,10 @@ class MixtureGaussianHMMLayer(nn.Module):
         if (c is not None and c[0] is src and c[1] == src._version and c[2] == log_transitions.device
                 and c[3] == tuple(log_transitions.shape)):
             return c[4]
-        plan = ops.make_plan(log_transitions.detach())
+        # (a trainable matrix under autograd changes every step: skip the plan's host read, so
+        # a training forward makes no synchronous device -> host copy; ops.make_plan)
+        plan = ops.make_plan(log_transitions.detach(),
+                             read_banded=not (torch.is_grad_enabled() and src.requires_grad))
         self.__dict__["_plan_cache"] = (src, src._version, log_transitions.device, tuple(log_transitions.shape), plan)
         return plan
 

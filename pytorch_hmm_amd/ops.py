@@ -45,9 +45,17 @@ def _workspace(nbytes, device):
 
 
 # ------------------------------------------------------------------ forward-backward
-def make_plan(log_P: Tensor) -> Tensor:
+def make_plan(log_P: Tensor, read_banded: bool = True) -> Tensor:
     """Measure log_P's banded structure once (hmm355_plan_f32) into a device byte tensor that
-    forward_backward / viterbi accept as `plan` (valid while log_P is unchanged)."""
+    forward_backward / viterbi accept as `plan` (valid while log_P is unchanged).
+
+    The kernels read the structure from the plan on the device; the host only needs it to
+    choose between launch shapes (the pair kernel, the psi followers), and reading it back is
+    one synchronous device -> host copy.  With read_banded=False (a plan re-formed on every
+    training step, where log_P changes each call) that read is skipped and the plan's host
+    word stays unknown (None): forward_backward takes the two-kernel path, whose chains branch
+    on the device-side structure, and viterbi asks for psi followers, which return at once on
+    a banded plan (vit_kern.h vit_psi_follow) -- so the call stays asynchronous."""
     nat.require_gpu(log_P)
     log_P = _f32c(log_P)
     N = log_P.shape[0]
@@ -55,6 +63,9 @@ def make_plan(log_P: Tensor) -> Tensor:
     plan = torch.empty(L.hmm355_plan_bytes(N), dtype=torch.uint8, device=log_P.device)
     with torch.cuda.device(log_P.device):
         nat.check(L.hmm355_plan_f32(nat.ptr(log_P), N, nat.ptr(plan), nat.stream_of(log_P.device)))
+        if not read_banded:
+            plan._hmm355_banded = None
+            return plan
         # banded in both directions: forward_backward then runs both chains of a sequence in
         # one workgroup (HMM355_FB_PAIR, csrc/fbpair.h).  One synchronous read per plan.
         banded = L.hmm355_plan_banded(nat.ptr(plan), nat.stream_of(log_P.device))
@@ -118,7 +129,7 @@ def forward_backward(obs: Tensor, log_P: Tensor, log_p0: Tensor, obs_mode: int,
         return post, fwd, bwd, loglik, lik_ref
     nbytes = L.hmm355_fb_workspace_bytes(B, T, N)
     ws = _workspace(nbytes, dev)
-    if plan is not None and getattr(plan, "_hmm355_banded", False) and _use_pair(B, dev):
+    if plan is not None and getattr(plan, "_hmm355_banded", False) is True and _use_pair(B, dev):
         out_mask |= FB_PAIR
     with torch.cuda.device(dev):
         nat.check(L.hmm355_forward_backward_plan_f32(
@@ -156,11 +167,13 @@ def viterbi(obs: Tensor, log_P: Tensor, init: Tensor, obs_mode: int,
     # launch instead of three).  Off by default: measured 10 us slower per op at the north-star
     # shape (profiles/r4b_*), its composer and in-kernel backtrace cost more
     # than the two launches they replace.
-    flags = VIT_PLAN_BANDED if (plan is not None and getattr(plan, "_hmm355_banded", False)
+    flags = VIT_PLAN_BANDED if (plan is not None and getattr(plan, "_hmm355_banded", False) is True
                                 and os.environ.get("HMM355_VIT_TAIL", "0") == "1") else 0
     # a dense plan: the argmax pointers computed beside the chain, on the CUs it leaves
     # (HMM355_VIT_FOLLOW; _VIT_FOLLOW_DEFAULT: DESIGN.md round 4 item 15)
-    if (plan is not None and not getattr(plan, "_hmm355_banded", True)
+    # (a plan whose structure the host never read, make_plan(read_banded=False), asks for them
+    # too: on a banded matrix they return at once)
+    if (plan is not None and getattr(plan, "_hmm355_banded", True) is not True
             and os.environ.get("HMM355_VIT_FOLLOW", _VIT_FOLLOW_DEFAULT) != "0"):
         flags |= VIT_PLAN_DENSE
     with torch.cuda.device(dev):

@@ -7,7 +7,9 @@ per-frame Python loops run as gfx950 kernels (csrc/stream.hip): ``_greedy_decode
 (streaming.py:322-377) as K rounds of wave argmax per frame over the hypotheses'
 expansions, with the reference's stable tie order.  The emission network stays a torch
 module (two GEMMs on hipBLASLt); the chunk buffering and bookkeeping are host logic, as in
-the reference.  ``AdaptiveLatencyController`` (streaming.py:506-593) is mirrored as is.
+the reference.  The reference's latency-control helpers (``optimize_for_latency``,
+``get_latency_breakdown``, ``AdaptiveLatencyController``, streaming.py:444-592) are out of
+scope and not provided.
 """
 import queue
 import threading
@@ -289,82 +291,3 @@ class StreamingHMMProcessor(nn.Module):
             "beam_width": self.beam_width if self.use_beam_search else 1,
             "processing_mode": "beam_search" if self.use_beam_search else "greedy",
         }
-
-    def optimize_for_latency(self, target_latency_ms: float = 50.0):
-        stats = self.get_performance_stats()
-        if "avg_processing_time_ms" not in stats:
-            warnings.warn("No performance data available for optimization")
-            return
-        cur = stats["avg_processing_time_ms"]
-        if cur > target_latency_ms:
-            if self.use_beam_search and self.beam_width > 2:
-                self.beam_width = max(2, self.beam_width - 1)
-                print(f"Reduced beam width to {self.beam_width}")
-            elif self.use_beam_search:
-                self.use_beam_search = False
-                print("Switched to greedy decoding for lower latency")
-            elif self.chunk_size > 80:
-                self.chunk_size = max(80, int(self.chunk_size * 0.8))
-                print(f"Reduced chunk size to {self.chunk_size}")
-        elif cur < target_latency_ms * 0.5:
-            if not self.use_beam_search:
-                self.use_beam_search = True
-                self.beam_width = 4
-                print("Enabled beam search for better accuracy")
-            elif self.beam_width < 8:
-                self.beam_width += 1
-                print(f"Increased beam width to {self.beam_width}")
-
-    def get_latency_breakdown(self) -> Dict[str, float]:
-        stats = self.get_performance_stats()
-        if "avg_processing_time_ms" not in stats:
-            return {}
-        tot = stats["avg_processing_time_ms"]
-        shares = {"feature_extraction": 0.1, "emission_computation": 0.3, "transition_computation": 0.1,
-                  "viterbi_decoding": 0.4, "bookkeeping": 0.1}
-        out = {k: tot * v for k, v in shares.items()}
-        out["total"] = tot
-        return out
-
-
-class AdaptiveLatencyController:
-    """Chunk-size / beam recommendations from recent latencies (streaming.py:506-593)."""
-
-    def __init__(self, initial_chunk_size: int = 160, min_chunk_size: int = 80, max_chunk_size: int = 320,
-                 target_latency_ms: float = 50.0, adaptation_rate: float = 0.1):
-        self.chunk_size = initial_chunk_size
-        self.min_chunk_size = min_chunk_size
-        self.max_chunk_size = max_chunk_size
-        self.target_latency_ms = target_latency_ms
-        self.adaptation_rate = adaptation_rate
-        self.latency_history = deque(maxlen=100)
-        self.adjustment_cooldown = 0
-        self.last_adjustment_time = 0
-
-    def update(self, processing_time_ms: float, buffer_size: int) -> Dict[str, Any]:
-        self.latency_history.append(processing_time_ms)
-        now = time.time()
-        if now - self.last_adjustment_time < 1.0 or len(self.latency_history) < 10:
-            return {}
-        recent = list(self.latency_history)[-20:]
-        avg = sum(recent) / len(recent)
-        var = torch.tensor(recent).var().item()
-        rec = {}
-        if avg > self.target_latency_ms * 1.2:
-            if self.chunk_size > self.min_chunk_size:
-                self.chunk_size = max(self.min_chunk_size, int(self.chunk_size * (1 - self.adaptation_rate)))
-                rec["chunk_size"] = self.chunk_size
-            rec["beam_width"] = max(1, int(4 * 0.8))
-            rec["use_beam_search"] = not avg > self.target_latency_ms * 2
-        elif avg < self.target_latency_ms * 0.6 and var < 10.0:
-            if self.chunk_size < self.max_chunk_size and buffer_size > 100:
-                self.chunk_size = min(self.max_chunk_size, int(self.chunk_size * (1 + self.adaptation_rate)))
-                rec["chunk_size"] = self.chunk_size
-            rec["beam_width"] = min(8, 6)
-            rec["use_beam_search"] = True
-        elif var > 25.0:
-            rec["use_beam_search"] = False
-            rec["chunk_size"] = max(self.min_chunk_size, int(self.chunk_size * 0.9))
-        if rec:
-            self.last_adjustment_time = now
-        return rec

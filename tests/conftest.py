@@ -36,7 +36,8 @@ HOST_BITEXACT_TESTS = {
     "test_hsmm_layer_tables_match_reference", "test_hmmpytorch_oracle_bitexact",
     "test_ties_and_wiki", "test_hmmlayer_first_call_renormalises", "test_mixture_oracle",
     "test_mixture_chunked_emission_identical", "test_hsmm_oracle",
-    "test_neural_oracle_bitexact", "test_duration_tables_bitexact",
+    "test_neural_oracle_bitexact", "test_duration_tables_bitexact", "test_mixture_cov_oracle",
+    "test_gaussian_cov_log_probs",
 }
 FINGERPRINT_FILE = os.path.join(GOLDEN, "host_numerics.txt")
 

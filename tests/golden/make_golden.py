@@ -219,6 +219,51 @@ def fx_mixture_full(name, S, D, C, B, T, seed):
          states=npf(states), scores=npf(scores), input_sha256=sha(npf(x)))
 
 
+def fx_mixture_cov(name, S, D, C, B, T, seed, cov):
+    """MixtureGaussianHMMLayer(covariance_type='tied' | 'spherical') (mixture_gaussian.py:242-269,
+    LSE :141-155, Viterbi :290-338).  The log-variances are drawn off their zero init so the
+    variance terms of each branch's expression (sum diff^2/var + sum log_var for 'tied';
+    sum diff^2 / var + D*log_var for 'spherical') take part."""
+    torch.manual_seed(seed)
+    m = MixtureGaussianHMMLayer(S, D, num_components=C, covariance_type=cov)
+    with torch.no_grad():
+        m.log_vars.copy_(0.4 * torch.randn_like(m.log_vars))
+    x = torch.randn(B, T, D)
+    with torch.no_grad():
+        lp = m.get_observation_log_probs(x)
+        log_T = m._safe_log(m.get_transition_matrix())
+        states, scores = m(x, return_log_probs=True)
+    save(name, x=npf(x), transition_logits=npf(m.transition_logits),
+         mixture_weights_logits=npf(m.mixture_weights_logits), means=npf(m.means),
+         log_vars=npf(m.log_vars), log_probs=npf(lp), log_T=npf(log_T), states=npf(states),
+         scores=npf(scores), covariance_type=np.array(cov), input_sha256=sha(npf(x)))
+
+
+def fx_gaussian_cov(name, K, D, B, T, seed, cov):
+    """GaussianHMMLayer(covariance_type='spherical' | 'full') (hmm_layer.py:289-298 and :311-319,
+    the 'full' branch using the diagonal of log_scales), then exp -> HMMLayer as fx_gaussian.
+    Small D so exp(log_probs) does not underflow and the HMM sees real emissions; log_scales
+    drawn off their zero init (for 'full' the whole (K,D,D) tensor, of which the reference
+    reads only the diagonal)."""
+    torch.manual_seed(seed)
+    layer = GaussianHMMLayer(K, D, covariance_type=cov)
+    with torch.no_grad():
+        layer.log_scales.copy_(0.3 * torch.randn_like(layer.log_scales))
+    x = torch.randn(B, T, D)
+    lp = layer._compute_gaussian_log_probs(x)
+    probs = torch.exp(lp)
+    layer.train()
+    post = layer(x)                                              # call 1 (FB)
+    layer.eval()
+    onehot, states = layer.hmm_layer(probs, return_alignment=True)   # call 2 (Viterbi)
+    loss = layer.compute_loss(x)                                 # call 3
+    save(name, x=npf(x), means=npf(layer.means), log_scales=npf(layer.log_scales),
+         logits=npf(layer.hmm_layer.log_transition_logits),
+         init_logits=npf(layer.hmm_layer.log_initial_logits), log_probs=npf(lp), probs=npf(probs),
+         posterior=npf(post), onehot=npf(onehot), states=npf(states), loss=npf(loss),
+         covariance_type=np.array(cov), input_sha256=sha(npf(x)))
+
+
 def fx_hsmm(name, S, D, Dmax, B, T, seed, dur_params=None):
     """HSMMLayer segment Viterbi (hsmm.py:181-354); the literal 5-deep loop, small sizes only.
     dur_params = (shape, rate) raw parameter values (before softplus) to favour long segments."""
@@ -470,6 +515,10 @@ def main():
         ("mixture_s128", lambda: fx_mixture("mixture_s128", 128, 80, 4, 1, 64, 0)),
         ("mixture_single", lambda: fx_mixture("mixture_single", 1, 10, 1, 1, 20, 3)),
         ("mixture_full", lambda: fx_mixture_full("mixture_full", 6, 7, 3, 2, 40, 11)),
+        ("mixture_tied", lambda: fx_mixture_cov("mixture_tied", 16, 20, 4, 2, 128, 21, "tied")),
+        ("mixture_spherical", lambda: fx_mixture_cov("mixture_spherical", 16, 20, 4, 2, 128, 22, "spherical")),
+        ("gaussian_spherical", lambda: fx_gaussian_cov("gaussian_spherical", 8, 6, 2, 64, 23, "spherical")),
+        ("gaussian_full", lambda: fx_gaussian_cov("gaussian_full", 8, 6, 2, 64, 24, "full")),
         ("hsmm_s5", lambda: fx_hsmm("hsmm_s5", 5, 30, 20, 2, 30, 0)),
         ("hsmm_s2", lambda: fx_hsmm("hsmm_s2", 2, 3, 2, 1, 4, 1)),
         ("hsmm_s8", lambda: fx_hsmm("hsmm_s8", 8, 20, 10, 1, 40, 2)),

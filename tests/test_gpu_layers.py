@@ -104,6 +104,65 @@ def test_mixture_full_covariance():
     assert m.cholesky_params.grad is not None and torch.isfinite(m.cholesky_params.grad).all()
 
 
+@pytest.mark.parametrize("name", ["mixture_tied", "mixture_spherical"])
+def test_mixture_layer_covariance(name):
+    """covariance_type='tied' / 'spherical' (mixture_gaussian.py:242-269) against the reference's
+    fixtures (tests/golden/make_golden.py fx_mixture_cov): the scorer takes per-dimension
+    log-variances (the tied vector or the spherical scalar repeated over D) in fp64, so the
+    emissions are within the diag scorer's rtol 2e-6 of the reference's fp32 expression, and the
+    decoded states are bit-exact end to end."""
+    g = golden(name)
+    cov = str(g["covariance_type"])
+    S, C, D = g["means"].shape
+    m = ph.MixtureGaussianHMMLayer(S, D, num_components=C, covariance_type=cov).to(DEV)
+    with torch.no_grad():
+        for k in ("transition_logits", "mixture_weights_logits", "means", "log_vars"):
+            getattr(m, k).copy_(t(g[k]))
+    x = t(g["x"])
+    with torch.no_grad():
+        lp = m.get_observation_log_probs(x)
+    np.testing.assert_allclose(lp.cpu().numpy(), g["log_probs"], rtol=2e-6, atol=2e-5)
+    with torch.no_grad():
+        states, scores = m(x, return_log_probs=True)
+    assert np.array_equal(states.cpu().numpy(), g["states"])
+    np.testing.assert_allclose(scores.cpu().numpy(), g["scores"], rtol=2e-6)
+    # given the reference's own log-probs the decode is bit-exact, score included
+    with torch.no_grad():
+        s2, sc2 = m._viterbi_decode(t(g["log_probs"]), t(g["log_T"]))
+    assert np.array_equal(s2.cpu().numpy(), g["states"]) and np.array_equal(sc2.cpu().numpy(), g["scores"])
+    # trainable through the emission's analytic backward
+    s3, sc3 = m(x, return_log_probs=True)
+    sc3.sum().backward()
+    assert m.log_vars.grad is not None and torch.isfinite(m.log_vars.grad).all()
+
+
+@pytest.mark.parametrize("name", ["gaussian_spherical", "gaussian_full"])
+def test_gaussian_layer_covariance(name):
+    """GaussianHMMLayer 'spherical' (hmm_layer.py:289-298) and 'full' (its diagonal, :311-319)
+    with D = 6 (real, non-underflowing emissions) against the reference's call sequence."""
+    g = golden(name)
+    cov = str(g["covariance_type"])
+    K, D = g["means"].shape
+    layer = ph.GaussianHMMLayer(K, D, covariance_type=cov).to(DEV)
+    with torch.no_grad():
+        layer.means.copy_(t(g["means"]))
+        layer.log_scales.copy_(t(g["log_scales"]))
+        layer.hmm_layer.log_transition_logits.copy_(t(g["logits"]))
+        layer.hmm_layer.log_initial_logits.copy_(t(g["init_logits"]))
+    x = t(g["x"])
+    with torch.no_grad():
+        lp = layer._compute_gaussian_log_probs(x).cpu().numpy()
+        np.testing.assert_allclose(lp, g["log_probs"], rtol=2e-6, atol=2e-5)
+        layer.train()
+        post = layer(x)
+        np.testing.assert_allclose(post.cpu().numpy(), g["posterior"], atol=2e-4)
+        layer.eval()
+        onehot, states = layer.hmm_layer(torch.exp(layer._compute_gaussian_log_probs(x)), return_alignment=True)
+        assert np.array_equal(states.cpu().numpy(), g["states"])
+        assert np.array_equal(onehot.cpu().numpy(), g["onehot"])
+        np.testing.assert_allclose(layer.compute_loss(x).cpu().numpy(), g["loss"], rtol=1e-5)
+
+
 @pytest.mark.parametrize("name,S,D,Dm,seed", [("hsmm_s5", 5, 30, 20, 0), ("hsmm_s2", 2, 3, 2, 1),
                                               ("hsmm_s8", 8, 20, 10, 2)])
 def test_hsmm_layer(name, S, D, Dm, seed):

@@ -81,3 +81,50 @@ def test_trained_hmmlayer_posteriors_dense_vs_fp64():
     lo = np.log((torch.sigmoid(x).cpu().numpy() + np.float32(1e-8)).astype(np.float64)).astype(np.float32)
     ref = O.c_fb64(lo, lP.numpy(), lp0.numpy())[2]
     assert np.allclose(post.cpu().numpy(), ref, atol=2e-5, rtol=0)
+
+
+def test_training_step_makes_no_plan_sync():
+    """A training step re-forms the transition plan (log_P changes every step) without the
+    plan's synchronous device -> host read (ops.make_plan read_banded=False): over 20 Adam steps
+    of HMMLayer (train-mode posteriors with a supervised loss, and compute_loss) the read is
+    never called, and torch's sync debug mode sees no synchronising torch op in the forward or
+    backward.  (hmm_layer.py:73-89,144-173)"""
+    import warnings
+    import pytorch_hmm_amd._native as nat
+    L = nat.lib()
+    calls = []
+    real = L.hmm355_plan_banded
+
+    def counted(*a):
+        calls.append(1)
+        return real(*a)
+    N, B, T = 32, 4, 50
+    torch.manual_seed(0)
+    layer = ph.HMMLayer(N).to(DEV)
+    opt = torch.optim.Adam(layer.parameters(), lr=1e-3)
+    g = torch.Generator(device=DEV).manual_seed(1)
+    xs = [torch.randn(B, T, N, device=DEV, generator=g) for _ in range(20)]
+    tgt = torch.randint(0, N, (B, T), device=DEV, generator=g)
+    layer.train()
+    layer(xs[0])  # first call (HMMPyTorch construction, the reference's renormalisation)
+    torch.cuda.synchronize()
+    L.hmm355_plan_banded = counted
+    try:
+        with warnings.catch_warnings(record=True) as rec:
+            warnings.simplefilter("always")
+            torch.cuda.set_sync_debug_mode("warn")
+            try:
+                for i, x in enumerate(xs):
+                    loss = layer.compute_loss(x, tgt) if i % 2 else layer.compute_loss(x)
+                    opt.zero_grad()
+                    loss.backward()
+                    opt.step()
+            finally:
+                torch.cuda.set_sync_debug_mode("default")
+    finally:
+        L.hmm355_plan_banded = real
+    torch.cuda.synchronize()
+    assert not calls, f"{len(calls)} synchronous plan reads in 20 training steps"
+    syncs = [str(w.message) for w in rec if "called a synchronizing" in str(w.message)]
+    assert not syncs, syncs[:3]
+    assert torch.isfinite(loss.detach())

@@ -102,3 +102,86 @@ def test_followers_obs_prob(monkeypatch):
     b = _run(x, lP, lp0, plan, False, monkeypatch, ops.OBS_PROB)
     for u, v in zip(a, b):
         assert np.array_equal(u, v)
+
+
+def _abi_viterbi(lo_dev, lPd, lp0d, plan, flags, stream=None):
+    """hmm355_viterbi_plan_ex_f32 through ctypes; returns (states, delta, workspace)."""
+    import pytorch_hmm_amd._native as nat
+    from pytorch_hmm_amd import ops
+    B, T, N = lo_dev.shape
+    L = nat.lib()
+    states = torch.zeros(B, T, dtype=torch.int64, device=DEV)
+    delta = torch.empty(B, T, N, device=DEV)
+    final = torch.zeros(B, device=DEV)
+    ws = torch.empty(L.hmm355_viterbi_workspace_bytes(B, T, N), dtype=torch.uint8, device=DEV)
+    p = lambda t: ctypes.c_void_p(t.data_ptr())
+    st = nat.stream_of(torch.device(DEV, 0)) if stream is None else ctypes.c_void_p(stream.cuda_stream)
+    rc = L.hmm355_viterbi_plan_ex_f32(p(lo_dev), ops.OBS_LOG, p(lPd), p(lp0d), p(plan), flags, B, T, N,
+                                      p(states), p(delta), p(final), p(ws), ws.numel(), st)
+    assert rc == 0
+    return states, delta, ws
+
+
+def test_followers_complete_chunks():
+    """The followers really do the work: after a dense decode the workspace's done words
+    (viterbi.hip layout: the last B*nchunks bytes, 256-aligned) mark the chunks they finished.
+    With two followers per sequence keeping pace with the chain nearly every chunk is theirs."""
+    import pytorch_hmm_amd._native as nat
+    from pytorch_hmm_amd import ops
+    N, B, T = 128, 8, 2000
+    lP, lp0 = O.hmm_params(_dense(N, 5))
+    lPd = lP.to(DEV)
+    plan = ops.make_plan(lPd)
+    rng = np.random.default_rng(4)
+    lo = np.log(rng.random((B, T, N), dtype=np.float32) + np.float32(1e-3)).astype(np.float32)
+    s, d, ws = _abi_viterbi(torch.from_numpy(lo).to(DEV), lPd, lp0.to(DEV), plan, nat.VIT_PLAN_DENSE)
+    torch.cuda.synchronize()
+    nc = (T + 63) // 64
+    span = (B * nc + 255) // 256 * 256
+    done = ws[ws.numel() - span: ws.numel() - span + B * nc].cpu().numpy()
+    frac = float((done == 1).mean())
+    print(f"followers finished {int((done == 1).sum())} of {B * nc} chunks")
+    assert frac > 0.5, frac
+    cs, cd, _ = O.c_viterbi(lo, lP.numpy(), lp0.numpy())
+    assert np.array_equal(d.cpu().numpy(), cd) and np.array_equal(s.cpu().numpy(), cs)
+
+
+def test_followers_no_cliff_beside_busy_stream(monkeypatch):
+    """A second stream keeps the chip busy (a queue of GEMMs) while a dense decode runs: the
+    decode with followers stays within 2x of the same decode without them under the same load,
+    and far from the old per-task 200 ms wait bound (one 2 ms stall budget per launch now)."""
+    from pytorch_hmm_amd import ops
+    N, B, T = 128, 32, 2000
+    lP, lp0 = O.hmm_params(_dense(N, 9))
+    lPd, lp0d = lP.to(DEV), lp0.to(DEV)
+    plan = ops.make_plan(lPd)
+    g = torch.Generator().manual_seed(3)
+    lo = torch.log(torch.rand(B, T, N, generator=g) + 1e-3).to(DEV)
+    a = torch.randn(4096, 4096, device=DEV)
+    busy = torch.cuda.Stream()
+    vs = torch.cuda.Stream()
+
+    def run(follow):
+        monkeypatch.setenv("HMM355_VIT_FOLLOW", "1" if follow else "0")
+        with torch.cuda.stream(vs):
+            ops.viterbi(lo, lPd, lp0d, ops.OBS_LOG, plan)   # warm
+        torch.cuda.synchronize()
+        times = []
+        for _ in range(3):
+            with torch.cuda.stream(busy):
+                for _ in range(40):
+                    a2 = a @ a
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            with torch.cuda.stream(vs):
+                e0.record()
+                out = ops.viterbi(lo, lPd, lp0d, ops.OBS_LOG, plan)
+                e1.record()
+            torch.cuda.synchronize()
+            times.append(e0.elapsed_time(e1))
+        return min(times), out
+    t_on, out_on = run(True)
+    t_off, out_off = run(False)
+    print(f"busy-stream Viterbi op: followers on {t_on:.3f} ms, off {t_off:.3f} ms")
+    assert torch.equal(out_on[0], out_off[0]) and torch.equal(out_on[1], out_off[1])
+    assert t_on < 2 * t_off + 1.0, (t_on, t_off)
+    assert t_on < 50.0

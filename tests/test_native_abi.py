@@ -72,6 +72,19 @@ def test_workspace_sizes(L):
     assert L.hmm355_hsmm_workspace_bytes(16, 2000, 64, 40) > 0
 
 
+def test_fb_workspace_layout_matches_header(L):
+    """include/hmm355.h's forward-backward workspace layout (U | V | LA | LB | BandDesc | (B,NP) |
+    (B) | (B,T) | CA | CB, 256-B aligned) is what hmm355_fb_workspace_bytes sizes, so the adjoint's
+    views of CA / CB (autograd._run_fb) end exactly at the workspace's end."""
+    al = lambda n: ((n + 255) // 256) * 256
+    for B, T, N in ((32, 2000, 128), (3, 17, 5), (2, 1, 200), (7, 129, 64)):
+        NP = 64 if N <= 64 else (128 if N <= 128 else 256)
+        rows = B * T
+        want = (al(2 * rows * NP * 4) + al(2 * rows * 4) + al(L.hmm355_plan_bytes(N)) + al(B * NP * 4) + al(B * 4)
+                + al(rows * 4) + al(2 * rows * 4))
+        assert L.hmm355_fb_workspace_bytes(B, T, N) == want, (B, T, N)
+
+
 def test_argument_rejection_before_launch(L):
     """Invalid arguments return the documented code; nothing touches the (absent) GPU."""
     d = header_defines()

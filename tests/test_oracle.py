@@ -96,6 +96,36 @@ def test_mixture_oracle(name):
     assert eq(cs, g["states"]) and eq(cd[:, -1].max(-1), g["scores"])
 
 
+@pytest.mark.parametrize("name", ["mixture_tied", "mixture_spherical"])
+def test_mixture_cov_oracle(name):
+    """'tied' / 'spherical' (mixture_gaussian.py:242-269) in the reference's own expression order."""
+    g = golden(name)
+    cov = str(g["covariance_type"])
+    lp = O.mixture_log_probs(torch.from_numpy(g["x"]), torch.from_numpy(g["mixture_weights_logits"]),
+                             torch.from_numpy(g["means"]), torch.from_numpy(g["log_vars"]), covariance_type=cov)
+    assert eq(lp, g["log_probs"])
+    s, sc = O.mixture_viterbi(lp, torch.from_numpy(g["log_T"]))
+    assert eq(s, g["states"]) and eq(sc, g["scores"])
+    # the fp64 C scorer on the per-dimension form the kernels take is within 2e-6
+    S, C, D = g["means"].shape
+    lv = g["log_vars"]
+    lv3 = (np.broadcast_to(lv.reshape(1, 1, D), (S, C, D)) if cov == "tied"
+           else np.broadcast_to(lv.reshape(S, C, 1), (S, C, D)))
+    lw = O._safe_log(torch.softmax(torch.from_numpy(g["mixture_weights_logits"]), -1)).numpy()
+    np.testing.assert_allclose(O.c_gmm64(g["x"], g["means"], np.ascontiguousarray(lv3, np.float32), lw),
+                               g["log_probs"], rtol=2e-6, atol=2e-5)
+
+
+@pytest.mark.parametrize("name", ["gaussian_spherical", "gaussian_full"])
+def test_gaussian_cov_log_probs(name):
+    """GaussianHMMLayer 'spherical' (hmm_layer.py:289-298) and 'full' (diagonal, :311-319)."""
+    g = golden(name)
+    lp = O.gaussian_log_probs(torch.from_numpy(g["x"]), torch.from_numpy(g["means"]),
+                              torch.from_numpy(g["log_scales"]), str(g["covariance_type"]))
+    assert eq(lp, g["log_probs"])
+    assert (g["probs"] > 0).mean() > 0.5  # small D: the HMM sees real emissions
+
+
 def test_mixture_chunked_emission_identical():
     g = golden("mixture_s16")
     args = [torch.from_numpy(g[k]) for k in ("x", "mixture_weights_logits", "means", "log_vars")]

@@ -9,7 +9,6 @@ import torch
 
 from conftest import golden
 from oracle import hmm_oracle as O
-from pytorch_hmm_amd.streaming import AdaptiveLatencyController
 
 NAMES = ["stream_n5", "stream_n12", "stream_n3k16"]
 
@@ -65,16 +64,6 @@ def test_beam_oracle_matches_reference(name):
         assert np.array_equal(states, g[f"beam_states{i}"])
         conf = torch.exp(torch.tensor(hs[0]) / int(plen[0]))
         assert float(conf) == float(g[f"beam_conf{i}"][0])
-
-
-def test_adaptive_latency_controller():
-    """streaming.py:506-593: no advice before 10 samples or within the 1 s cooldown."""
-    c = AdaptiveLatencyController(target_latency_ms=50.0)
-    for _ in range(9):
-        assert c.update(200.0, 0) == {}
-    rec = c.update(200.0, 0)
-    assert rec["chunk_size"] == 144 and rec["use_beam_search"] is False and rec["beam_width"] == 3
-    assert c.update(200.0, 0) == {}   # cooldown
 
 
 def test_async_worker_queue_semantics():
