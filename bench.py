@@ -93,10 +93,38 @@ def setup_dist(args):
     return rank, world, local
 
 
+def csrc_sha16():
+    """sha256 (16 hex digits) of the kernel sources (pytorch_hmm_amd/csrc): a committed PMC
+    summary records it (tools/prof_summary.py), so a bench line reports those bytes as the
+    kernel's current traffic only when they were counted on these sources."""
+    import glob
+    import hashlib
+    h = hashlib.sha256()
+    for f in sorted(glob.glob(os.path.join(HERE, "pytorch_hmm_amd", "csrc", "*.h")) +
+                    glob.glob(os.path.join(HERE, "pytorch_hmm_amd", "csrc", "*.hip"))):
+        h.update(os.path.basename(f).encode())
+        with open(f, "rb") as fh:
+            h.update(fh.read())
+    return h.hexdigest()[:16]
+
+
+def traffic_fields(v, src, fresh):
+    """roofline fields for PMC bytes from a committed summary: `traffic` when they were counted
+    on the current kernel sources; else `traffic` null and the stale bytes as
+    `traffic_committed` (no stale counts beside live timings)."""
+    if v is None:
+        return {"traffic": None, "traffic_source": None}
+    if fresh:
+        return {"traffic": v, "traffic_source": src}
+    return {"traffic": None, "traffic_committed": v,
+            "traffic_source": f"{src} (counted on earlier kernel sources)"}
+
+
 def profiled_traffic(op, B, T, N, transition):
     """HBM bytes per launch of `op` from the committed rocprofv3 PMC summary (FETCH_SIZE x 2 +
     WRITE_SIZE, MI355X_MICROARCH.md's gfx950 correction; tools/gpu_prof.sh -> profiles/),
-    when it was taken on this exact configuration; else None."""
+    when it was taken on this exact configuration: (bytes, file, counted on these sources);
+    else (None, None, False)."""
     import glob
     for f in sorted(glob.glob(os.path.join(HERE, "profiles", "*_summary.json")), reverse=True):
         try:
@@ -110,19 +138,19 @@ def profiled_traffic(op, B, T, N, transition):
             continue
         v = d.get("ops", {}).get(op, {}).get("hbm_bytes_per_launch")
         if v:
-            return float(v), os.path.relpath(f, HERE)
-    return None, None
+            return float(v), os.path.relpath(f, HERE), d.get("csrc_sha16") == csrc_sha16()
+    return None, None, False
 
 
 def profiled_kernel_traffic(kernel, desc):
     """HBM bytes per launch of `kernel` (a torch.profiler kernel name) from the committed
     rocprofv3 PMC summary of the same layer workload (tools/gpu_prof.sh --workload ...;
-    FETCH_SIZE x 2 + WRITE_SIZE), or (None, None)."""
+    FETCH_SIZE x 2 + WRITE_SIZE): (bytes, file, counted on these sources) or (None, None, False)."""
     import glob
     import re
     m = re.search(r"hmm355::(\w+)(<[^>]*>)?", kernel or "")
     if not m:
-        return None, None
+        return None, None, False
     short = (m.group(1) + (m.group(2) or "")).replace(" ", "")
     for f in sorted(glob.glob(os.path.join(HERE, "profiles", "*_summary.json")), reverse=True):
         try:
@@ -134,8 +162,8 @@ def profiled_kernel_traffic(kernel, desc):
             continue
         v = (d.get("traffic") or {}).get(short, {}).get("hbm_bytes_per_launch")
         if v:
-            return float(v), os.path.relpath(f, HERE)
-    return None, None
+            return float(v), os.path.relpath(f, HERE), d.get("csrc_sha16") == csrc_sha16()
+    return None, None, False
 
 
 def cpu_baseline(B, T, N, budget, P):
@@ -431,7 +459,7 @@ def layer_workload(args, rank, world, dev):
         roof = kroof
         # the committed PMC bytes of the same kernel (for a VALU-bound kernel too: HBM bytes far
         # above its algorithmic bytes would still be the first thing to fix)
-        roof["traffic"], roof["traffic_source"] = profiled_kernel_traffic(roof.get("kernel"), desc)
+        roof.update(traffic_fields(*profiled_kernel_traffic(roof.get("kernel"), desc)))
     elif flops is not None:
         achieved = flops / (step_ms * 1e-3) / 1e12
         roof = {"bound": "valu", "kernel": dom, "achieved": achieved, "peak": VALU_PEAK_TFLOPS, "unit": "TFLOP/s",
@@ -769,14 +797,14 @@ def main():
         dom, dur_ms, bytes_per_launch = "viterbi", vit_ms, (8 * N + 8) * B * T
         kernels = "vit_fwd_kernel + vit_psi_kernel + vit_backtrace_kernel"
     achieved = bytes_per_launch / (dur_ms * 1e-3) / 1e9
-    traffic, traffic_src = profiled_traffic(dom, B, T, N, args.transition)
+    dom_traffic = traffic_fields(*profiled_traffic(dom, B, T, N, args.transition))
     # both ops' fractions (north_star's target names forward-backward's)
     op_roofline = {}
     for name, ms, bpl in (("forward_backward", fb_ms, 16 * N * B * T), ("viterbi", vit_ms, (8 * N + 8) * B * T)):
         a_ = bpl / (ms * 1e-3) / 1e9
-        tr, trs = profiled_traffic(name, B, T, N, args.transition)
-        op_roofline[name] = {"achieved": a_, "frac": a_ / HBM_PEAK_GBS, "bytes_per_launch": bpl,
-                             "avg_launch_ms": ms, "traffic": tr, "traffic_source": trs}
+        op_roofline[name] = dict({"achieved": a_, "frac": a_ / HBM_PEAK_GBS, "bytes_per_launch": bpl,
+                                  "avg_launch_ms": ms},
+                                 **traffic_fields(*profiled_traffic(name, B, T, N, args.transition)))
     out = {
         "metric": "frames/sec forward-backward+Viterbi, B=32 T=2000 N=128, 1/2/4/8 GPU",
         "value": value, "unit": "frames/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
@@ -796,7 +824,7 @@ def main():
         "op_ms": {"forward_backward": fb_ms, "viterbi": vit_ms},
         "roofline": {"bound": "hbm", "kernel": dom, "kernels": kernels, "achieved": achieved,
                      "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
-                     "traffic": traffic, "traffic_source": traffic_src,
+                     **dom_traffic,
                      "bytes_per_launch": bytes_per_launch, "avg_launch_ms": dur_ms},
         "roofline_ops": op_roofline,
     }

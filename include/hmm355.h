@@ -150,7 +150,10 @@ int hmm355_viterbi_plan_f32(const float* obs, int obs_mode, const float* log_P, 
  * of the chain's own launch on the CUs the chain leaves idle (they follow the rows the chain
  * has flushed; a chunk they did not finish is computed by the pass after the chain, so the
  * result never depends on their timing).  Without the flag the pointers are computed after the
- * chain.  The flag with a banded plan only costs the idle launch. */
+ * chain.  With HMM355_OBS_PROB the flag also forms log(x + 1e-8) in one full-tensor pass into
+ * the workspace first (the dense chain's staging waves share their SIMDs with the chain and
+ * would pay for the log on every step).  The flag with a banded plan only costs the idle launch
+ * and that pass. */
 #define HMM355_VIT_PLAN_DENSE 0x2u
 int hmm355_viterbi_plan_ex_f32(const float* obs, int obs_mode, const float* log_P, const float* init,
                                const void* plan, unsigned flags, int B, int T, int N, int64_t* states,
@@ -307,7 +310,9 @@ int hmm355_tv_fb_viterbi_f32(const float* log_obs, const float* log_A, long long
  *   identical fp32 quad/table inputs.
  * Forward outputs: log_prob (B) = LSE over (s,d) of log alpha[T-1]; log_alpha (B,T,S,Dmax)
  *   optional (NULL = not written), -inf where a segment is impossible.
- * 1 <= S <= 64, 1 <= Dmax <= 63.
+ * 1 <= S <= 1024, 1 <= Dmax <= 1024.  S <= 64 with Dmax <= 63 runs the register form; larger
+ * sizes the general form (its workspace holds a (B,T,S,Dmax) fp32 segment-score table:
+ * hmm355_semimarkov_workspace_bytes).
  * ------------------------------------------------------------------------------ */
 size_t hmm355_semimarkov_workspace_bytes(int B, int T, int S, int Dmax);
 int hmm355_semimarkov_quad_f32(const float* x, const float* means_t, const float* vars_t, int B,

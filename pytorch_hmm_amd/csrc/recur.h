@@ -165,21 +165,6 @@ __device__ __forceinline__ void red4_add_with_c(float& s0, float& s1, float s2, 
       : "+v"(s0), "+v"(s1), "+v"(c)
       : "v"(s3), "v"(s2));
 }
-// the same reduce-scatter without the scale's all-reduce (the lagged-scale dense FB chain: the
-// normaliser is formed by a helper wave, off the chain)
-__device__ __forceinline__ void red4_add(float& s0, float& s1, float s2, float s3) {
-  asm("s_nop 1\n\t"
-      "v_add_f32_dpp %0, %2, %0 row_mirror row_mask:0xf bank_mask:0xf\n\t"
-      "v_add_f32_dpp %1, %3, %1 row_mirror row_mask:0xf bank_mask:0xf\n\t"
-      "s_nop 1\n\t"
-      "v_add_f32_dpp %0, %1, %0 row_half_mirror row_mask:0xf bank_mask:0xf\n\t"
-      "s_nop 1\n\t"
-      "v_add_f32_dpp %0, %0, %0 quad_perm:[3,2,1,0] row_mask:0xf bank_mask:0xf\n\t"
-      "s_nop 1\n\t"
-      "v_add_f32_dpp %0, %0, %0 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf"
-      : "+v"(s0), "+v"(s1)
-      : "v"(s3), "v"(s2));
-}
 __device__ __forceinline__ void red4_max(float& s0, float& s1, float s2, float s3) {
   asm("s_nop 1\n\t"
       "v_max_f32_dpp %0, %2, %0 row_mirror row_mask:0xf bank_mask:0xf\n\t"
@@ -399,9 +384,7 @@ __device__ __forceinline__ void rec_stage(const RecArgs& a, float* lds, int blk,
 // double.  Every flushing wave computes it (so each knows its rows' log-scales for the exp
 // outputs and keeps its own `base`); the one with write_ls stores LA / LB.  Lane j < 16
 // returns LS of row 16*blk + j.
-// INV (the lagged-scale dense chain, rec_run_rb): the slot holds the multiplier k the step applied
-// (u_rho = z e k), so the log-scale grows by -log k.
-template <int NP, int KIND, bool INV = false>
+template <int NP, int KIND>
 __device__ __forceinline__ float rec_ls_scan(const RecArgs& a, const float* lds, int b, int blk, double& base,
                                              bool write_ls) {
   using C = RC<NP>;
@@ -410,10 +393,10 @@ __device__ __forceinline__ float rec_ls_scan(const RecArgs& a, const float* lds,
   const int rho = blk * 16 + j;
   const float c = lds[C::OFF_SC + 64 * ((rho - 1) & (C::RING - 1))];  // unconditional (see rec_flush)
   const bool live = lane < 16 && rho >= 1 && rho < a.T;
-  float x = live ? (INV ? -__logf(c) : __logf(c)) : 0.f;
+  float x = live ? __logf(c) : 0.f;
   // the step's normaliser by time for the adjoint (alpha: time rho - 1; beta: time T - rho)
   if (write_ls && a.cs && live)
-    a.cs[(size_t)b * a.T + (KIND == kFbBeta ? a.T - rho : rho - 1)] = INV ? 1.f / c : c;
+    a.cs[(size_t)b * a.T + (KIND == kFbBeta ? a.T - rho : rho - 1)] = c;
   if (a.obs_mode == HMM355_OBS_LOG) {
     // shifted emissions: alpha row rho used M_{tau(rho)}, beta row rho used M_{tau(rho)+1}
     // (the row staged as rho - 1); beta row 0 (the terminal vector) none
@@ -896,27 +879,6 @@ __device__ __forceinline__ void rec_run_bc(const RecArgs& a, float* lds, int b) 
 template <int KIND>
 constexpr int kRbItems = 7;
 
-// how the dense FB chain normalises (rec_run_rb; diagnostic builds: -DHMM355_FBSCALE=n)
-#ifndef HMM355_FBSCALE
-#define HMM355_FBSCALE 0
-#endif
-constexpr int kFbScale = HMM355_FBSCALE;
-template <bool V>
-struct BoolTag {
-  static constexpr bool value = V;
-};
-
-// the sum of step q + 1's input vector (alpha: the ring row q; beta: v_q * e_q in Pv), on every lane
-template <int NP, int KIND>
-__device__ __forceinline__ float rb_input_sum(const float* lds, int q) {
-  using C = RC<NP>;
-  const int l = threadIdx.x & 63;
-  const float* src = KIND == kFbBeta ? lds + C::OFF_PART + (q & 1) * NP : lds + C::OFF_RING + (q & (C::RING - 1)) * NP;
-  float x = 0.f;
-#pragma unroll
-  for (int m = 0; m < NP / 64; ++m) x += src[64 * m + l];
-  return wave_sum_bcast(x);
-}
 
 template <int NP, int KIND>
 __device__ __forceinline__ void rec_rb_helper(const RecArgs& a, float* lds, int b) {
@@ -935,51 +897,6 @@ __device__ __forceinline__ void rec_rb_helper(const RecArgs& a, float* lds, int 
   }
   lds_barrier();  // (the chain's: block 0 staged)
   lds_barrier();  // (the chain's: row 0 written)
-  float* sc = lds + C::OFF_SC;
-  // FB, the chain's multipliers (rec_run_rb; SC slot j holds k_{j+1}, the multiplier step j + 1
-  // applies), formed two steps ahead by ONE helper (hs), pipelined over two steps with its whole
-  // state in registers: in step q it reads its lanes' part of step q's input (the sum c_{q-1});
-  // in step q + 1, first thing after the barrier -- while the chain waves wait for their own
-  // LDS reads, so none of its dependent reduction lands on a step -- it reduces them and forms
-  //     k_{q+2} = c_{q-2}^2 k_{q-1}^2 / (c_{q-1}^3 k_q k_{q+1})
-  // (the exact 1 / s_{q+1} if the input sum s grew in steps q and q + 1 by its growth e_{q-1} of
-  // step q - 1, s_{q-1} = s_{q-2} e_{q-1} k_{q-1}).  Then log s_{q+2} = f_q + f_{q+1} + f_{q+2} -
-  // 2 f_{q-1} with f = log e: bounded by the emissions' range as the exact per-step normalisation
-  // (log s = f_q) is, and equal to it for a constant growth.  (A first version spread this over
-  // the helpers with the history in LDS: its scalar LDS reads pushed the reduction into the chain
-  // waves' compute phase and delayed the step barrier, FB op 0.85 -> 0.89 ms.)
-  constexpr int hs = NH - 1;
-  float cpart = 0.f, c_m1 = 1.f, k_m1 = 1.f, k_0 = 1.f, k_1 = 1.f;  // c_{p-3}, k_{p-2}, k_{p-1}, k_p
-  if constexpr (KIND != kVit && kFbScale != 0) {
-    // k_1 = k_2 = 1 / c_0 before step 1; the fictitious k_0 = c_{-1} = 1
-    if (h == hs) {
-      const float c0 = rb_input_sum<NP, KIND>(lds, 0);
-      k_0 = k_1 = 1.f / c0;
-      if (l == 0) {
-        sc[0] = k_0;
-        sc[64] = k_1;
-      }
-    }
-    lds_barrier();  // (the chain's third: k_1, k_2 out)
-  }
-  auto scale_read = [&](int q) {  // step q: this lane's part of c_{q-1}
-    const float* src = KIND == kFbBeta ? lds + C::OFF_PART + ((q - 1) & 1) * NP
-                                       : lds + C::OFF_RING + ((q - 1) & (C::RING - 1)) * NP;
-    float x = 0.f;
-#pragma unroll
-    for (int m = 0; m < NP / 64; ++m) x += src[64 * m + l];
-    cpart = x;
-  };
-  auto scale_math = [&](int p) {  // step p: c_{p-2} (read in step p - 1) -> k_{p+1} into slot p
-    const float c2 = wave_sum_bcast(cpart);
-    const float t = c_m1 * __builtin_amdgcn_rcpf(c2);  // ~ 1 / e_{p-2}
-    const float kn = (t * k_m1 * __builtin_amdgcn_rcpf(k_1)) * (t * k_m1 * __builtin_amdgcn_rcpf(c2 * k_0));
-    if (l == 0) sc[64 * (p & (C::RING - 1))] = kn;
-    c_m1 = c2;
-    k_m1 = k_0;
-    k_0 = k_1;
-    k_1 = kn;
-  };
   double base = (KIND == kFbBeta && a.bscale) ? (double)a.bscale[b] : 0.0;
   float lsv = 0.f;
   // psi followers (Viterbi, vit_kern.h): the count of flushed blocks, published once per 64-step
@@ -1011,7 +928,7 @@ __device__ __forceinline__ void rec_rb_helper(const RecArgs& a, float* lds, int 
       case 1: if (kb + 1 < nblocks) rec_stage<NP, KIND>(a, lds, kb + 1, 2 * h + 1, l, cur[1]); break;
       case 2: rec_load<NP, KIND>(a, b, kb + 2 < nblocks ? kb + 2 : nblocks - 1, 2 * h, l, nxt[0]); break;
       case 3: rec_load<NP, KIND>(a, b, kb + 2 < nblocks ? kb + 2 : nblocks - 1, 2 * h + 1, l, nxt[1]); break;
-      case 4: if (kb >= 2) lsv = rec_ls_scan<NP, KIND, kFbScale != 0>(a, lds, b, kb - 2, base, h == NH - 1); break;
+      case 4: if (kb >= 2) lsv = rec_ls_scan<NP, KIND>(a, lds, b, kb - 2, base, h == NH - 1); break;
       case 5: if (kb >= 2) rec_flush<NP, KIND>(a, lds, b, kb - 2, th, lsv); break;
       case 6:
         if (kb >= 2) {
@@ -1027,10 +944,6 @@ __device__ __forceinline__ void rec_rb_helper(const RecArgs& a, float* lds, int 
     const int q1 = (kb + 1) * 16 < T ? (kb + 1) * 16 : T;
     int it = 0;
     for (int q = q0; q < q1; ++q, ++it) {
-      if (KIND != kVit && kFbScale == 1 && h == hs) {
-        if (q >= 2) scale_math(q);
-        scale_read(q);
-      }
       if (it < kRbItems<KIND>) item(kb, it, cur, nxt);
       step_barrier();
     }
@@ -1044,11 +957,11 @@ __device__ __forceinline__ void rec_rb_helper(const RecArgs& a, float* lds, int 
   lds_barrier();  // (the chain's: the last rows and c_{T-1} written)
   static_assert(2 * NH * kWave == C::NT, "two flush passes cover the block");
   if (nblocks >= 2) {
-    lsv = rec_ls_scan<NP, KIND, kFbScale != 0>(a, lds, b, nblocks - 2, base, h == NH - 1);
+    lsv = rec_ls_scan<NP, KIND>(a, lds, b, nblocks - 2, base, h == NH - 1);
     rec_flush<NP, KIND>(a, lds, b, nblocks - 2, th, lsv);
     rec_flush<NP, KIND>(a, lds, b, nblocks - 2, th + NH * kWave, lsv);
   }
-  lsv = rec_ls_scan<NP, KIND, kFbScale != 0>(a, lds, b, nblocks - 1, base, h == NH - 1);
+  lsv = rec_ls_scan<NP, KIND>(a, lds, b, nblocks - 1, base, h == NH - 1);
   rec_flush<NP, KIND>(a, lds, b, nblocks - 1, th, lsv);
   rec_flush<NP, KIND>(a, lds, b, nblocks - 1, th + NH * kWave, lsv);
   if (follow) {
@@ -1096,6 +1009,8 @@ __device__ __forceinline__ void rec_run_rb(const RecArgs& a, float* lds, int b) 
     return;
   }
   // the chain waves issue first: a helper takes the SIMD only while they wait (LDS, barrier)
+  // (one priority for all chain waves: the younger half one level above the older half,
+  // MI355X_MICROARCH.md "Two waves per SIMD" item 4, measured the same, round 5)
   __builtin_amdgcn_s_setprio(2);
   const int w = tid >> 6, l = tid & 63, r = l >> 4, c = l & 15;
   const int g = 4 * w + r;      // output group
@@ -1144,7 +1059,6 @@ __device__ __forceinline__ void rec_run_rb(const RecArgs& a, float* lds, int b) 
     }
   }
   lds_barrier();
-  if (FB && kFbScale != 0) lds_barrier();  // (a helper forms k_1 = k_2 = 1 / c_0: rec_rb_helper)
 
   unsigned long long st_acc[4] = {0, 0, 0, 0}, st_prev = 0, st_t0 = 0, st_steps = 0;
   long long rt0 = 0;
@@ -1153,22 +1067,14 @@ __device__ __forceinline__ void rec_run_rb(const RecArgs& a, float* lds, int b) 
     if (kStamp) { const unsigned long long t = stamp(); st_acc[k] += t - st_prev; st_prev = t; }
   };
 
-  // FB scale modes (kFbScale): 0 every wave reduces c_{q-1} = sum of its input beside the products
-  // and applies 1 / c_{q-1} (the reciprocal on the chain); 1 one helper wave forms the multiplier
-  // two steps ahead (rec_rb_helper); 3 wave 0 alone reduces c_{q-1} and, after its row write, forms
-  // k_{q+1} = c_{q-2} k_{q-1} / (c_{q-1}^2 k_q) into SC slot q.  Modes 1 and 3 read k_q with the
-  // step's gather, so no reduction or reciprocal sits on any chain wave's critical path.
-  float h_c2 = 1.f, h_k1 = 1.f;  // mode 3, wave 0: c_{q-2}, k_{q-1}
-  auto step = [&](int q, auto withc) {
-    constexpr bool WITHC = decltype(withc)::value;
+  // one step q of the chain (ring row q from row q - 1)
+  auto stepq = [&](int q) {
     if (kStamp) mark(3);
     const float* src = KIND == kFbBeta ? Pv + ((q - 1) & 1) * NP : ring + ((q - 1) & (C::RING - 1)) * NP;
     // alpha / Viterbi: emission of output o; beta: of v_q -> P.  Read first and pinned below:
     // used only by the writer lanes, it would otherwise sink behind the reduction into their
     // branch and put an LDS round trip on the chain
     float eo = emis(q, o);
-    // FB (lagged modes): the multiplier of this step, formed a step or two ago
-    float kq = (FB && kFbScale != 0) ? lds[C::OFF_SC + 64 * ((q - 1) & (C::RING - 1))] : 0.f;
     f2 yin[NM][2];
 #pragma unroll
     for (int m = 0; m < NM; ++m) {
@@ -1177,7 +1083,6 @@ __device__ __forceinline__ void rec_run_rb(const RecArgs& a, float* lds, int b) 
       yin[m][1] = f2{v4.z, v4.w};
     }
     keep(eo);
-    if (FB && kFbScale != 0) keep(kq);
     if (kStamp) { keep(yin[0][0]); mark(0); }
     float s0, s1, s2, s3;
     float cs = 0.f;
@@ -1192,19 +1097,16 @@ __device__ __forceinline__ void rec_run_rb(const RecArgs& a, float* lds, int b) 
         for (int p = 0; p < 2; ++p) {
 #pragma unroll
           for (int k = 0; k < 4; ++k) acc[k] = __builtin_elementwise_fma(yin[m][p], Mk[k][m][p], acc[k]);
-          if (WITHC) ysum += yin[m][p];
+          ysum += yin[m][p];
         }
+      // c_{q-1}: the row's 16 lanes hold all NP inputs; an all-reduce of their sums (every
+      // lane, every row and every wave ends with the same bits), interleaved with the outputs'
+      // reduction (issue is in order within a wave)
+      float cx = ysum.x + ysum.y;
       s0 = acc[0].x + acc[0].y; s1 = acc[1].x + acc[1].y;
       s2 = acc[2].x + acc[2].y; s3 = acc[3].x + acc[3].y;
-      if (WITHC) {
-        // c_{q-1}: the row's 16 lanes hold all NP inputs; an all-reduce of their sums (every
-        // lane, every row and every wave ends with the same bits), interleaved with the outputs'
-        float cx = ysum.x + ysum.y;
-        red4_add_with_c(s0, s1, s2, s3, cx);
-        cs = cx;
-      } else {
-        red4_add(s0, s1, s2, s3);
-      }
+      red4_add_with_c(s0, s1, s2, s3, cx);
+      cs = cx;
     } else {
       // the four packed sums of one input pair first, then their max3 folds: no max waits on
       // the packed add just issued (tools/mb_dense.hip: 329 -> 291 ns per step), and the first
@@ -1227,14 +1129,10 @@ __device__ __forceinline__ void rec_run_rb(const RecArgs& a, float* lds, int b) 
     if (kStamp) { keep(s0); mark(1); }
     float val, pval = 0.f;
     if (FB) {
-      if (kFbScale == 0) {
-        const float scale = __builtin_amdgcn_rcpf(cs);
-        // (every lane holds the same c: wave 0 writes it, a wave-uniform branch)
-        if (w == 0) lds[C::OFF_SC + 64 * ((q - 1) & (C::RING - 1))] = cs;
-        val = KIND == kFbAlpha ? s0 * (scale * eo) : s0 * scale;  // alpha: u_q = z e_q / c;  beta: v_q = z / c
-      } else {
-        val = KIND == kFbAlpha ? s0 * (kq * eo) : s0 * kq;        // alpha: u_q = z e_q k_q;  beta: v_q = z k_q
-      }
+      const float scale = __builtin_amdgcn_rcpf(cs);
+      // (every lane holds the same c: wave 0 writes it, a wave-uniform branch)
+      if (w == 0) lds[C::OFF_SC + 64 * ((q - 1) & (C::RING - 1))] = cs;
+      val = KIND == kFbAlpha ? s0 * (scale * eo) : s0 * scale;  // alpha: u_q = z e_q / c;  beta: v_q = z / c
       if (KIND == kFbBeta) pval = val * eo;
     } else {
       val = s0 + eo;  // delta_q = max(...) + lo_q (exact: monotone)
@@ -1244,25 +1142,21 @@ __device__ __forceinline__ void rec_run_rb(const RecArgs& a, float* lds, int b) 
     // (tools/mb_dense.hip: 291 -> 268 ns per Viterbi step, 255 -> 229 ns FB)
     ring[(q & (C::RING - 1)) * NP + o] = val;
     if (KIND == kFbBeta) Pv[(q & 1) * NP + o] = pval;
-    if (FB && kFbScale == 3 && WITHC) {
-      // wave 0, behind its row write (in the write's latency, off the chain): k_{q+1}
-      __builtin_amdgcn_sched_barrier(0);
-      const float t = h_c2 * __builtin_amdgcn_rcpf(cs);
-      const float kn = t * h_k1 * __builtin_amdgcn_rcpf(cs * kq);
-      if (l == 0) lds[C::OFF_SC + 64 * (q & (C::RING - 1))] = kn;
-      h_c2 = cs;
-      h_k1 = kq;
-    }
     if (kStamp) { mark(2); ++st_steps; }
     step_barrier();
   };
   auto run_block = [&](int kb) {
     const int q0 = kb * 16 < 1 ? 1 : kb * 16;
     const int q1 = (kb + 1) * 16 < T ? (kb + 1) * 16 : T;
-    for (int q = q0; q < q1; ++q) {
-      if (!FB || kFbScale == 0) step(q, BoolTag<true>{});   // (Viterbi: the flag is unused)
-      else if (kFbScale == 3 && w == 0) step(q, BoolTag<true>{});
-      else step(q, BoolTag<false>{});
+    if (q0 == kb * 16 && q1 == q0 + 16) {
+      // a whole 16-step block, unrolled: the ring / staging indices of every step are the
+      // block's plus a constant, so no per-step scalar index arithmetic (round 5: the rolled
+      // loop spent ~20 SALU instructions per step on them; the dense FB op 714 -> 646 us,
+      // Viterbi 788 -> 764 us alone at B=32, T=2000, N=128, tools/ab.py, profiles/r5j_ab.log)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) stepq(kb * 16 + i);
+    } else {
+      for (int q = q0; q < q1; ++q) stepq(q);
     }
   };
   for (int k = 0; k < nblocks; ++k) run_block(k);

@@ -38,6 +38,8 @@
 //                   sum and predecessor score live in its slot's registers; ONE barrier per end
 //                   time, for the only cross-wave value, Dm (double-buffered in LDS).
 // smk_backtrace_kernel  one wave per sequence walks the segments back (semi_markov.py:548-568).
+#include <stdlib.h>
+
 #include "common.h"
 
 #pragma clang fp contract(off)
@@ -97,7 +99,7 @@ __device__ __forceinline__ float sm_seg_obs(float cs, float Q, bool gaussian) {
 __global__ void __launch_bounds__(256) smk_quad_kernel(const float* __restrict__ x, const float* __restrict__ muT,
                                                        const float* __restrict__ varT, int F, int Df, int S,
                                                        float* __restrict__ q) {
-  const int s = threadIdx.x & 63;
+  const int s = (threadIdx.x & 63) + 64 * blockIdx.y;
   const long long f = (long long)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (f >= F || s >= S) return;
   const float* xf = x + f * Df;
@@ -343,20 +345,268 @@ __global__ void __launch_bounds__(64) smk_backtrace_kernel(SmArgs a) {
   if (l == 0) a.seg_count[b] = k;
 }
 
+// ---------------------------------------------------------------- the general form
+// For S > 64 or Dmax > 63 (up to S, Dmax <= 1024), where the open segments no longer fit the
+// register slots of smk_fwd_kernel: the same recursion and the same fp32 operations in the same
+// order, with the segment scores and the predecessor history in the workspace instead of
+// registers (the design of hsmm_wide.hip).
+//   smk_wide_osum_kernel  o(st, d, s) = seg_obs(Q), Q = q[st] + ... + q[st+d-1] left to right
+//                         (the running sum smk_fwd_kernel keeps per slot, so the same bits),
+//                         one thread per (sequence, start, state), stored by END time
+//                         os[e][d-1][s] so the recursion reads coalesced rows over states.
+//   smk_wide_kernel       one 1024-thread workgroup per sequence; per end time t: phase 1,
+//                         Dm[t][s'] = max_d delta(t, s', d) (forward: LSE_d, and log alpha),
+//                         lanes over s', waves over d, partials through LDS; phase 2,
+//                         M[t][s] = max_{s' != s} fl(Dm[t][s'] + logT[s'][s]) (forward: LSE),
+//                         1024 / S threads per state (or states in turn).  Viterbi then walks
+//                         the segments in the same workgroup: each step's pointer is the first
+//                         candidate (s' ascending, d' ascending) whose fl(delta + logT) equals
+//                         M (semi_markov.py:513-530's strict >), found by one parallel pass over
+//                         the S * Dmax candidates instead of a stored argS.
+// Forward LSE sums run in another order than smk_fwd_kernel's (checked against float64, not bit
+// for bit); the Viterbi path and scores are bit-identical to the register form and to the
+// literal loop (tests/test_gpu_semimarkov.py).
+constexpr int kSwS = 1024;
+constexpr int kSwD = 1024;
+constexpr int kSwNT = 1024;
+
+struct SwArgs {
+  const float* q;      // (B,T,S)
+  const float* cseg;   // (S) or null
+  const float* li;     // (S)
+  const float* logT;   // (S,S)
+  const float* dur;    // (S,Dm)
+  float* Mg;           // (B,T,S) M[tau][s] (forward: L), for segments starting at tau + 1
+  float* os;           // (B,T,Dm,S) by end time
+  float* scores;       // (B)
+  float* alpha;        // (B,T,S,Dm) or null (forward)
+  int64_t* seg_states; // (B,T)
+  int64_t* seg_durs;   // (B,T)
+  int* seg_count;      // (B)
+  int B, T, S, Dm;
+};
+
+__global__ void __launch_bounds__(256) smk_wide_osum_kernel(SwArgs a) {
+  const size_t idx = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const size_t n = (size_t)a.B * a.T * a.S;
+  if (idx >= n) return;
+  const int s = (int)(idx % a.S);
+  const size_t bt = idx / a.S;
+  const int st = (int)(bt % a.T);
+  const int b = (int)(bt / a.T);
+  const bool gaussian = a.cseg != nullptr;
+  const float cs = gaussian ? a.cseg[s] : 0.f;
+  const float* col = a.q + ((size_t)b * a.T + st) * a.S + s;
+  float* out = a.os + (((size_t)b * a.T + st) * a.Dm) * a.S + s;
+  const size_t estep = (size_t)(a.Dm + 1) * a.S;  // (e + 1, d + 1) from (e, d)
+  const int dlim = a.Dm < a.T - st ? a.Dm : a.T - st;
+  float acc = 0.f;
+  for (int d = 1; d <= dlim; ++d) {
+    acc = d == 1 ? col[0] : acc + col[(size_t)(d - 1) * a.S];
+    out[(size_t)(d - 1) * estep] = sm_seg_obs(cs, acc, gaussian);
+  }
+}
+
+__device__ __forceinline__ float sw_fresh(const float* p) {  // M rows other waves wrote (L1 bypass)
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// delta(end t, state s, duration d) exactly as smk_fwd_kernel forms it
+__device__ __forceinline__ float sw_delta(const SwArgs& a, int b, int t, int s, int d) {
+  const int st = t - d + 1;
+  if (st < 0) return -INFINITY;
+  const float o = a.os[(((size_t)b * a.T + t) * a.Dm + (d - 1)) * a.S + s];
+  const float u = a.dur[(size_t)s * a.Dm + (d - 1)];
+  if (st == 0) return (a.li[s] + o) + u;
+  const float m = sw_fresh(a.Mg + ((size_t)b * a.T + (st - 1)) * a.S + s);
+  return m == -INFINITY ? -INFINITY : (m + o) + u;
+}
+
+// workgroup reductions over kSwNT threads: max of a float; min of an int
+__device__ __forceinline__ float wg_max_sw(float v, float* red) {
+  for (int off = 32; off >= 1; off >>= 1) v = fmaxf(v, __shfl_xor(v, off));
+  __syncthreads();
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
+  __syncthreads();
+  float r = red[0];
+  for (int k = 1; k < kSwNT / 64; ++k) r = fmaxf(r, red[k]);
+  return r;
+}
+__device__ __forceinline__ int wg_min_sw(int v, int* red) {
+  for (int off = 32; off >= 1; off >>= 1) v = min(v, __shfl_xor(v, off));
+  __syncthreads();
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
+  __syncthreads();
+  int r = red[0];
+  for (int k = 1; k < kSwNT / 64; ++k) r = min(r, red[k]);
+  return r;
+}
+
+// (max, sum of exp(x - max)) pairs: the online log-sum-exp merge
+__device__ __forceinline__ void lse_merge(float& m, float& z, float m2, float z2) {
+  if (m2 == -INFINITY) return;
+  if (m == -INFINITY) { m = m2; z = z2; return; }
+  if (m2 > m) { z = z * __expf(m - m2) + z2; m = m2; }
+  else z = z + z2 * __expf(m2 - m);
+}
+
+template <bool kViterbi>
+__global__ void __launch_bounds__(kSwNT) smk_wide_kernel(SwArgs a) {
+  __shared__ float dm[kSwS];     // Dm[t][s'] (forward: A[t][s'])
+  __shared__ float pm[kSwNT];    // phase-2 partials (max)
+  __shared__ float pz[kSwNT];    //                  (forward: sum)
+  __shared__ float redf[kSwNT / 64];
+  __shared__ int redi[kSwNT / 64];
+  extern __shared__ float part[];  // [16][S] phase-1 partial maxima, then [16][S] sums (forward)
+  const int b = blockIdx.x, tid = threadIdx.x, w = tid >> 6, l = tid & 63;
+  const int T = a.T, S = a.S, Dm = a.Dm;
+  constexpr int NWv = kSwNT / 64;
+  float* Mrow = a.Mg + (size_t)b * T * S;
+  float* alpha = a.alpha ? a.alpha + (size_t)b * T * S * Dm : nullptr;
+  for (int t = 0; t < T; ++t) {
+    // ---- phase 1: lanes over s', waves over d
+    for (int s0 = 0; s0 < S; s0 += 64) {
+      const int sp = s0 + l;
+      if (sp < S) {
+        float m = -INFINITY, z = 0.f;
+        for (int d = w + 1; d <= Dm; d += NWv) {
+          const float v = sw_delta(a, b, t, sp, d);
+          if (alpha) alpha[((size_t)t * S + sp) * Dm + d - 1] = v;
+          if (kViterbi) m = fmaxf(m, v);
+          else lse_merge(m, z, v, 1.f);
+        }
+        part[w * S + sp] = m;
+        if (!kViterbi) part[(NWv + w) * S + sp] = z;
+      }
+    }
+    __syncthreads();
+    for (int sp = tid; sp < S; sp += kSwNT) {
+      float m = part[sp], z = kViterbi ? 0.f : part[NWv * S + sp];
+      for (int k = 1; k < NWv; ++k) {
+        if (kViterbi) m = fmaxf(m, part[k * S + sp]);
+        else lse_merge(m, z, part[k * S + sp], part[(NWv + k) * S + sp]);
+      }
+      dm[sp] = kViterbi ? m : (m == -INFINITY ? -INFINITY : m + __logf(z));
+    }
+    __syncthreads();
+    if (t == T - 1) break;
+    // ---- phase 2: M[t][s] over s' != s (P threads per state, or states in turn)
+    const int P = S <= kSwNT ? kSwNT / S : 1;
+    for (int s0 = 0; s0 < S; s0 += kSwNT / P) {
+      const int s = s0 + tid / P, pt = tid % P;
+      float m = -INFINITY, z = 0.f;
+      if (s < S) {
+        for (int sp = pt; sp < S; sp += P) {
+          const float lt = a.logT[(size_t)sp * S + s];
+          const float dv = dm[sp];
+          const float c = (sp == s || lt == -INFINITY || dv == -INFINITY) ? -INFINITY : dv + lt;
+          if (kViterbi) m = fmaxf(m, c);
+          else lse_merge(m, z, c, 1.f);
+        }
+      }
+      pm[tid] = m;
+      pz[tid] = z;
+      __syncthreads();
+      if (s < S && pt == 0) {
+        for (int k = 1; k < P; ++k) {
+          if (kViterbi) m = fmaxf(m, pm[tid + k]);
+          else lse_merge(m, z, pm[tid + k], pz[tid + k]);
+        }
+        Mrow[(size_t)t * S + s] = kViterbi ? m : (m == -INFINITY ? -INFINITY : m + __logf(z));
+      }
+      __syncthreads();
+    }
+    // the M row is read by other waves (sw_fresh, from L2): the stores complete first
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  }
+  // ---- final (dm holds row T-1)
+  if constexpr (!kViterbi) {
+    float m = -INFINITY, z = 0.f;
+    for (int s = tid; s < S; s += kSwNT) lse_merge(m, z, dm[s], 1.f);
+    for (int off = 32; off >= 1; off >>= 1) {
+      const float m2 = __shfl_xor(m, off), z2 = __shfl_xor(z, off);
+      lse_merge(m, z, m2, z2);
+    }
+    if (l == 0) { pm[w] = m; pz[w] = z; }
+    __syncthreads();
+    if (tid == 0) {
+      for (int k = 1; k < NWv; ++k) lse_merge(m, z, pm[k], pz[k]);
+      a.scores[b] = m == -INFINITY ? -INFINITY : m + __logf(z);
+    }
+    return;
+  } else {
+    // first (s ascending, d ascending) with the best delta (semi_markov.py:548-556)
+    float bv = -INFINITY;
+    for (int s = tid; s < S; s += kSwNT) bv = fmaxf(bv, dm[s]);
+    const float best = wg_max_sw(bv, redf);
+    const int nk = S * Dm;
+    int bk = 0x7fffffff;
+    if (best != -INFINITY)
+      for (int j = tid; j < nk; j += kSwNT) {
+        const int s = j % S, d = j / S + 1;
+        if (sw_delta(a, b, T - 1, s, d) == best) bk = min(bk, s * Dm + d - 1);
+      }
+    bk = wg_min_sw(bk, redi);
+    int cs = 0, cd = 1;  // every score -inf: the reference's defaults
+    if (bk != 0x7fffffff) { cs = bk / Dm; cd = bk % Dm + 1; }
+    if (tid == 0) a.scores[b] = best;
+    // ---- segment walk (semi_markov.py:558-568), right-aligned output as smk_backtrace_kernel
+    int t = T - 1, k = 0;
+    while (t >= 0) {
+      if (tid == 0) {
+        a.seg_states[(size_t)b * T + (T - 1 - k)] = cs;
+        a.seg_durs[(size_t)b * T + (T - 1 - k)] = cd;
+      }
+      ++k;
+      const int tau = t - cd;
+      if (tau < 0) break;
+      const float M = sw_fresh(Mrow + (size_t)tau * S + cs);
+      int ns = 0, nd = 1;
+      if (M != -INFINITY) {
+        const int dlim = Dm < tau + 1 ? Dm : tau + 1;
+        int win = 0x7fffffff;
+        for (int j = tid; j < S * dlim; j += kSwNT) {
+          const int sp = j % S, dp = j / S + 1;
+          if (sp == cs) continue;
+          const float lt = a.logT[(size_t)sp * S + cs];
+          const float dv = sw_delta(a, b, tau, sp, dp);
+          if (lt != -INFINITY && dv != -INFINITY && dv + lt == M) win = min(win, sp * Dm + dp - 1);
+        }
+        win = wg_min_sw(win, redi);
+        if (win != 0x7fffffff) { ns = win / Dm; nd = win % Dm + 1; }
+      }
+      t = tau;
+      cs = ns;
+      cd = nd;
+      __syncthreads();
+    }
+    if (tid == 0) a.seg_count[b] = k;
+  }
+}
+
 }  // namespace hmm355
 
 using namespace hmm355;
 
+// the register form holds S <= 64, Dmax <= 63; the general form the rest (HMM355_SMK_WIDE=1
+// forces it, for tests and comparison)
+static bool smk_wide(int S, int Dmax) {
+  const char* e = getenv("HMM355_SMK_WIDE");
+  return (S > kSmS || Dmax >= kSmR) || (e && e[0] == '1');
+}
+
 HMM355_API size_t hmm355_semimarkov_workspace_bytes(int B, int T, int S, int Dmax) {
-  if (B < 0 || T < 1 || S < 1 || S > kSmS || Dmax < 1 || Dmax >= kSmR) return 0;
+  if (B < 0 || T < 1 || S < 1 || S > kSwS || Dmax < 1 || Dmax > kSwD) return 0;
   const size_t n = (size_t)B * T * S;
+  if (smk_wide(S, Dmax)) return align_up(n * 4, 256) + align_up(n * (size_t)Dmax * 4, 256);
   return align_up(n * 4, 256) + align_up(n * 4, 256) + align_up(n, 256) + align_up((size_t)B * 8, 256);
 }
 
 static int smk_check(int B, int T, int S, int Dmax) {
   if (B < 0 || S < 0 || Dmax < 0) return HMM355_E_ARG;
-  if (S < 1 || S > kSmS) return HMM355_E_STATES;
-  if (Dmax < 1 || Dmax >= kSmR) return HMM355_E_DURATION;
+  if (S < 1 || S > kSwS) return HMM355_E_STATES;
+  if (Dmax < 1 || Dmax > kSwD) return HMM355_E_DURATION;
   if (T < 1) return HMM355_E_SHAPE;
   return HMM355_OK;
 }
@@ -364,11 +614,11 @@ static int smk_check(int B, int T, int S, int Dmax) {
 HMM355_API int hmm355_semimarkov_quad_f32(const float* x, const float* means_t, const float* vars_t, int B, int T,
                                           int Df, int S, float* quad, void* stream) {
   if (B < 0 || T < 0 || Df < 1) return HMM355_E_ARG;
-  if (S < 1 || S > kSmS) return HMM355_E_STATES;
+  if (S < 1 || S > kSwS) return HMM355_E_STATES;
   const long long F = (long long)B * T;
   if (F == 0) return HMM355_OK;
   if (!x || !means_t || !vars_t || !quad) return HMM355_E_ARG;
-  hipLaunchKernelGGL(smk_quad_kernel, dim3((unsigned)((F + 3) / 4)), dim3(256), 0,
+  hipLaunchKernelGGL(smk_quad_kernel, dim3((unsigned)((F + 3) / 4), (unsigned)((S + 63) / 64)), dim3(256), 0,
                      static_cast<hipStream_t>(stream), x, means_t, vars_t, (int)F, Df, S, quad);
   const hipError_t e = hipGetLastError();
   return e == hipSuccess ? HMM355_OK : (int)e;
@@ -386,6 +636,25 @@ static int smk_run(bool viterbi, const float* quad, const float* seg_const, cons
   if (workspace_bytes < hmm355_semimarkov_workspace_bytes(B, T, S, Dmax)) return HMM355_E_WORKSPACE;
   const size_t n = (size_t)B * T * S;
   char* ws = static_cast<char*>(workspace);
+  if (smk_wide(S, Dmax)) {
+    SwArgs wa{quad, seg_const, log_init, log_T, dur_lp, reinterpret_cast<float*>(ws),
+              reinterpret_cast<float*>(ws + align_up(n * 4, 256)), scores, alpha, seg_states, seg_durs, seg_count,
+              B, T, S, Dmax};
+    hipStream_t st = static_cast<hipStream_t>(stream);
+    hipLaunchKernelGGL(smk_wide_osum_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, wa);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return (int)e;
+    const size_t lds = (viterbi ? 1 : 2) * (kSwNT / 64) * (size_t)S * sizeof(float);
+    if (viterbi) {
+      if ((e = allow_lds(smk_wide_kernel<true>, lds)) != hipSuccess) return (int)e;
+      hipLaunchKernelGGL(smk_wide_kernel<true>, dim3(B), dim3(kSwNT), lds, st, wa);
+    } else {
+      if ((e = allow_lds(smk_wide_kernel<false>, lds)) != hipSuccess) return (int)e;
+      hipLaunchKernelGGL(smk_wide_kernel<false>, dim3(B), dim3(kSwNT), lds, st, wa);
+    }
+    e = hipGetLastError();
+    return e == hipSuccess ? HMM355_OK : (int)e;
+  }
   float* Mg = reinterpret_cast<float*>(ws);
   uint8_t* argS = reinterpret_cast<uint8_t*>(ws + 2 * align_up(n * 4, 256));
   int* fin = reinterpret_cast<int*>(ws + 2 * align_up(n * 4, 256) + align_up(n, 256));

@@ -41,13 +41,34 @@ hipError_t launch_vit(const VitArgs& va, bool prep, bool tail, hipStream_t sm);
 
 using namespace hmm355;
 
+// OBS_PROB emissions of a dense plan: log(x + 1e-8) correctly rounded (logcr.h, the fp32 sum as
+// hmm.py:152 forms it) in one full-chip pass before the chain, which then stages them as
+// OBS_LOG.  The banded chain takes the log in its staging helpers for free (they sit on SIMDs
+// the single chain wave does not use); the dense chain's helpers share their SIMDs with the
+// chain waves, and the log there cost the chain ~60 ns per step (vit_fwd 725 us OBS_PROB vs
+// 603 us OBS_LOG at B=32, T=2000, N=128, profiles/r5h_*): this pass moves 2 x 33 MB instead.
+__global__ void __launch_bounds__(256) vit_log_obs_kernel(const float* __restrict__ x, float* __restrict__ lo,
+                                                          size_t n, int vec) {
+  const size_t n4 = vec ? n / 4 : 0;
+  const size_t stride = (size_t)gridDim.x * blockDim.x;
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += stride) {
+    const float4 v = reinterpret_cast<const float4*>(x)[i];
+    reinterpret_cast<float4*>(lo)[i] = make_float4(logcr_fast(v.x + 1e-8f, g_logcr_tab), logcr_fast(v.y + 1e-8f, g_logcr_tab),
+                                                   logcr_fast(v.z + 1e-8f, g_logcr_tab), logcr_fast(v.w + 1e-8f, g_logcr_tab));
+  }
+  for (size_t i = 4 * n4 + (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride)
+    lo[i] = logcr_fast(x[i] + 1e-8f, g_logcr_tab);
+}
+
 HMM355_API size_t hmm355_viterbi_workspace_bytes(int B, int T, int N) {
   if (B < 0 || T < 1 || N < 1 || N > 256) return 0;
   const size_t NP = pad_states(N);
   const size_t nc = (T + kChunk - 1) / kChunk;
-  // psi rows, chunk maps, the plan-less band descriptor, the psi followers' progress and done words
+  // psi rows, chunk maps, the plan-less band descriptor, the log-emissions of a dense plan, the
+  // psi followers' progress and done words (last)
   return align_up((size_t)B * T * NP, 256) + align_up((size_t)B * nc * NP, 256) + align_up(sizeof(BandDesc), 256) +
-         align_up((size_t)B * kProgSlots * sizeof(int), 256) + align_up((size_t)B * nc, 256);
+         align_up((size_t)B * T * N * sizeof(float), 256) + align_up((size_t)B * kProgSlots * sizeof(int), 256) +
+         align_up((size_t)B * nc, 256);
 }
 
 // CUs of the current device (cached per device): the psi followers take the ones the chain
@@ -83,7 +104,8 @@ HMM355_API int hmm355_viterbi_plan_ex_f32(const float* obs, int obs_mode, const 
   uint8_t* psi = static_cast<uint8_t*>(workspace);
   uint8_t* G = psi + align_up((size_t)B * T * NP, 256);
   uint8_t* bandp = G + align_up((size_t)B * nc * NP, 256);
-  int* prog = reinterpret_cast<int*>(bandp + align_up(sizeof(BandDesc), 256));
+  float* lobuf = reinterpret_cast<float*>(bandp + align_up(sizeof(BandDesc), 256));
+  int* prog = reinterpret_cast<int*>(reinterpret_cast<uint8_t*>(lobuf) + align_up((size_t)B * T * N * sizeof(float), 256));
   uint8_t* done = reinterpret_cast<uint8_t*>(prog) + align_up((size_t)B * kProgSlots * sizeof(int), 256);
   BandDesc* band = use_band() ? (plan ? static_cast<BandDesc*>(const_cast<void*>(plan))
                                       : reinterpret_cast<BandDesc*>(bandp))
@@ -118,6 +140,16 @@ HMM355_API int hmm355_viterbi_plan_ex_f32(const float* obs, int obs_mode, const 
     va.done = done;
   }
   hipError_t e;
+  if ((flags & HMM355_VIT_PLAN_DENSE) && plan && obs_mode == HMM355_OBS_PROB) {
+    const size_t n = (size_t)B * T * N;
+    size_t blocks = (n / 4 + 255) / 256;
+    blocks = blocks < 8192 ? (blocks > 0 ? blocks : 1) : 8192;
+    const int vec = (reinterpret_cast<uintptr_t>(obs) & 15) == 0;  // (lobuf is 256-B aligned)
+    hipLaunchKernelGGL(vit_log_obs_kernel, dim3((unsigned)blocks), dim3(256), 0, sm, obs, lobuf, n, vec);
+    if ((e = hipGetLastError()) != hipSuccess) return (int)e;
+    va.obs = lobuf;
+    va.obs_mode = HMM355_OBS_LOG;
+  }
   switch (NP) {
     case 64: e = launch_vit<64>(va, plan == nullptr, false, sm); break;
     case 128: e = launch_vit<128>(va, plan == nullptr, tail, sm); break;

@@ -231,18 +231,7 @@ def hsmm_viterbi(lp: Tensor, dur_lp: Tensor, log_T: Tensor) -> Tuple[Tensor, Ten
     # The general form (S or Dmax beyond the register-slot kernels) keeps a (B,T,S,Dmax+1) fp32
     # table: checked against the device's free memory up front, and decoded in batch slices
     # that fit when the whole batch does not (sequences are independent).
-    per_seq = L.hmm355_hsmm_workspace_bytes(1, T, S, Dm)
-    need = L.hmm355_hsmm_workspace_bytes(B, T, S, Dm)
-    Bc = B
-    if need > _HSMM_WS_CHECK_BYTES:
-        free, _ = torch.cuda.mem_get_info(dev)
-        avail = free + torch.cuda.memory_reserved(dev) - torch.cuda.memory_allocated(dev)
-        if per_seq > 0.9 * avail:
-            raise torch.cuda.OutOfMemoryError(
-                f"HSMM decode of one sequence (T={T}, S={S}, max_duration={Dm}) needs "
-                f"{per_seq / 2**30:.1f} GiB of workspace (T*S*(max_duration+1)*4 bytes), "
-                f"{avail / 2**30:.1f} GiB are available on {dev}")
-        Bc = max(1, min(B, int(0.9 * avail) // per_seq))
+    Bc = _ws_batch(L.hmm355_hsmm_workspace_bytes, B, T, S, Dm, dev, "HSMM decode")
     ws = _workspace(L.hmm355_hsmm_workspace_bytes(Bc, T, S, Dm), dev)
     with torch.cuda.device(dev):
         for b0 in range(0, B, Bc):
@@ -255,6 +244,23 @@ def hsmm_viterbi(lp: Tensor, dur_lp: Tensor, log_T: Tensor) -> Tuple[Tensor, Ten
 
 
 _HSMM_WS_CHECK_BYTES = 1 << 30  # workspaces above this are checked against free device memory
+
+
+def _ws_batch(ws_bytes, B, T, S, Dm, dev, what):
+    """The batch slice whose workspace fits the device (general-form segment recursions keep a
+    (B,T,S,Dmax) fp32 table): B when the whole batch's workspace is small or fits, else the
+    largest slice that fits; OutOfMemoryError when not even one sequence does."""
+    need = ws_bytes(B, T, S, Dm)
+    if need <= _HSMM_WS_CHECK_BYTES:
+        return B
+    per_seq = ws_bytes(1, T, S, Dm)
+    free, _ = torch.cuda.mem_get_info(dev)
+    avail = free + torch.cuda.memory_reserved(dev) - torch.cuda.memory_allocated(dev)
+    if per_seq > 0.9 * avail:
+        raise torch.cuda.OutOfMemoryError(
+            f"{what} of one sequence (T={T}, S={S}, max_duration={Dm}) needs {per_seq / 2**30:.1f} GiB "
+            f"of workspace (about T*S*max_duration*4 bytes), {avail / 2**30:.1f} GiB are available on {dev}")
+    return max(1, min(B, int(0.9 * avail) // per_seq))
 
 
 @hsmm_viterbi.register_fake
@@ -439,12 +445,15 @@ def semimarkov_viterbi(quad: Tensor, seg_const: Optional[Tensor], log_init: Tens
     if B == 0:
         return seg_s, seg_d, cnt, scores
     L = nat.lib()
-    ws = _workspace(L.hmm355_semimarkov_workspace_bytes(B, T, S, Dm), dev)
+    Bc = _ws_batch(L.hmm355_semimarkov_workspace_bytes, B, T, S, Dm, dev, "semi-Markov decode")
+    ws = _workspace(L.hmm355_semimarkov_workspace_bytes(Bc, T, S, Dm), dev)
     with torch.cuda.device(dev):
-        nat.check(L.hmm355_semimarkov_viterbi_f32(
-            nat.ptr(quad), nat.ptr(seg_const), nat.ptr(log_init), nat.ptr(log_T), nat.ptr(dur_lp),
-            B, T, S, Dm, nat.ptr(seg_s), nat.ptr(seg_d), nat.ptr(cnt), nat.ptr(scores),
-            nat.ptr(ws), ws.numel(), nat.stream_of(dev)))
+        for b0 in range(0, B, Bc):
+            nb = min(Bc, B - b0)
+            nat.check(L.hmm355_semimarkov_viterbi_f32(
+                nat.ptr(quad[b0:b0 + nb]), nat.ptr(seg_const), nat.ptr(log_init), nat.ptr(log_T), nat.ptr(dur_lp),
+                nb, T, S, Dm, nat.ptr(seg_s[b0:b0 + nb]), nat.ptr(seg_d[b0:b0 + nb]), nat.ptr(cnt[b0:b0 + nb]),
+                nat.ptr(scores[b0:b0 + nb]), nat.ptr(ws), ws.numel(), nat.stream_of(dev)))
     return seg_s, seg_d, cnt, scores
 
 
@@ -466,12 +475,15 @@ def semimarkov_forward(quad: Tensor, seg_const: Optional[Tensor], log_init: Tens
     if B == 0:
         return lp, alpha
     L = nat.lib()
-    ws = _workspace(L.hmm355_semimarkov_workspace_bytes(B, T, S, Dm), dev)
+    Bc = _ws_batch(L.hmm355_semimarkov_workspace_bytes, B, T, S, Dm, dev, "semi-Markov forward")
+    ws = _workspace(L.hmm355_semimarkov_workspace_bytes(Bc, T, S, Dm), dev)
     with torch.cuda.device(dev):
-        nat.check(L.hmm355_semimarkov_forward_f32(
-            nat.ptr(quad), nat.ptr(seg_const), nat.ptr(log_init), nat.ptr(log_T), nat.ptr(dur_lp),
-            B, T, S, Dm, nat.ptr(alpha) if want_alpha else None, nat.ptr(lp),
-            nat.ptr(ws), ws.numel(), nat.stream_of(dev)))
+        for b0 in range(0, B, Bc):
+            nb = min(Bc, B - b0)
+            nat.check(L.hmm355_semimarkov_forward_f32(
+                nat.ptr(quad[b0:b0 + nb]), nat.ptr(seg_const), nat.ptr(log_init), nat.ptr(log_T), nat.ptr(dur_lp),
+                nb, T, S, Dm, nat.ptr(alpha[b0:b0 + nb]) if want_alpha else None, nat.ptr(lp[b0:b0 + nb]),
+                nat.ptr(ws), ws.numel(), nat.stream_of(dev)))
     return lp, alpha
 
 

@@ -161,3 +161,75 @@ def test_c5_shape_smoke():
             sup = m(x[b:b + 1], st.unsqueeze(0), du.unsqueeze(0))["log_probability"]
         li = float(m._log_initial()[int(st[0])])
         assert abs(float(sup) + li - float(sc)) <= 2e-6 * abs(float(sc)), (float(sup), li, float(sc))
+
+
+# ------------------------------------------------------------------ the general form (S > 64 / Dmax > 63)
+@pytest.mark.parametrize("seed,B,T,S,Dm,gaussian,ties", [
+    (20, 2, 60, 70, 10, True, False),     # S > 64
+    (21, 1, 200, 5, 80, True, False),     # Dmax > 63
+    (22, 2, 150, 3, 100, False, True),    # Dmax > 63, tie-heavy
+    (23, 1, 40, 130, 6, True, True),      # S > 128, tie-heavy
+    (24, 2, 1, 90, 70, True, False),      # T = 1
+    (25, 1, 70, 66, 64, False, False),    # both just past the register form
+])
+def test_wide_viterbi_bitexact_vs_literal(seed, B, T, S, Dm, gaussian, ties):
+    """SemiMarkovHMM.viterbi_decode (semi_markov.py:455-570) beyond the register form's S <= 64,
+    Dmax <= 63: csrc/semimarkov.hip smk_wide_kernel, bit-exact (segments and score) against
+    the literal loop."""
+    rng = np.random.default_rng(seed)
+    q, cs, li, lT, du = random_tables(rng, B, T, S, Dm, gaussian, ties)
+    got = gpu_viterbi(q, cs, li, lT, du)
+    for b in range(B):
+        ss, sd, sc = O.c_smk_viterbi(q[b], cs, li, lT, du)
+        gs, gd, gsc = got[b]
+        assert np.array_equal(gs, ss) and np.array_equal(gd, sd), (b, gs, ss, gd, sd)
+        assert np.float32(gsc) == np.float32(sc) or (np.isinf(gsc) and np.isinf(sc)), (gsc, sc)
+
+
+def test_wide_forced_equals_register_form(monkeypatch):
+    """HMM355_SMK_WIDE=1 forces the general form on a size the register form holds: the same
+    segments and scores bit for bit, the forward within float64 tolerance of both."""
+    rng = np.random.default_rng(30)
+    for gaussian, ties in ((True, False), (False, True)):
+        q, cs, li, lT, du = random_tables(rng, 3, 300, 20, 30, gaussian, ties)
+        monkeypatch.setenv("HMM355_SMK_WIDE", "0")
+        a = gpu_viterbi(q, cs, li, lT, du)
+        fa = ops.semimarkov_forward(t(q), None if cs is None else t(cs), t(li), t(lT), t(du), True)
+        monkeypatch.setenv("HMM355_SMK_WIDE", "1")
+        b = gpu_viterbi(q, cs, li, lT, du)
+        fb = ops.semimarkov_forward(t(q), None if cs is None else t(cs), t(li), t(lT), t(du), True)
+        for (s1, d1, c1), (s2, d2, c2) in zip(a, b):
+            assert np.array_equal(s1, s2) and np.array_equal(d1, d2) and np.float32(c1) == np.float32(c2)
+        np.testing.assert_allclose(fb[0].cpu().numpy(), fa[0].cpu().numpy(), rtol=2e-6)
+        la, lb = fa[1].cpu().numpy(), fb[1].cpu().numpy()
+        assert np.array_equal(np.isfinite(la), np.isfinite(lb))
+        np.testing.assert_allclose(lb[np.isfinite(lb)], la[np.isfinite(la)], rtol=2e-6, atol=2e-4)
+
+
+@pytest.mark.parametrize("seed,B,T,S,Dm,gaussian", [(40, 1, 50, 72, 8, True), (41, 2, 120, 4, 90, False)])
+def test_wide_forward_vs_fp64(seed, B, T, S, Dm, gaussian):
+    rng = np.random.default_rng(seed)
+    q, cs, li, lT, du = random_tables(rng, B, T, S, Dm, gaussian)
+    lp, la = ops.semimarkov_forward(t(q), None if cs is None else t(cs), t(li), t(lT), t(du), True)
+    lp, la = lp.cpu().numpy(), la.cpu().numpy()
+    for b in range(B):
+        tot, ra = O.c_smk_forward64(q[b], cs, li, lT, du)
+        assert abs(lp[b] - tot) <= 2e-6 * max(1.0, abs(tot)), (lp[b], tot)
+        fin = np.isfinite(ra)
+        assert np.array_equal(fin, np.isfinite(la[b]))
+        np.testing.assert_allclose(la[b][fin], ra[fin], rtol=2e-6, atol=2e-4)
+
+
+def test_wide_module_large_model():
+    """SemiMarkovHMM(68 states, max_duration 66) end to end through the module: the quad table
+    for S > 64 and the general-form decode, checked against the literal loop on the module's
+    own tables."""
+    torch.manual_seed(3)
+    m = SemiMarkovHMM(68, 12, max_duration=66).to(DEV)
+    x = torch.randn(1, 90, 12, device=DEV)
+    (st, du, sc), = m.viterbi_decode_batch(x)
+    with torch.no_grad():
+        q, cs, li, lT, dtab = (v.cpu().numpy() if v is not None else None for v in m._tables(x))
+    ss, sd, sref = O.c_smk_viterbi(q[0], cs, li, lT, dtab)
+    assert np.array_equal(st.cpu().numpy(), ss) and np.array_equal(du.cpu().numpy(), sd)
+    assert np.float32(float(sc)) == np.float32(sref)

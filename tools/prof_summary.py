@@ -40,7 +40,7 @@ for k, c in counters.items():
 # band_prep_kernel runs once per transition plan (HMMPyTorch measures its fixed log_P once),
 # not per launch of an op, so it is not part of an op's per-launch sum
 ops = {"forward_backward": ["fb_recur_kernel", "fb_posterior_kernel"],
-       "viterbi": ["log_obs_kernel", "vit_fwd_kernel", "vit_psi_kernel", "vit_backtrace_kernel"]}
+       "viterbi": ["vit_log_obs_kernel", "vit_fwd_kernel", "vit_psi_kernel", "vit_backtrace_kernel"]}
 op_sum = {}
 for op, ks in ops.items():
     sel = [k for k in stats if k.split("<")[0] in ks]
@@ -51,5 +51,7 @@ for f in glob.glob(os.path.join(D, "bench_trace.log")):
     for line in open(f):
         if line.startswith("{"):
             bench = json.loads(line)
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from bench import csrc_sha16  # noqa: E402  (the kernel sources these counters were taken on)
 print(json.dumps({"kernels": stats, "traffic": traffic, "ops": op_sum,
-                  "bench_config": bench["config"] if bench else None}, indent=1))
+                  "bench_config": bench["config"] if bench else None, "csrc_sha16": csrc_sha16()}, indent=1))
