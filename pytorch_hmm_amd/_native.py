@@ -34,7 +34,7 @@ EXPORTS = (
     "hmm355_semimarkov_viterbi_f32", "hmm355_semimarkov_forward_f32",
     "hmm355_stream_greedy_f32", "hmm355_stream_beam_f32",
     "hmm355_plan_bytes", "hmm355_plan_f32", "hmm355_plan_banded", "hmm355_forward_backward_plan_f32", "hmm355_viterbi_plan_f32",
-    "hmm355_viterbi_plan_ex_f32",
+    "hmm355_viterbi_plan_ex_f32", "hmm355_viterbi_part_f32", "hmm355_gmm_diag_logprob_slice_f32",
     "hmm355_fb_adjoint_f32", "hmm355_tv_fb_adjoint_f32",
 )
 
@@ -102,6 +102,10 @@ def lib():
     L.hmm355_viterbi_plan_f32.restype = I
     L.hmm355_viterbi_plan_ex_f32.argtypes = [P, I, P, P, P, U, I, I, I, P, P, P, P, S, P]
     L.hmm355_viterbi_plan_ex_f32.restype = I
+    L.hmm355_viterbi_part_f32.argtypes = [P, I, P, P, P, U, I, I, I, I, I, P, P, P, P, S, P]
+    L.hmm355_viterbi_part_f32.restype = I
+    L.hmm355_gmm_diag_logprob_slice_f32.argtypes = [P, P, P, P, I, I, I, I, I, I, I, I, P, P, S, P]
+    L.hmm355_gmm_diag_logprob_slice_f32.restype = I
     L.hmm355_stream_greedy_f32.argtypes, L.hmm355_stream_greedy_f32.restype = [P, P, P, F, I, I, I, P, P, P], I
     L.hmm355_stream_beam_f32.argtypes = [P, P, I, I, I, I, I, P, P, P, P, P, P, P, P]
     L.hmm355_stream_beam_f32.restype = I

@@ -221,8 +221,16 @@ __global__ void __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(kG
                                                              const double* __restrict__ cst,
                                                              float* __restrict__ out, int nframes, int D,
                                                              int NDC, int S, int C, int P, int PP,
-                                                             int mix_lse) {
+                                                             int mix_lse, int T, int t0, int L) {
   using G = G4<FG, NW, kG4Nf>;
+  // frame f of this launch is row f + (f / L) (T - L) + t0 of x / out: the time slice
+  // [t0, t0 + L) of every sequence (L = T, t0 = 0: every frame in order, no division)
+  const bool sliced = L != T;
+  auto row_of = [&](size_t f) -> size_t {
+    if (!sliced) return f;
+    const unsigned q = (unsigned)f / (unsigned)L;  // (frames < 2^31: gmm_run checks)
+    return f + (size_t)q * (size_t)(T - L) + (size_t)t0;
+  };
   __shared__ double2 ps[2][G::PS];
   __shared__ double xs[2][G::XS];
   const int tid = threadIdx.x, w = tid >> 6, l = tid & 63;
@@ -279,7 +287,7 @@ __global__ void __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(kG
       const int f = i / kG4Dc, k = i % kG4Dc;
       const size_t frame = f0 + f;
       const int d = dc * kG4Dc + k;
-      pre_x[r] = (i < G::FT * kG4Dc && frame < (size_t)nframes && d < D) ? x[frame * D + d] : 0.f;
+      pre_x[r] = (i < G::FT * kG4Dc && frame < (size_t)nframes && d < D) ? x[row_of(frame) * D + d] : 0.f;
     }
   };
   auto stage_x = [&](int buf) {
@@ -388,18 +396,19 @@ __global__ void __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(kG
         for (int cc = 0; cc < C; ++cc) e += expf((float)(v[j0 + cc] - m));
         r = (double)logf(fmaxf(e, 1e-8f)) + m;  // :149-153
       }
-      out[frame * S + p0 / C] = (float)r;
+      out[row_of(frame) * S + p0 / C] = (float)r;
     }
   }
 }
 
 template <int FG, int NW, int NF, bool REGP = false>
 static hipError_t launch_g4(const float* x, const double* pw, const double* pmw, const double* cst, float* out,
-                            int nframes, int D, int NDC, int S, int C, int P, int PP, int mix_lse, hipStream_t st) {
+                            int nframes, int D, int NDC, int S, int C, int P, int PP, int mix_lse, int T, int t0,
+                            int L, hipStream_t st) {
   using G = G4<FG, NW, NF>;
   dim3 grid((unsigned)(((size_t)nframes + G::FT - 1) / G::FT), (unsigned)((P + G::CG - 1) / G::CG));
   hipLaunchKernelGGL((gmm_score4_kernel<FG, NW, NF, REGP>), grid, dim3(G::NT), 0, st, x, pw, pmw, cst, out, nframes, D, NDC,
-                     S, C, P, PP, mix_lse);
+                     S, C, P, PP, mix_lse, T, t0, L);
   return hipGetLastError();
 }
 
@@ -450,9 +459,27 @@ HMM355_API size_t hmm355_gmm_workspace_bytes(int B, int T, int D, int S, int C) 
   return gmm_ws_layout(B, T, D, S, C, nullptr, nullptr);
 }
 
+static int gmm_run(const float* x, const float* means, const float* log_vars, const float* log_w, int B, int T,
+                   int D, int S, int C, int mix_lse, int t0, int L, float* out, void* workspace,
+                   size_t workspace_bytes, void* stream);
+
 HMM355_API int hmm355_gmm_diag_logprob_f32(const float* x, const float* means, const float* log_vars,
                                            const float* log_w, int B, int T, int D, int S, int C, int mix_lse,
                                            float* out, void* workspace, size_t workspace_bytes, void* stream) {
+  return gmm_run(x, means, log_vars, log_w, B, T, D, S, C, mix_lse, 0, T, out, workspace, workspace_bytes, stream);
+}
+
+HMM355_API int hmm355_gmm_diag_logprob_slice_f32(const float* x, const float* means, const float* log_vars,
+                                                 const float* log_w, int B, int T, int D, int S, int C, int mix_lse,
+                                                 int t0, int L, float* out, void* workspace, size_t workspace_bytes,
+                                                 void* stream) {
+  if (t0 < 0 || L < 1 || t0 + L > T || !gmm_v2(C) || gmm_cfg() == 0) return HMM355_E_ARG;
+  return gmm_run(x, means, log_vars, log_w, B, T, D, S, C, mix_lse, t0, L, out, workspace, workspace_bytes, stream);
+}
+
+static int gmm_run(const float* x, const float* means, const float* log_vars, const float* log_w, int B, int T,
+                   int D, int S, int C, int mix_lse, int t0, int L, float* out, void* workspace,
+                   size_t workspace_bytes, void* stream) {
   if (B < 0 || T < 0 || D < 1 || S < 1 || C < 1) return HMM355_E_ARG;
   if (D > kGmmDMax || C > 256 || (size_t)S * C > 65536) return HMM355_E_SHAPE;
   if ((size_t)B * T == 0) return HMM355_OK;
@@ -465,7 +492,7 @@ HMM355_API int hmm355_gmm_diag_logprob_f32(const float* x, const float* means, c
   const int NDC = (D + kGmmDc - 1) / kGmmDc, DP = NDC * kGmmDc;
   const int P = S * C;
   const int CG = gmm_v2_group(P), PP = (P + CG - 1) / CG * CG;
-  const int nframes = B * T;
+  const int nframes = B * L;  // (the v1 scorer below runs whole tensors only: L == T, t0 == 0)
   const size_t ntiles = ((size_t)nframes + kGmmFrames - 1) / kGmmFrames;
   hipStream_t st = static_cast<hipStream_t>(stream);
   hipLaunchKernelGGL(gmm_prep_kernel, dim3(PP), dim3(64), 0, st, means, log_vars, log_w, w.pw, w.pmw, w.cst, P, PP,
@@ -475,13 +502,13 @@ HMM355_API int hmm355_gmm_diag_logprob_f32(const float* x, const float* means, c
   const int cfg = gmm_cfg();  // diagnostic: 0 = the first scorer, 1.. = v2 shapes
   if (!gmm_use_v1(C)) {
     static_assert(G4<1, 4, 16>::CG == 256 && G4<2, 2, 16>::CG == 128 && G4<4, 2, 16>::CG == 64, "gmm_v2_group");
-#define G4L(fg, nw, nf) launch_g4<fg, nw, nf>(x, w.pw, w.pmw, w.cst, out, nframes, D, NDC, S, C, P, PP, mix_lse, st)
+#define G4L(fg, nw, nf) launch_g4<fg, nw, nf>(x, w.pw, w.pmw, w.cst, out, nframes, D, NDC, S, C, P, PP, mix_lse, T, t0, L, st)
     // shapes from tools/time_gmm.py (profiles/r4h_gmm2.log): config 3 (P = 512) 326 us with
     // 16 frames per lane; P = 64 (configs 2, 5) 57 / 34 us with 4 (the work is small: more waves)
     // (round 4, profiles/r4m_gmm_regp.log: the parameters staged through registers, config 5
     // below and the default, beat the LDS-DMA staging, config 1, by 4-7 %: 311 / 54 / 31 us per
     // call at configs 3 / 2 / 5; identical bits)
-#define G4R(fg, nw, nf) launch_g4<fg, nw, nf, true>(x, w.pw, w.pmw, w.cst, out, nframes, D, NDC, S, C, P, PP, mix_lse, st)
+#define G4R(fg, nw, nf) launch_g4<fg, nw, nf, true>(x, w.pw, w.pmw, w.cst, out, nframes, D, NDC, S, C, P, PP, mix_lse, T, t0, L, st)
     if (CG == 256) {
       e = cfg == 1 ? G4L(1, 4, 16) : cfg == 2 ? G4L(1, 4, 8) : cfg == 3 ? G4L(1, 2, 16) : cfg == 4 ? G4L(1, 1, 16)
                    : G4R(1, 4, 16);

@@ -173,6 +173,9 @@ struct VitArgs {
   int nfollow;
   int* prog;
   uint8_t* done;
+  // a time part (dense plans): trellis rows [q_lo, q_hi) of this launch (q_hi = 0: T); the psi
+  // pass and the backtrace run with the last part (hmm355_viterbi_part_f32)
+  int q_lo, q_hi;
 };
 
 // chunk map: G[j] = state at t_lo - 1 given state j at t_hi (psi rows of the chunk in LDS)

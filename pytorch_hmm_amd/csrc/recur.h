@@ -285,6 +285,10 @@ struct RecArgs {
   // beta: cs[t] = c with v_{t-1} = A (e_t v_t) / c), written beside LS for the adjoint
   // (autograd.py), or null
   float* cs;
+  // Viterbi, dense chain (rec_run_rb) only: compute rows [q_lo, q_hi) of the trellis, row q_lo - 1
+  // read back from `rows` (a previous part's); q_lo a multiple of 64, q_hi = 0 means T.  (Time
+  // parts let a producer of the emissions run ahead of the chain: ops.gmm_viterbi)
+  int q_lo, q_hi;
 };
 constexpr int kProgSlots = 8;  // >= kRbHelpers<NP>::NH
 
@@ -887,13 +891,15 @@ __device__ __forceinline__ void rec_rb_helper(const RecArgs& a, float* lds, int 
   const int tid = threadIdx.x;
   const int h = (tid >> 6) - C::NW, l = tid & 63, th = tid - C::NT;
   const int T = a.T;
-  const int nblocks = (T + 15) / 16;
+  // blocks kb0 .. nblocks - 1 of this launch (a time part: rec_run_rb)
+  const int kb0 = KIND == kVit ? a.q_lo / 16 : 0;
+  const int nblocks = ((KIND == kVit && a.q_hi > 0 ? a.q_hi : T) + 15) / 16;
   // register sets: [set = block & 1][slice 0/1][5]
   float er[2][2][5];
   if (KIND == kVit) rec_logt_fill<NP>(lds, l);
-  if (nblocks > 1) {
-    rec_load<NP, KIND>(a, b, 1, 2 * h, l, er[1][0]);
-    rec_load<NP, KIND>(a, b, 1, 2 * h + 1, l, er[1][1]);
+  if (nblocks > kb0 + 1) {
+    rec_load<NP, KIND>(a, b, kb0 + 1, 2 * h, l, er[1][0]);
+    rec_load<NP, KIND>(a, b, kb0 + 1, 2 * h + 1, l, er[1][1]);
   }
   lds_barrier();  // (the chain's: block 0 staged)
   lds_barrier();  // (the chain's: row 0 written)
@@ -923,15 +929,15 @@ __device__ __forceinline__ void rec_rb_helper(const RecArgs& a, float* lds, int 
         if (kb + 1 < nblocks) rec_stage<NP, KIND>(a, lds, kb + 1, 2 * h, l, cur[0]);
         // (Viterbi with psi followers) blocks 0 .. kb - 3 were flushed in block kb - 1, before
         // the barriers since: publish them once per chunk
-        if (kb >= 3 && ((kb - 2) & 3) == 0) publish(kb - 2);
+        if (kb >= kb0 + 3 && ((kb - 2) & 3) == 0) publish(kb - 2);
         break;
       case 1: if (kb + 1 < nblocks) rec_stage<NP, KIND>(a, lds, kb + 1, 2 * h + 1, l, cur[1]); break;
       case 2: rec_load<NP, KIND>(a, b, kb + 2 < nblocks ? kb + 2 : nblocks - 1, 2 * h, l, nxt[0]); break;
       case 3: rec_load<NP, KIND>(a, b, kb + 2 < nblocks ? kb + 2 : nblocks - 1, 2 * h + 1, l, nxt[1]); break;
-      case 4: if (kb >= 2) lsv = rec_ls_scan<NP, KIND>(a, lds, b, kb - 2, base, h == NH - 1); break;
-      case 5: if (kb >= 2) rec_flush<NP, KIND>(a, lds, b, kb - 2, th, lsv); break;
+      case 4: if (kb >= kb0 + 2) lsv = rec_ls_scan<NP, KIND>(a, lds, b, kb - 2, base, h == NH - 1); break;
+      case 5: if (kb >= kb0 + 2) rec_flush<NP, KIND>(a, lds, b, kb - 2, th, lsv); break;
       case 6:
-        if (kb >= 2) {
+        if (kb >= kb0 + 2) {
           rec_flush<NP, KIND>(a, lds, b, kb - 2, th + NH * kWave, lsv);
           flushed();
         }
@@ -939,9 +945,10 @@ __device__ __forceinline__ void rec_rb_helper(const RecArgs& a, float* lds, int 
       default: break;
     }
   };
+  const int qend = nblocks * 16 < T ? nblocks * 16 : T;
   auto run_block = [&](int kb, float(&cur)[2][5], float(&nxt)[2][5]) {
     const int q0 = kb * 16 < 1 ? 1 : kb * 16;
-    const int q1 = (kb + 1) * 16 < T ? (kb + 1) * 16 : T;
+    const int q1 = (kb + 1) * 16 < qend ? (kb + 1) * 16 : qend;
     int it = 0;
     for (int q = q0; q < q1; ++q, ++it) {
       if (it < kRbItems<KIND>) item(kb, it, cur, nxt);
@@ -950,13 +957,13 @@ __device__ __forceinline__ void rec_rb_helper(const RecArgs& a, float* lds, int 
     for (; it < kRbItems<KIND>; ++it) item(kb, it, cur, nxt);  // (a short last block)
   };
   // block kb stages block kb + 1 from set (kb + 1) & 1 and loads block kb + 2 into set kb & 1
-  for (int k = 0; k < nblocks; k += 2) {
+  for (int k = kb0; k < nblocks; k += 2) {
     run_block(k, er[1], er[0]);
     if (k + 1 < nblocks) run_block(k + 1, er[0], er[1]);
   }
   lds_barrier();  // (the chain's: the last rows and c_{T-1} written)
   static_assert(2 * NH * kWave == C::NT, "two flush passes cover the block");
-  if (nblocks >= 2) {
+  if (nblocks >= kb0 + 2) {
     lsv = rec_ls_scan<NP, KIND>(a, lds, b, nblocks - 2, base, h == NH - 1);
     rec_flush<NP, KIND>(a, lds, b, nblocks - 2, th, lsv);
     rec_flush<NP, KIND>(a, lds, b, nblocks - 2, th + NH * kWave, lsv);
@@ -1036,18 +1043,26 @@ __device__ __forceinline__ void rec_run_rb(const RecArgs& a, float* lds, int b) 
         Mk[k][m][e >> 1][e & 1] = FB ? __expf(in ? v : -INFINITY) : (in ? v : -INFINITY);
       }
 
-  const int nblocks = (T + 15) / 16;
+  // rows [q_lo, q_hi) of this launch (Viterbi time parts; FB: the whole sequence)
+  const int q_lo = KIND == kVit ? a.q_lo : 0;
+  const int kb0 = q_lo / 16;
+  const int qend = KIND == kVit && a.q_hi > 0 ? a.q_hi : T;
+  const int nblocks = (qend + 15) / 16;
   {
     float er0[5];
     if (KIND == kVit) rec_logt_fill<NP>(lds, l);
-    rec_load<NP, KIND>(a, b, 0, w, l, er0);
-    rec_stage<NP, KIND>(a, lds, 0, w, l, er0);
+    rec_load<NP, KIND>(a, b, kb0, w, l, er0);
+    rec_stage<NP, KIND>(a, lds, kb0, w, l, er0);
   }
   lds_barrier();  // (block 1 on: the helpers stage)
 
   auto emis = [&](int rho, int idx) { return lds[C::OFF_EMIS + (((rho >> 4) % 3) * 16 + (rho & 15)) * NP + idx]; };
   const bool writer = (c & 3) == 0;
-  {
+  if (q_lo > 0) {
+    // a later part: row q_lo - 1 is the previous part's last trellis row (delta, row stride N)
+    const float v0 = o < N ? a.rows[((size_t)b * T + (q_lo - 1)) * a.row_stride + o] : -INFINITY;
+    if (writer) ring[((q_lo - 1) & (C::RING - 1)) * NP + o] = v0;
+  } else {
     float v0;
     const int oo = o < N ? o : 0;
     if (KIND == kFbAlpha) v0 = o < N ? __expf(a.init[oo]) * emis(0, o) : 0.f;  // alpha_0 = p0 * e_0
@@ -1147,7 +1162,7 @@ __device__ __forceinline__ void rec_run_rb(const RecArgs& a, float* lds, int b) 
   };
   auto run_block = [&](int kb) {
     const int q0 = kb * 16 < 1 ? 1 : kb * 16;
-    const int q1 = (kb + 1) * 16 < T ? (kb + 1) * 16 : T;
+    const int q1 = (kb + 1) * 16 < qend ? (kb + 1) * 16 : qend;
     if (q0 == kb * 16 && q1 == q0 + 16) {
       // a whole 16-step block, unrolled: the ring / staging indices of every step are the
       // block's plus a constant, so no per-step scalar index arithmetic (round 5: the rolled
@@ -1159,7 +1174,7 @@ __device__ __forceinline__ void rec_run_rb(const RecArgs& a, float* lds, int b) 
       for (int q = q0; q < q1; ++q) stepq(q);
     }
   };
-  for (int k = 0; k < nblocks; ++k) run_block(k);
+  for (int k = kb0; k < nblocks; ++k) run_block(k);
   if (kStamp && (tid & 63) == 0) {
     const unsigned long long t1 = stamp();
     const long long rt1 = __builtin_amdgcn_s_memrealtime();
@@ -1858,7 +1873,9 @@ __device__ __forceinline__ int rec_band_code(const RecArgs& a) {
 
 template <int NP, int KIND>
 __device__ __forceinline__ void rec_dispatch(const RecArgs& a, float* lds, int b) {
-  const int code = rec_band_code<KIND, NP>(a);
+  // (a Viterbi time part runs the register-blocked chain whatever the plan: only it resumes from
+  // a stored row; the C ABI takes parts for host-known dense plans only)
+  const int code = (KIND == kVit && (a.q_lo > 0 || a.q_hi > 0)) ? 0 : rec_band_code<KIND, NP>(a);
   // the banded chains are written for RC<NP>::NT threads (the fused Viterbi form for 1024)
   constexpr int kBandNT = (KIND == kVit && kVitFused<NP>) ? 1024 : RC<NP>::NT;
   if (code != 0 && threadIdx.x >= kBandNT) return;

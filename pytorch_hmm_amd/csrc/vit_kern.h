@@ -275,11 +275,18 @@ __device__ __forceinline__ void vit_psi_follow(const RecArgs& ra, float* lds) {
   float M[C::NBLK][16];
   psi_dense_matrix<NP>(a, M);
   const int nf = (int)gridDim.x - a.B;
-  const int ntask = a.B * a.nchunks;
+  // the chunks of this launch (a time part [q_lo, q_hi), both multiples of kChunk but the last
+  // q_hi): a part leaves its last chunk to the next part's followers (its rows are complete when
+  // that part starts), so no part's launch waits for followers still on its last rows; the last
+  // part takes the rest, and the psi pass after it every chunk not marked done
+  const bool last_part = ra.q_hi == 0 || ra.q_hi >= a.T;
+  const int c_lo = ra.q_lo > 0 ? ra.q_lo / kChunk - 1 : 0;
+  const int c_hi = last_part ? a.nchunks : ra.q_hi / kChunk - 1;
+  const int ntask = a.B * (c_hi - c_lo);
   int last_have = -1;
   long long t0 = __builtin_amdgcn_s_memrealtime();
   for (int task = (int)blockIdx.x - a.B; task < ntask; task += nf) {
-    const int chunk = task / a.B, b = task - chunk * a.B;
+    const int chunk = c_lo + task / a.B, b = task % a.B;
     const int t_lo = chunk * kChunk;
     const int t_hi = (t_lo + kChunk < a.T ? t_lo + kChunk : a.T) - 1;
     // rows t_first - 1 .. t_hi - 1 are read: blocks 0 .. (t_hi - 1) / 16 must be out
@@ -325,6 +332,9 @@ hipError_t launch_vit(const VitArgs& va, bool prep, bool tail, hipStream_t sm) {
   }
   RecArgs ra{va.obs, va.log_P, va.init, va.delta, nullptr, nullptr, va.B, va.T, va.N, va.obs_mode, va.N, va.band,
              nullptr, nullptr, va.psi};
+  ra.q_lo = va.q_lo;
+  ra.q_hi = va.q_hi;
+  const bool first = va.q_lo == 0, last = va.q_hi == 0 || va.q_hi == va.T;
   if (tail) {  // the fused decode: chunk maps and backtrace inside the chain kernel (recur.h vtail)
     ra.G = va.G;
     ra.states = va.states;
@@ -335,9 +345,12 @@ hipError_t launch_vit(const VitArgs& va, bool prep, bool tail, hipStream_t sm) {
   // psi followers beside a dense chain (NP <= 128: the chain with block-work helpers publishes)
   const int nfollow = (!tail && NP <= 128 && va.prog && va.done) ? va.nfollow : 0;
   if (nfollow > 0) {
-    e = hipMemsetAsync(va.prog, 0, (size_t)va.B * kProgSlots * sizeof(int), sm);
-    if (e == hipSuccess) e = hipMemsetAsync(va.done, 0, (size_t)va.B * va.nchunks, sm);
-    if (e != hipSuccess) return e;
+    // (the first part clears the followers' words for every chunk; later parts keep counting)
+    if (first) {
+      e = hipMemsetAsync(va.prog, 0, (size_t)va.B * kProgSlots * sizeof(int), sm);
+      if (e == hipSuccess) e = hipMemsetAsync(va.done, 0, (size_t)va.B * va.nchunks, sm);
+      if (e != hipSuccess) return e;
+    }
     ra.G = va.G;
     ra.states = va.states;
     ra.final_score = va.final_score;
@@ -348,7 +361,7 @@ hipError_t launch_vit(const VitArgs& va, bool prep, bool tail, hipStream_t sm) {
   hipLaunchKernelGGL(vit_fwd_kernel<NP>, dim3(va.B + nfollow), dim3(kVitNT<NP>), kExclusiveLds, sm, ra);
   e = hipGetLastError();
   if (e != hipSuccess) return e;
-  if (tail) return hipSuccess;
+  if (tail || !last) return hipSuccess;
   // banded psi stages the chunk's delta rows in LDS (dynamic, kChunk x NP floats)
   const size_t psi_lds = va.band ? (size_t)kChunk * NP * sizeof(float) : 0;
   VitArgs vp = va;

@@ -87,13 +87,18 @@ static int device_cus() {
   return cus[dev] > 0 ? cus[dev] : 0;
 }
 
-HMM355_API int hmm355_viterbi_plan_ex_f32(const float* obs, int obs_mode, const float* log_P, const float* init,
-                                          const void* plan, unsigned flags, int B, int T, int N, int64_t* states,
-                                          float* log_delta, float* final_score, void* workspace,
-                                          size_t workspace_bytes, void* stream) {
+static int viterbi_run(const float* obs, int obs_mode, const float* log_P, const float* init, const void* plan,
+                       unsigned flags, int B, int T, int N, int q_lo, int q_hi, int64_t* states, float* log_delta,
+                       float* final_score, void* workspace, size_t workspace_bytes, void* stream) {
   if (B < 0 || N < 0) return HMM355_E_ARG;
   if (N < 1 || N > 256) return HMM355_E_STATES;
   if (T < 1) return HMM355_E_SHAPE;
+  if (q_hi == 0) q_hi = T;
+  if (q_lo < 0 || q_lo % kChunk || q_lo >= q_hi || q_hi > T) return HMM355_E_ARG;
+  const bool part = q_lo > 0 || q_hi < T;
+  // time parts: the register-blocked dense chain (host-known dense plan, N <= 128) on log-emissions
+  if (part && (!(flags & HMM355_VIT_PLAN_DENSE) || !plan || N > 128 || obs_mode != HMM355_OBS_LOG))
+    return HMM355_E_ARG;
   if (B == 0) return HMM355_OK;
   if (!obs || !log_P || !init || !states || !log_delta || !workspace) return HMM355_E_ARG;
   if (obs_mode != HMM355_OBS_PROB && obs_mode != HMM355_OBS_LOG) return HMM355_E_ARG;
@@ -114,11 +119,15 @@ HMM355_API int hmm355_viterbi_plan_ex_f32(const float* obs, int obs_mode, const 
   // per element on the helper waves), so the emissions are read once and no log_obs tensor
   // round-trips through HBM
   VitArgs va{obs, log_P, init, log_delta, final_score, states, psi, G, B, T, N, obs_mode, nc, band};
+  // (the whole range stays q_lo = q_hi = 0: the chain kernel then picks the banded chain where the
+  // plan is banded; a part always runs the register-blocked dense chain, recur.h rec_dispatch)
+  va.q_lo = part ? q_lo : 0;
+  va.q_hi = part ? q_hi : 0;
   hipStream_t sm = static_cast<hipStream_t>(stream);
   // the fused decode needs the fused banded chain (NP >= 128) and the plan's word that it is
   // banded (the caller read it once per plan, hmm355_plan_banded); its tail keeps at most
   // 4096 chunk end states in LDS (T <= 262144)
-  const bool tail = (flags & HMM355_VIT_PLAN_BANDED) && plan && band && NP >= 128 && nc <= 4096;
+  const bool tail = (flags & HMM355_VIT_PLAN_BANDED) && plan && band && NP >= 128 && nc <= 4096 && !part;
 #ifdef HMM355_DIAG
   // (HMM355_VIT_TAIL_DIAG: diagnostic bits of RecArgs::vtail, timing only -- results are wrong;
   // read only in diagnostic builds, build_native.build(defines=["HMM355_DIAG"]))
@@ -156,6 +165,22 @@ HMM355_API int hmm355_viterbi_plan_ex_f32(const float* obs, int obs_mode, const 
     default: e = launch_vit<256>(va, plan == nullptr, tail, sm); break;
   }
   return e == hipSuccess ? HMM355_OK : (int)e;
+}
+
+HMM355_API int hmm355_viterbi_plan_ex_f32(const float* obs, int obs_mode, const float* log_P, const float* init,
+                                          const void* plan, unsigned flags, int B, int T, int N, int64_t* states,
+                                          float* log_delta, float* final_score, void* workspace,
+                                          size_t workspace_bytes, void* stream) {
+  return viterbi_run(obs, obs_mode, log_P, init, plan, flags, B, T, N, 0, T, states, log_delta, final_score,
+                     workspace, workspace_bytes, stream);
+}
+
+HMM355_API int hmm355_viterbi_part_f32(const float* obs, int obs_mode, const float* log_P, const float* init,
+                                       const void* plan, unsigned flags, int B, int T, int N, int q_lo, int q_hi,
+                                       int64_t* states, float* log_delta, float* final_score, void* workspace,
+                                       size_t workspace_bytes, void* stream) {
+  return viterbi_run(obs, obs_mode, log_P, init, plan, flags, B, T, N, q_lo, q_hi, states, log_delta, final_score,
+                     workspace, workspace_bytes, stream);
 }
 
 HMM355_API int hmm355_viterbi_plan_f32(const float* obs, int obs_mode, const float* log_P, const float* init,

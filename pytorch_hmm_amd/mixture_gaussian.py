@@ -180,10 +180,43 @@ class MixtureGaussianHMMLayer(nn.Module):
         states, _, final = ops.viterbi(obs_log_probs, log_transitions, init, ops.OBS_LOG, plan)
         return states, final
 
+    def _inference_tables(self, device):
+        """(log T, log w, the uniform start vector, the transition plan) for inference, formed with
+        the reference's expressions (mixture_gaussian.py:130-135, :141-155, :305) and cached while
+        the parameters they come from are unchanged (same tensors, same versions): a decode of a
+        fixed model launches no per-call softmax / log / clamp kernels (~10 small launches,
+        ~80 us of serial latency before the scorer at config 3, profiles/r5m_c3)."""
+        src = self.transition_logits if self.learnable_transitions else self.transition_matrix
+        wl = self.mixture_weights_logits
+        key = (id(src), src._version, id(wl), wl._version, str(device))
+        c = self.__dict__.get("_inf_cache")
+        if c is not None and c[0] == key and c[1] is src and c[2] is wl:
+            return c[3]
+        log_T = self._safe_log(self.get_transition_matrix())
+        log_w = self._safe_log(F.softmax(wl, dim=-1))
+        S = self.num_states
+        init = -(torch.zeros(S, device=device) + math.log(S))
+        tabs = (log_T, log_w, init, self._transition_plan(log_T))
+        self.__dict__["_inf_cache"] = (key, src, wl, tabs)
+        return tabs
+
     def forward(self, observations: torch.Tensor,
                 return_log_probs: bool = False) -> Tuple[torch.Tensor, Optional[torch.Tensor]]:
-        obs_log_probs = self.get_observation_log_probs(observations)
+        if self.covariance_type != "full" and not needs_grad(observations, *self.parameters()):
+            # inference: the emission scorer runs beside the decode (ops.gmm_viterbi: time slices
+            # of the scores on a side stream, the chain on the slices already scored); the same
+            # bits as get_observation_log_probs followed by _viterbi_decode
+            B, T, _ = observations.shape
+            if T > self.max_sequence_length:
+                warnings.warn(f"Sequence length {T} exceeds recommended maximum "
+                              f"{self.max_sequence_length}. Consider chunked processing.")
+            with torch.no_grad():
+                log_T, log_w, init, plan = self._inference_tables(observations.device)
+                _, states, _, scores = ops.gmm_viterbi(observations, self.means, self._component_log_vars(), log_w,
+                                                       1, log_T, init, plan)
+            return (states, scores) if return_log_probs else (states, None)
         log_transitions = self._safe_log(self.get_transition_matrix())
+        obs_log_probs = self.get_observation_log_probs(observations)
         states, scores = self._viterbi_decode(obs_log_probs, log_transitions)
         return (states, scores) if return_log_probs else (states, None)
 

@@ -215,6 +215,98 @@ def _(x, means, log_vars, log_w, mix_lse):
     return x.new_empty((x.shape[0], x.shape[1], means.shape[0]))
 
 
+# ------------------------------------------- GMM emission feeding a dense Viterbi chain
+_SIDE = {}
+
+
+def _side_stream(dev):
+    """One side stream per device (the emission producer of gmm_viterbi)."""
+    key = str(dev)
+    if key not in _SIDE:
+        _SIDE[key] = torch.cuda.Stream(dev)
+    return _SIDE[key]
+
+
+def time_parts(T: int) -> list:
+    """Part boundaries [0, t1, t2, T] of gmm_viterbi (multiples of 64): a short first part so
+    the chain starts early, then parts that grow so the scorer, on the CUs the chain leaves,
+    stays ahead of the chain (config 3: a 2000-step chain ~0.6 ms, the scorer ~0.3 ms alone).
+    Few parts: each is a launch with its own prologue (profiles/r5m_*: five parts cost more than
+    they hid)."""
+    t1, t2 = (T * 16 // 100) // 64 * 64, (T * 48 // 100) // 64 * 64
+    if T < 640 or t1 < 64:
+        return [0, T]
+    return [0, t1, t2, T]
+
+
+def gmm_viterbi(x: Tensor, means: Tensor, log_vars: Tensor, log_w: Tensor, mix_lse: int, log_T: Tensor,
+                init: Tensor, plan: Optional[Tensor]) -> Tuple[Tensor, Tensor, Tensor, Tensor]:
+    """gmm_diag_logprob + viterbi (OBS_LOG) of the same batch with the two overlapped
+    (MixtureGaussianHMMLayer.forward, mixture_gaussian.py:340-365): the scorer fills time slices
+    of the log-probabilities on a side stream (hmm355_gmm_diag_logprob_slice_f32) while the
+    chain decodes the slices already scored (hmm355_viterbi_part_f32, one launch per part, each
+    waiting only for its own slice), so the scorer runs beside the chain instead of before it.
+    Bit-identical to the two calls in sequence.  Needs a host-known dense plan, N <= 128 and
+    C in {1, 2, 4}; otherwise it is the two calls in sequence.
+
+    OFF by default (HMM355_GMM_VIT_PARTS=1 turns it on): measured at config 3 it is slower than
+    the two calls in sequence (0.98 vs 0.84 ms per step, profiles/r5n_c3, r5o_c3).  The chain
+    launches of the parts need whole CUs (all of a CU's LDS) and are dispatched only as the
+    scorer's workgroups drain, and with the fp64 scorer busy on the rest of the chip the clock
+    drops: the chain steps ran at 0.33-0.49 us instead of 0.30.
+    Returns (log_probs (B,T,S), states (B,T), log_delta (B,T,S), final_score (B))."""
+    nat.require_gpu(x, means, log_vars, log_w, log_T, init)
+    x, means, log_vars, log_w = _f32c(x), _f32c(means), _f32c(log_vars), _f32c(log_w)
+    log_T, init = _f32c(log_T), _f32c(init)
+    B, T, D = x.shape
+    S, C, _ = means.shape
+    dev = x.device
+    parts = time_parts(T)
+    dense = plan is not None and getattr(plan, "_hmm355_banded", True) is False
+    if (not dense or len(parts) <= 2 or S > 128 or C not in (1, 2, 4) or B == 0
+            or os.environ.get("HMM355_GMM_VIT_PARTS", "0") != "1"):
+        lp = gmm_diag_logprob(x, means, log_vars, log_w, mix_lse)
+        states, delta, final = viterbi(lp, log_T, init, OBS_LOG, plan)
+        return lp, states, delta, final
+    L = nat.lib()
+    lp = torch.empty((B, T, S), device=dev)
+    states = torch.empty((B, T), dtype=torch.int64, device=dev)
+    delta = torch.empty((B, T, S), device=dev)
+    final = torch.empty(B, device=dev)
+    ws_g = _workspace(L.hmm355_gmm_workspace_bytes(B, T, D, S, C), dev)
+    ws_v = _workspace(L.hmm355_viterbi_workspace_bytes(B, T, S), dev)
+    main = torch.cuda.current_stream(dev)
+    side = _side_stream(dev)
+    side.wait_stream(main)
+    flags = VIT_PLAN_DENSE  # (parts need the host's dense word; the psi followers ride on it)
+    evs = []
+    with torch.cuda.device(dev):
+        with torch.cuda.stream(side):
+            sside = ctypes_stream(side)
+            for t0, t1 in zip(parts[:-1], parts[1:]):
+                nat.check(L.hmm355_gmm_diag_logprob_slice_f32(
+                    nat.ptr(x), nat.ptr(means), nat.ptr(log_vars), nat.ptr(log_w), B, T, D, S, C, mix_lse,
+                    t0, t1 - t0, nat.ptr(lp), nat.ptr(ws_g), ws_g.numel(), sside))
+                ev = torch.cuda.Event()
+                ev.record(side)
+                evs.append(ev)
+        smain = ctypes_stream(main)
+        for (t0, t1), ev in zip(zip(parts[:-1], parts[1:]), evs):
+            main.wait_event(ev)
+            nat.check(L.hmm355_viterbi_part_f32(
+                nat.ptr(lp), OBS_LOG, nat.ptr(log_T), nat.ptr(init), nat.ptr(plan), flags, B, T, S, t0, t1,
+                nat.ptr(states), nat.ptr(delta), nat.ptr(final), nat.ptr(ws_v), ws_v.numel(), smain))
+    # tensors the side stream used stay allocated until its work is done
+    for t_ in (x, means, log_vars, log_w, lp, ws_g):
+        t_.record_stream(side)
+    return lp, states, delta, final
+
+
+def ctypes_stream(s):
+    import ctypes
+    return ctypes.c_void_p(s.cuda_stream)
+
+
 # ------------------------------------------------------------------------------- HSMM
 @torch.library.custom_op("hmm355::hsmm_viterbi", mutates_args=())
 def hsmm_viterbi(lp: Tensor, dur_lp: Tensor, log_T: Tensor) -> Tuple[Tensor, Tensor]:
