@@ -610,13 +610,13 @@ __device__ void hs_walk(const HsWalk& w, int l, int t, int cs, int cd, float o, 
 #pragma unroll
       for (int k = 0; k < K; ++k)
         if (l + 64 * k + 1 < nd && dv[k] != -INFINITY) xb = fmaxf(xb, dv[k] + lt);
-      xb = wave_max(xb);
+      xb = wave_max_dpp2(xb);  // (DPP + permlane: no ds_bpermute round trips on the walk)
       // the next segment's obs_sum is candidate nd's
       {
         float ok = ov[0];
 #pragma unroll
         for (int k = 1; k < K; ++k) ok = (nd - 1) >> 6 == k ? ov[k] : ok;
-        on = __shfl(ok, (nd - 1) & 63);
+        on = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, ok), (nd - 1) & 63));
       }
       const float u = sdur[cs * Dm + cd - 1];
       const float F = (M + o) + u;
@@ -752,7 +752,7 @@ __global__ void __launch_bounds__(64) hsmm_chunk_walk_kernel(HsArgs a, HsChunks 
       const int sp = l + 64 * k;
       if (sp < S) argmax_combine(bv, bi, w.Db[(size_t)t0 * S + sp], sp);
     }
-    wave_argmax(bv, bi);
+    wave_argmax_dpp(bv, bi);
     cs = bi < S ? bi : 0;
     cd = 1;
   }
@@ -788,8 +788,18 @@ __global__ void __launch_bounds__(64) hsmm_stitch_kernel(HsArgs a, HsChunks c) {
   const int4* recb = c.rec + (size_t)b * c.C * kHsCap;
   const int* cntb = c.cnt + (size_t)b * c.C;
   const int c0 = c.C - c.stage;  // staged: chunks c0 .. C-1
-  // independent loads (entries past a record's count are read but never used): one round trip
-  for (int ch = c0; ch < c.C; ++ch) srec[(ch - c0) * 64 + l] = recb[(size_t)ch * kHsCap + l];
+  // independent loads (entries past a record's count are read but never used), 16 chunks' entries
+  // in flight at a time: a plain loop waits for each load before its LDS store, one round trip per
+  // chunk (round 4: 32 serial round trips at config 5, most of the stitch's 68 us)
+  for (int ch0 = c0; ch0 < c.C; ch0 += 16) {
+    int4 v[16];
+#pragma unroll
+    for (int k = 0; k < 16; ++k)
+      v[k] = ch0 + k < c.C ? recb[(size_t)(ch0 + k) * kHsCap + l] : make_int4(0, 0, 0, 0);
+#pragma unroll
+    for (int k = 0; k < 16; ++k)
+      if (ch0 + k < c.C) srec[(ch0 + k - c0) * 64 + l] = v[k];
+  }
   for (int k = l; k < c.stage; k += 64) scnt[k] = cntb[c0 + k];
   int t = T - 1, cs = a.fin[2 * b], cd = a.fin[2 * b + 1];
   float o = hs_obs_sum_wave(w.lp, a.S, T - cd, cd, cs, w.pcol, l);
