@@ -479,18 +479,20 @@ __host__ __device__ inline size_t hsmm_walk_lds(int S, int Dm, int R) {
 
 // global -> LDS copy by one wave, 16 loads per lane in flight (a plain strided loop waits
 // for each load before the next: one round trip per 64 values)
+// (indices past n are clamped to n - 1, which rewrites that entry with its own value: no
+// branch per load or store)
 __device__ __forceinline__ void hs_copy_lds(float* dst, const float* src, int n, int l) {
   for (int i0 = 0; i0 < n; i0 += 64 * 16) {
     float v[16];
 #pragma unroll
     for (int k = 0; k < 16; ++k) {
       const int i = i0 + 64 * k + l;
-      v[k] = i < n ? src[i] : 0.f;
+      v[k] = src[i < n ? i : n - 1];
     }
 #pragma unroll
     for (int k = 0; k < 16; ++k) {
       const int i = i0 + 64 * k + l;
-      if (i < n) dst[i] = v[k];
+      dst[i < n ? i : n - 1] = v[k];
     }
   }
 }
@@ -523,6 +525,25 @@ __device__ __forceinline__ void hs_walk_tables(const HsArgs& a, const HsWalk& w,
   hs_copy_lds(w.slt, a.logT, a.S * a.S, l);
 }
 
+#ifdef HMM355_HSMM_STAMP
+// diagnostic: walker cycles per phase summed over every segment of every chunk walk
+__device__ unsigned long long g_hs_stamp[8];
+// (accumulated in registers, one atomic per phase when the walk returns: an atomic per phase
+// and segment would put its completion on the next load's wait)
+struct HsStampAcc {
+  long long a[7] = {0, 0, 0, 0, 0, 0, 0};
+  bool on;
+  int l;
+  __device__ ~HsStampAcc() {
+    if (on && l == 0)
+      for (int k = 0; k < 7; ++k) atomicAdd(&g_hs_stamp[k], (unsigned long long)a[k]);
+  }
+};
+#define HS_STAMP(k) do { const long long _n = clock64(); st_acc.a[k] += _n - st_t; st_t = _n; } while (0)
+#else
+#define HS_STAMP(k) do { } while (0)
+#endif
+
 // Walks from the segment (end t, state cs, duration cd, obs_sum o) towards t = 0, calling
 // emit(t, cs, cd, o, start) for every segment in walk order (the first one included); stops
 // when emit returns true, or after the first segment that ends below `stop`, starts at 0, or
@@ -540,11 +561,21 @@ __device__ void hs_walk(const HsWalk& w, int l, int t, int cs, int cd, float o, 
   float* pcol = w.pcol;
   float* rcol = w.rcol;
   float* rmc = w.rmc;
+#ifdef HMM355_HSMM_STAMP
+  HsStampAcc st_acc;
+  st_acc.on = stop >= 0;  // chunk walks (and the stitch's own walks)
+  st_acc.l = l;
+  long long st_t = clock64();
+#endif
   while (t >= 0 && cd > 0) {
     int start = t - cd + 1;
     if (start < 0) start = 0;
     if (emit(t, cs, cd, o, start)) return;
     if (start == 0 || t < stop) return;
+    HS_STAMP(0);
+#ifdef HMM355_HSMM_STAMP
+    st_acc.a[6] += 1;
+#endif
     const int tau = start - 1;  // end of the previous segment
     // round trip 1: M and the Dm row at tau
     const float M = Mb[(size_t)tau * S + cs];
@@ -568,6 +599,7 @@ __device__ void hs_walk(const HsWalk& w, int l, int t, int cs, int cd, float o, 
         if (ns < 0 && mask) ns = 64 * k + __ffsll((long long)mask) - 1;
       }
       if (ns < 0) ns = 0;  // unreachable: M is the maximum of these candidates
+      HS_STAMP(1);
       const float lt = slt[ns * S + cs];
       float xo = -INFINITY;  // best total of the states before ns
 #pragma unroll
@@ -586,6 +618,7 @@ __device__ void hs_walk(const HsWalk& w, int l, int t, int cs, int cd, float o, 
         if (pin) pcol[e] = pv;
       }
       __syncthreads();
+      HS_STAMP(2);
       // first d' of ns whose fl(delta + logT) equals M, and the best earlier total (xb)
       float dv[K], ov[K];
       nd = 0;
@@ -606,6 +639,7 @@ __device__ void hs_walk(const HsWalk& w, int l, int t, int cs, int cd, float o, 
         if (nd == 0 && mask) nd = 64 * k + __ffsll((long long)mask);  // lane index + 1 = d'
       }
       if (nd == 0) nd = 1;
+      HS_STAMP(3);
       float xb = xo;
 #pragma unroll
       for (int k = 0; k < K; ++k)
@@ -677,6 +711,7 @@ __device__ void hs_walk(const HsWalk& w, int l, int t, int cs, int cd, float o, 
         on = hs_obs_sum_wave(lp, S, tau - nd + 1, nd, ns, pcol, l);
       }
       __syncthreads();  // the column is restaged for the next segment
+      HS_STAMP(4);
     }
     t = start - 1;
     cs = ns;
@@ -780,6 +815,9 @@ __global__ void __launch_bounds__(64) hsmm_stitch_kernel(HsArgs a, HsChunks c) {
   const int b = blockIdx.x, l = threadIdx.x;
   const int T = a.T;
   // the walker's tables are copied only if the stitch has to walk itself (records usually merge)
+#ifdef HMM355_HSMM_STAMP
+  const long long st0 = clock64();
+#endif
   const HsWalk w = hs_walk_init<R>(a, bsm, b, l, false);
   bool tables = false;
   // after the walker's tables: the first 64 records of the top kHsStage chunks, their counts
@@ -804,6 +842,9 @@ __global__ void __launch_bounds__(64) hsmm_stitch_kernel(HsArgs a, HsChunks c) {
   int t = T - 1, cs = a.fin[2 * b], cd = a.fin[2 * b + 1];
   float o = hs_obs_sum_wave(w.lp, a.S, T - cd, cd, cs, w.pcol, l);
   int64_t* st = a.states + (size_t)b * T;
+#ifdef HMM355_HSMM_STAMP
+  if (l == 0) atomicAdd(&g_hs_stamp[7], (unsigned long long)(clock64() - st0));
+#endif
   // Records come from LDS (staged, n <= 64) or from global memory, never both in one loop:
   // a load that may come from either makes the compiler wait for every outstanding global
   // operation at the join, the state stores included.
@@ -887,6 +928,9 @@ __global__ void __launch_bounds__(64) hsmm_stitch_kernel(HsArgs a, HsChunks c) {
     }
   }
   if (l == 0) c.cnt[(size_t)a.B * c.C + b] = serial;
+#ifdef HMM355_HSMM_STAMP
+  if (l == 0) atomicAdd(&g_hs_stamp[5], (unsigned long long)(clock64() - st0));
+#endif
 }
 
 // Geometries (S <= SMAX, Dmax < R).  The config-5 class S <= 64, Dmax <= 63 takes the
@@ -978,6 +1022,15 @@ inline bool hsmm_wide(int S, int Dm) {
 }  // namespace hmm355
 
 using namespace hmm355;
+
+#ifdef HMM355_HSMM_STAMP
+// diagnostic export: read and clear the walker phase counters (8 values)
+HMM355_API int hmm355_diag_hsmm_stamp(unsigned long long* out) {
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_hs_stamp), 8 * sizeof(unsigned long long)) != hipSuccess) return 1;
+  unsigned long long z[8] = {0};
+  return hipMemcpyToSymbol(HIP_SYMBOL(g_hs_stamp), z, sizeof(z)) == hipSuccess ? 0 : 1;
+}
+#endif
 
 HMM355_API size_t hmm355_hsmm_workspace_bytes(int B, int T, int S, int Dmax) {
   if (B < 0 || T < 1) return 0;

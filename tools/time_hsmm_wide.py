@@ -8,7 +8,8 @@ dev = torch.device("cuda", 0)
 CASES = [(16, 2000, 64, 40, "0"), (16, 2000, 64, 40, "1"), (16, 2000, 200, 50, "0"),
          (16, 2000, 512, 64, "0"), (4, 2000, 64, 400, "0")]
 if os.environ.get("EDGE") == "1":   # the register form's edge (Dmax 71) and the general form above it
-    CASES = [(16, 2000, 64, 71, "0"), (16, 2000, 64, 72, "0"), (16, 2000, 64, 100, "0"), (16, 2000, 64, 127, "0")]
+    CASES = [(16, 2000, 64, 71, "0"), (16, 2000, 64, 72, "0"), (16, 2000, 64, 100, "0"), (16, 2000, 64, 127, "0"),
+             (32, 2000, 64, 71, "0"), (32, 2000, 64, 100, "0")]
 for B, T, S, Dm, force in CASES:
     os.environ["HMM355_HSMM_WIDE"] = force
     g = torch.Generator(device=dev).manual_seed(0)
