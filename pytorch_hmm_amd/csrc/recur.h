@@ -1258,6 +1258,7 @@ __device__ __forceinline__ void band_chain(const RecArgs& a, float* lds, int b, 
   float* ybuf = lds + C::OFF_PART;  // beta's LDS window source [2][NP] (LDS-window mode)
   constexpr int EL = KIND == kFbBeta ? 1 : 0;
   float en[NB];  // the next step's emission (alpha / Viterbi e_q, beta e_{q-1})
+  float gprev = -INFINITY;  // (diagnostic bit 1 << 24)
 
   // the value of state s + dd (s = NB*l + j) from register vector v
   auto at = [&](const float(&v)[NB], int j, int dd) -> float {
@@ -1296,7 +1297,7 @@ __device__ __forceinline__ void band_chain(const RecArgs& a, float* lds, int b, 
 #pragma unroll
       for (int j = 0; j < NB; ++j) { src[j] = y[j] * eo[j]; t = j == 0 ? src[j] : t + src[j]; }
       if (TW == 0) st(ybuf + ((q - 1) & 1) * NP + NB * l, src);
-      cs = wave_sum_bcast(t);
+      cs = (kAbl & (1 << 23)) ? __builtin_bit_cast(float, __builtin_amdgcn_readfirstlane(__builtin_bit_cast(int, t))) : wave_sum_bcast(t);  // (diag 1 << 23: no reduction)
       // the floor term fl_j * c is folded into the end: y_j = fl_j + (window sum) / c, one fma
       // after the reduction instead of a multiply before the window fmas and one after
 #pragma unroll
@@ -1305,7 +1306,7 @@ __device__ __forceinline__ void band_chain(const RecArgs& a, float* lds, int b, 
       float t = 0.f;
 #pragma unroll
       for (int j = 0; j < NB; ++j) { src[j] = y[j]; t = j == 0 ? y[j] : t + y[j]; }
-      cs = wave_sum_bcast(t);
+      cs = (kAbl & (1 << 23)) ? __builtin_bit_cast(float, __builtin_amdgcn_readfirstlane(__builtin_bit_cast(int, t))) : wave_sum_bcast(t);  // (diag 1 << 23: no reduction)
       float sw;
       if constexpr (decltype(UA)::value) {
         sw = 0.f;  // uniform floor: folded into the end as for beta, y = (afl0 + wsum / c) e
@@ -1321,7 +1322,17 @@ __device__ __forceinline__ void band_chain(const RecArgs& a, float* lds, int b, 
       float g = -INFINITY;
 #pragma unroll
       for (int j = 0; j < NB; ++j) { src[j] = y[j]; g = fmaxf(g, y[j] + fl[j]); }
-      const float M = wave_max_bcast(g);
+      // (diagnostic timing bits, wrong results: 1 << 23 no reduction, 1 << 24 the reduction of
+      // the previous step's values, off the step's dependency chain)
+      float M;
+      if constexpr (kAbl & (1 << 23)) {
+        M = __builtin_bit_cast(float, __builtin_amdgcn_readfirstlane(__builtin_bit_cast(int, g)));
+      } else if constexpr (kAbl & (1 << 24)) {
+        M = wave_max_bcast(gprev);
+        gprev = g;
+      } else {
+        M = wave_max_bcast(g);
+      }
       // fused psi: M_q = max_i fl(delta_{q-1,i} + r_i) is also psi row q's floor maximum
       if constexpr (FUSE) wlane(blk, M);
 #pragma unroll

@@ -41,12 +41,13 @@ hipError_t launch_vit(const VitArgs& va, bool prep, bool tail, hipStream_t sm);
 
 using namespace hmm355;
 
-// OBS_PROB emissions of a dense plan: log(x + 1e-8) correctly rounded (logcr.h, the fp32 sum as
-// hmm.py:152 forms it) in one full-chip pass before the chain, which then stages them as
-// OBS_LOG.  The banded chain takes the log in its staging helpers for free (they sit on SIMDs
-// the single chain wave does not use); the dense chain's helpers share their SIMDs with the
-// chain waves, and the log there cost the chain ~60 ns per step (vit_fwd 725 us OBS_PROB vs
-// 603 us OBS_LOG at B=32, T=2000, N=128, profiles/r5h_*): this pass moves 2 x 33 MB instead.
+// OBS_PROB emissions: log(x + 1e-8) correctly rounded (logcr.h, the fp32 sum as hmm.py:152
+// forms it) in one full-chip pass before the chain, which then stages them as OBS_LOG.  In the
+// chain's staging the log cost ~60 ns per dense step (vit_fwd 725 us OBS_PROB vs 603 us
+// OBS_LOG at B=32, T=2000, N=128, profiles/r5h_*), and on the banded chain, where one helper
+// wave staged 2048 logs per 16-step block, it bounded the chain (vit_fwd 202 -> 163 us, the
+// Viterbi op 229 -> 213 us, NS 269 -> 288 M frames/s, profiles/r5y*): this pass moves 2 x 33 MB
+// instead.
 __global__ void __launch_bounds__(256) vit_log_obs_kernel(const float* __restrict__ x, float* __restrict__ lo,
                                                           size_t n, int vec) {
   const size_t n4 = vec ? n / 4 : 0;
@@ -87,6 +88,13 @@ static int device_cus() {
   return cus[dev] > 0 ? cus[dev] : 0;
 }
 
+// OBS_PROB emissions go through the log pass for every chain (HMM355_VIT_LOGPASS=0: the banded
+// chain's staging helpers take the log themselves, the round-4 form, diagnostic)
+static bool vit_logpass() {
+  const char* e = getenv("HMM355_VIT_LOGPASS");
+  return !(e && e[0] == '0');
+}
+
 static int viterbi_run(const float* obs, int obs_mode, const float* log_P, const float* init, const void* plan,
                        unsigned flags, int B, int T, int N, int q_lo, int q_hi, int64_t* states, float* log_delta,
                        float* final_score, void* workspace, size_t workspace_bytes, void* stream) {
@@ -115,9 +123,8 @@ static int viterbi_run(const float* obs, int obs_mode, const float* log_P, const
   BandDesc* band = use_band() ? (plan ? static_cast<BandDesc*>(const_cast<void*>(plan))
                                       : reinterpret_cast<BandDesc*>(bandp))
                                : nullptr;
-  // OBS_PROB: the chain's staging takes log(x + 1e-8) itself (logcr.h, ~12 fp64 operations
-  // per element on the helper waves), so the emissions are read once and no log_obs tensor
-  // round-trips through HBM
+  // (OBS_PROB: the log pass below, or with HMM355_VIT_LOGPASS=0 on a plan that is not dense the
+  // chain's staging helpers take log(x + 1e-8) themselves, ~12 fp64 operations per element)
   VitArgs va{obs, log_P, init, log_delta, final_score, states, psi, G, B, T, N, obs_mode, nc, band};
   // (the whole range stays q_lo = q_hi = 0: the chain kernel then picks the banded chain where the
   // plan is banded; a part always runs the register-blocked dense chain, recur.h rec_dispatch)
@@ -149,7 +156,7 @@ static int viterbi_run(const float* obs, int obs_mode, const float* log_P, const
     va.done = done;
   }
   hipError_t e;
-  if ((flags & HMM355_VIT_PLAN_DENSE) && plan && obs_mode == HMM355_OBS_PROB) {
+  if (obs_mode == HMM355_OBS_PROB && (((flags & HMM355_VIT_PLAN_DENSE) && plan) || vit_logpass())) {
     const size_t n = (size_t)B * T * N;
     size_t blocks = (n / 4 + 255) / 256;
     blocks = blocks < 8192 ? (blocks > 0 ? blocks : 1) : 8192;

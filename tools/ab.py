@@ -54,7 +54,7 @@ p = lambda t: ctypes.c_void_p(t.data_ptr())
 lp0 = torch.full((N,), -4.85, device=dev)
 for mname, P in mats.items():
     lP = torch.log(P / P.sum(1, keepdim=True) + 1e-8)
-    fb = lambda L: L.hmm355_forward_backward_f32(p(obs), 0, p(lP), p(lp0), B, T, N, 7, p(post), p(fwd), p(bwd),
+    fb = lambda L: L.hmm355_forward_backward_f32(p(obs), 0, p(lP), p(lp0), B, T, N, int(os.environ.get("FBMASK", 7)), p(post), p(fwd), p(bwd),
                                                  p(ll), p(lr), p(ws), ws.numel(), st)
     vit = lambda L: L.hmm355_viterbi_f32(p(obs), 0, p(lP), p(lp0), B, T, N, p(states), p(delta), p(fin), p(wsv),
                                          wsv.numel(), st)
