@@ -9,6 +9,8 @@ D = sys.argv[1]
 
 def short(name):
     m = re.search(r"hmm355::(\w+)(<\d+(?:, *\w+)*>)?", name)
+    if not m:  # kernels outside the namespace (viterbi.hip's vit_log_obs_kernel)
+        m = re.match(r"(?:void\s+)?(\w+_kernel)(<\d+(?:, *\w+)*>)?\(", name)
     return (m.group(1) + (m.group(2) or "")).replace(" ", "") if m else None
 
 
