@@ -351,14 +351,15 @@ int hmm355_semimarkov_forward_f32(const float* quad, const float* seg_const,
 /* ---------------------------------------------------------------------------------
  * Streaming decoders of StreamingHMMProcessor, one chunk of B independent streams.
  *   emis (B,T,N): the emission network's log-probabilities; log_T (N,N) =
- *   log(softmax(transition_logits) + 1e-8).  1 <= N <= 128.
+ *   log(softmax(transition_logits) + 1e-8).  1 <= N <= 256 (log_T LDS-resident up to 128; above
+ *   that its rows are read from global memory per step).
  * hmm355_stream_greedy_f32 replaces _greedy_decode (streaming.py:267-320):
  *   s_t = argmax_j (log_T[s_{t-1}][j] + emis[t][j]), first index on ties; the chain starts
  *   from prev_state[b], or, when prev_state[b] < 0 (the stream's first chunk), from
  *   emis[0][j] - log_n with log_n = log(N) in fp32.  states (B,T) int64, scores (B,T) the
  *   chosen step scores (the reference returns exp(scores)).
  * hmm355_stream_beam_f32 replaces _beam_search_decode (streaming.py:322-377):
- *   hyp_score / hyp_last (B,16) and hyp_count (B) (<= 16) hold each stream's hypotheses in
+ *   hyp_score / hyp_last (B,32) and hyp_count (B) (<= 32) hold each stream's hypotheses in
  *   rank order and are updated in place (a stream may carry more hypotheses than the new K,
  *   after its beam width was lowered, streaming.py:459-461); first[b] != 0 applies the empty-path rule of the stream's first
  *   frame (score + emis, no transition).  Each step keeps the K best of the hyp_count * N
@@ -366,7 +367,8 @@ int hmm355_semimarkov_forward_f32(const float* quad, const float* seg_const,
  *   stable sort), score = (score_h + log_T[last_h][j]) + emis[t][j] in fp32.
  *   parent / hstate (B,T,K) int16: new hypothesis r at step t came from hypothesis
  *   parent[t][r] of step t-1 and entered state hstate[t][r].  states (B,T) int64: the best
- *   hypothesis' last T states.  1 <= K <= 16; live_max (<= 16) bounds every hyp_count[b].
+ *   hypothesis' last T states.  1 <= K <= 32 and live_max (<= 32) bounds every hyp_count[b];
+ *   for N > 128, K and live_max <= 16 (else HMM355_E_ARG).
  * ------------------------------------------------------------------------------ */
 int hmm355_stream_greedy_f32(const float* emis, const float* log_T, const int* prev_state,
                              float log_n, int B, int T, int N, int64_t* states, float* scores,

@@ -586,7 +586,7 @@ def _(quad, seg_const, log_init, log_T, dur_lp, want_alpha):
 
 
 # ------------------------------------------------------------------ streaming decoders
-STREAM_SLOTS = 16   # hypothesis slots per stream (max beam width)
+STREAM_SLOTS = 32   # hypothesis slots per stream (max beam width; 16 when N > 128)
 
 @torch.library.custom_op("hmm355::stream_greedy", mutates_args=())
 def stream_greedy(emis: Tensor, log_T: Tensor, prev_state: Tensor, log_n: float) -> Tuple[Tensor, Tensor]:
@@ -613,9 +613,9 @@ def _(emis, log_T, prev_state, log_n):
 
 def stream_beam(emis: Tensor, log_T: Tensor, beam_width: int, hyp_score: Tensor, hyp_last: Tensor,
                 hyp_count: Tensor, first: Tensor, live_max: int = STREAM_SLOTS):
-    """One chunk of beam search for B streams.  hyp_score (B,16) fp32, hyp_last (B,16) int32
+    """One chunk of beam search for B streams.  hyp_score (B,32) fp32, hyp_last (B,32) int32
     and hyp_count (B) int32 are the streams' hypotheses (rank order, STREAM_SLOTS slots),
-    updated IN PLACE; K = beam_width <= 16;
+    updated IN PLACE; K = beam_width <= 32 (<= 16 when N > 128), N <= 256;
     first (B) int32 marks streams whose paths are still empty; live_max bounds hyp_count.  Returns (best-path states
     (B,T) int64, parent (B,T,K) int16, state (B,T,K) int16): new hypothesis r at step t came
     from hypothesis parent[t, r] of step t-1 and entered state[t, r]."""

@@ -243,8 +243,9 @@ class StreamingHMMProcessor(nn.Module):
             K = self.beam_width
             hyps = self.beam_hypotheses
             kc = len(hyps)
-            if not 1 <= K <= ops.STREAM_SLOTS or kc > ops.STREAM_SLOTS:
-                raise ValueError(f"beam_width must be in [1, {ops.STREAM_SLOTS}] on this path, got {K}")
+            kmax = ops.STREAM_SLOTS if self.num_states <= 128 else 16  # (stream.hip: the lane's candidate mask)
+            if not 1 <= K <= kmax or kc > kmax:
+                raise ValueError(f"beam_width must be in [1, {kmax}] on this path for {self.num_states} states, got {K}")
             hs = torch.full((1, ops.STREAM_SLOTS), float("-inf"), device=dev)
             hl = torch.zeros((1, ops.STREAM_SLOTS), dtype=torch.int32, device=dev)
             if kc:

@@ -4,7 +4,7 @@ StreamingHMMProcessor.
 - kernels vs the C oracle (itself pinned to the reference, tests/test_streaming_cpu.py):
   exact states, step scores, hypotheses and back-pointers, given the same fp32 inputs —
   the reference's own emission log-probs from the fixtures, and random / tie-heavy inputs up
-  to N = 128, K = 16 over several 64-frame tiles;
+  to N = 256, K = 32 (K = 16 above N = 128) over several 64-frame tiles;
 - the processor (emission net on the GPU) against the reference's process_chunk and direct
   decode outputs: states exact; confidences within 1e-5 relative (GEMM rounding in the
   emission net).
@@ -77,7 +77,10 @@ def test_kernels_on_reference_emissions(name):
     (0, 3, 300, 128, 16, False, None), (1, 2, 129, 64, 8, False, None), (2, 4, 70, 7, 5, True, None),
     (3, 2, 65, 100, 3, True, None), (4, 1, 1, 9, 1, False, None),
     (5, 2, 80, 20, 4, False, 12),     # beam lowered: 12 live hypotheses, K = 4
-    (6, 2, 90, 100, 8, True, 8)])
+    (6, 2, 90, 100, 8, True, 8),
+    # round 5: N <= 256 (log T read from global memory above 128) and beams up to 32
+    (7, 2, 150, 256, 16, False, None), (8, 2, 100, 200, 12, True, None), (9, 2, 130, 129, 9, False, None),
+    (10, 2, 130, 128, 32, False, None), (11, 2, 70, 64, 32, True, None), (12, 2, 90, 50, 24, False, 30)])
 def test_kernels_vs_oracle_random(seed, B, T, N, K, ties, k0):
     rng = np.random.default_rng(seed)
     if ties:
@@ -137,3 +140,13 @@ def test_processor_vs_reference(name):
         stats = p.get_performance_stats()
         assert "avg_processing_time_ms" in stats or "message" in stats
         assert p.flush_buffer().status == "flushed"
+
+
+def test_beam_limits():
+    """K <= 32, and K <= 16 above N = 128 (the lane's candidate mask): larger asks raise."""
+    rng = np.random.default_rng(0)
+    for N, K in ((200, 17), (64, 33)):
+        emis = np.log(rng.dirichlet(np.ones(N), size=(1, 8))).astype(np.float32)
+        log_T = np.log(rng.dirichlet(np.ones(N), size=N) + 1e-8).astype(np.float32)
+        with pytest.raises((ValueError, RuntimeError)):
+            gpu_beam(emis, log_T, K, [np.zeros(1, np.float32)], [np.zeros(1, np.int64)], [True])
