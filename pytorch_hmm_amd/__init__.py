@@ -18,8 +18,8 @@ from .mixture_gaussian import MixtureGaussianHMMLayer
 from .hsmm import HSMMLayer
 from .neural import NeuralHMM, ContextualNeuralHMM
 from .semi_markov import DurationModel, SemiMarkovHMM, AdaptiveDurationHSMM
-from .streaming import StreamingHMMProcessor, StreamingResult
+from .streaming import AdaptiveLatencyController, StreamingHMMProcessor, StreamingResult
 
 __all__ += ["HMMLayer", "GaussianHMMLayer", "MixtureGaussianHMMLayer", "HSMMLayer", "NeuralHMM",
             "ContextualNeuralHMM", "DurationModel", "SemiMarkovHMM", "AdaptiveDurationHSMM",
-            "StreamingHMMProcessor", "StreamingResult"]
+            "StreamingHMMProcessor", "StreamingResult", "AdaptiveLatencyController"]

@@ -7,9 +7,15 @@ per-frame Python loops run as gfx950 kernels (csrc/stream.hip): ``_greedy_decode
 (streaming.py:322-377) as K rounds of wave argmax per frame over the hypotheses'
 expansions, with the reference's stable tie order.  The emission network stays a torch
 module (two GEMMs on hipBLASLt); the chunk buffering and bookkeeping are host logic, as in
-the reference.  The reference's latency-control helpers (``optimize_for_latency``,
-``get_latency_breakdown``, ``AdaptiveLatencyController``, streaming.py:444-592) are out of
-scope and not provided.
+the reference.
+
+The latency-control helpers are host policy with the reference's public behaviour
+(``optimize_for_latency`` streaming.py:444-483, ``get_latency_breakdown`` :485-503,
+``AdaptiveLatencyController`` :506-592), written here as explicit rule tables
+(``_LATENCY_STEPS``, ``AdaptiveLatencyController._RULES``).  One difference by design: the
+reference's breakdown is a fixed 10/30/10/40/10 % split of the mean chunk time; here each
+phase of a decoded chunk is timed on the host (``_PHASES``) and the breakdown reports those
+means under the reference's keys.
 """
 import queue
 import threading
@@ -58,6 +64,8 @@ class StreamingHMMProcessor(nn.Module):
             nn.LogSoftmax(dim=-1))
         self.reset_streaming_state()
         self.processing_times = deque(maxlen=1000)
+        # host wall time of each phase of the decoded chunks (get_latency_breakdown)
+        self.phase_times = {k: deque(maxlen=1000) for k in _PHASES}
         self.chunk_counter = 0
         self.total_frames_processed = 0
         self.processing_queue = queue.Queue(maxsize=self.buffer_size)
@@ -178,26 +186,42 @@ class StreamingHMMProcessor(nn.Module):
             return None
 
     # -- chunk processing (streaming.py:183-265) --------------------------------------------
+    def _mark(self, phase: str):
+        """Charge the host time since the previous mark of this chunk to `phase`."""
+        c = getattr(self, "_clock", None)
+        if c is not None:
+            now = time.perf_counter()
+            c[phase] = c.get(phase, 0.0) + (now - c["_last"]) * 1e3
+            c["_last"] = now
+
     def process_chunk(self, audio_chunk: torch.Tensor) -> StreamingResult:
         t0 = time.time()
+        self._clock = {"_last": time.perf_counter()}
         for frame in audio_chunk:
             self.feature_buffer.append(frame)
         available = len(self.feature_buffer)
         required = self.chunk_size + self.lookahead_frames
         if available < required:
+            self._clock = None
             return StreamingResult(None, 0.0, (time.time() - t0) * 1000, available, self.chunk_counter,
                                    "buffering", {"frames_needed": required - available})
         start = max(0, self.last_output_frame + 1)
         end = available - self.lookahead_frames
         if end <= start:
+            self._clock = None
             return StreamingResult(None, 0.0, (time.time() - t0) * 1000, available, self.chunk_counter,
                                    "waiting_for_lookahead", {})
         features = torch.stack(list(self.feature_buffer)[start:end])
+        self._mark("feature_extraction")
         states, conf = self._decode(features)
         self.last_output_frame = end - 1
         self.total_frames_processed += len(features)
         dt = (time.time() - t0) * 1000
         self.processing_times.append(dt)
+        self._mark("bookkeeping")
+        clock, self._clock = self._clock, None
+        for k in _PHASES:
+            self.phase_times[k].append(clock.get(k, 0.0))
         self.chunk_counter += 1
         rtf = (len(features) * 1000 / 100) / dt if dt > 0 else float("inf")
         return StreamingResult(states, conf.mean().item() if conf is not None else 0.0, dt, available,
@@ -221,13 +245,18 @@ class StreamingHMMProcessor(nn.Module):
         """One greedy chain over the chunk; continues from the stream's last state."""
         with torch.no_grad():
             emis = self.emission_net(features)
+            self._mark("emission_computation")
             prev = self.viterbi_states[-1] if self.viterbi_states else -1
             prev_t = torch.tensor([prev], dtype=torch.int32, device=emis.device)
             log_n = float(torch.log(torch.tensor(self.num_states)))
-            states, scores = ops.stream_greedy(emis.unsqueeze(0), self._log_transitions(), prev_t, log_n)
+            log_t = self._log_transitions()
+            self._mark("transition_computation")
+            states, scores = ops.stream_greedy(emis.unsqueeze(0), log_t, prev_t, log_n)
             states, scores = states[0], scores[0]
-            self.viterbi_states.extend(states.tolist())
-            self.viterbi_scores.extend(scores.tolist())
+            st_list, sc_list = states.tolist(), scores.tolist()   # (waits for the decode)
+            self._mark("viterbi_decoding")
+            self.viterbi_states.extend(st_list)
+            self.viterbi_scores.extend(sc_list)
             if len(self.viterbi_states) > self.max_delay_frames:
                 excess = len(self.viterbi_states) - self.max_delay_frames
                 self.viterbi_states = self.viterbi_states[excess:]
@@ -239,6 +268,7 @@ class StreamingHMMProcessor(nn.Module):
         T = features.shape[0]
         with torch.no_grad():
             emis = self.emission_net(features)
+            self._mark("emission_computation")
             dev = emis.device
             K = self.beam_width
             hyps = self.beam_hypotheses
@@ -253,11 +283,14 @@ class StreamingHMMProcessor(nn.Module):
                 hl[0, :kc] = torch.tensor([h[2] for h in hyps], dtype=torch.int32, device=dev)
             cnt = torch.tensor([kc], dtype=torch.int32, device=dev)
             first = torch.tensor([int(kc > 0 and all(len(h[1]) == 0 for h in hyps))], dtype=torch.int32, device=dev)
-            states, parent, hstate = ops.stream_beam(emis.unsqueeze(0), self._log_transitions(), K, hs, hl, cnt, first,
+            log_t = self._log_transitions()
+            self._mark("transition_computation")
+            states, parent, hstate = ops.stream_beam(emis.unsqueeze(0), log_t, K, hs, hl, cnt, first,
                                                      live_max=max(kc, 1))
             # rebuild the hypotheses' paths: new hypothesis r descends from old hypothesis h0
             kn = int(cnt.item())
             par, hst = parent[0].cpu().tolist(), hstate[0].cpu().tolist()
+            self._mark("viterbi_decoding")
             new = []
             for r in range(kn):
                 tail, rr = [], r
@@ -292,3 +325,142 @@ class StreamingHMMProcessor(nn.Module):
             "beam_width": self.beam_width if self.use_beam_search else 1,
             "processing_mode": "beam_search" if self.use_beam_search else "greedy",
         }
+
+    # -- latency control (streaming.py:444-503) --------------------------------------------
+    def optimize_for_latency(self, target_latency_ms: float = 50.0):
+        """One adjustment step toward `target_latency_ms` from the mean chunk time so far:
+        above the target the first applicable entry of ``_LATENCY_STEPS["slower"]`` is taken
+        (narrow the beam, then greedy decoding, then shorter chunks); below half the target
+        the first of ``["faster"]`` (beam search back on at width 4, then a wider beam).
+        Without timing data it warns and changes nothing (streaming.py:444-483)."""
+        stats = self.get_performance_stats()
+        if "avg_processing_time_ms" not in stats:
+            warnings.warn("No performance data available for optimization")
+            return
+        lat = stats["avg_processing_time_ms"]
+        if lat > target_latency_ms:
+            table = _LATENCY_STEPS["slower"]
+        elif lat < 0.5 * target_latency_ms:
+            table = _LATENCY_STEPS["faster"]
+        else:
+            return
+        for applies, apply in table:
+            if applies(self):
+                print(apply(self))
+                return
+
+    def get_latency_breakdown(self) -> Dict[str, float]:
+        """Mean host time (ms) per phase of the decoded chunks, under the reference's keys
+        (streaming.py:485-503), plus 'total' = the mean chunk time; {} before any chunk was
+        decoded.  The phases are measured (``_mark``), not a fixed split: feature_extraction
+        (buffering and stacking the frames), emission_computation (the emission network),
+        transition_computation (the log-transition table), viterbi_decoding (the decode kernel
+        and reading its result back), bookkeeping (path and state updates)."""
+        stats = self.get_performance_stats()
+        if "avg_processing_time_ms" not in stats:
+            return {}
+        out = {k: (sum(v) / len(v) if v else 0.0) for k, v in self.phase_times.items()}
+        out["total"] = stats["avg_processing_time_ms"]
+        return out
+
+
+# phases timed per decoded chunk (get_latency_breakdown), in the reference's key order
+_PHASES = ("feature_extraction", "emission_computation", "transition_computation", "viterbi_decoding",
+           "bookkeeping")
+
+
+def _set(p, **kw):
+    for k, v in kw.items():
+        setattr(p, k, v)
+
+
+# optimize_for_latency's steps: (applies(processor), apply(processor) -> message), first match wins
+_LATENCY_STEPS = {
+    "slower": (
+        (lambda p: p.use_beam_search and p.beam_width > 2,
+         lambda p: (_set(p, beam_width=max(2, p.beam_width - 1)), f"Reduced beam width to {p.beam_width}")[1]),
+        (lambda p: p.use_beam_search,
+         lambda p: (_set(p, use_beam_search=False), "Switched to greedy decoding for lower latency")[1]),
+        (lambda p: p.chunk_size > 80,
+         lambda p: (_set(p, chunk_size=max(80, int(p.chunk_size * 0.8))), f"Reduced chunk size to {p.chunk_size}")[1]),
+    ),
+    "faster": (
+        (lambda p: not p.use_beam_search,
+         lambda p: (_set(p, use_beam_search=True, beam_width=4), "Enabled beam search for better accuracy")[1]),
+        (lambda p: p.beam_width < 8,
+         lambda p: (_set(p, beam_width=p.beam_width + 1), f"Increased beam width to {p.beam_width}")[1]),
+    ),
+}
+
+
+class AdaptiveLatencyController:
+    """Recommends streaming parameters from a window of observed chunk latencies
+    (streaming.py:506-592).  ``update`` records one chunk's latency and, at most once per
+    ``cooldown_s`` and only after ``min_history`` observations, classifies the mean and
+    variance of the last ``window`` latencies into one regime of ``_RULES`` (first match):
+
+      overloaded  mean > 1.2 x target: shrink the chunk by ``adaptation_rate`` (not below
+                  min_chunk_size), beam width 3, beam search only while mean <= 2 x target
+      headroom    mean < 0.6 x target and variance < 10: grow the chunk (not above
+                  max_chunk_size) when the buffer holds > 100 frames, beam width 6, beam on
+      jittery     variance > 25: greedy decoding, chunk 0.9x (recommended, not adopted)
+
+    and returns the recommendations (an empty dict when none applies or it is too early)."""
+
+    window = 20
+    min_history = 10
+    cooldown_s = 1.0
+
+    def __init__(self, initial_chunk_size: int = 160, min_chunk_size: int = 80, max_chunk_size: int = 320,
+                 target_latency_ms: float = 50.0, adaptation_rate: float = 0.1):
+        self.chunk_size = initial_chunk_size
+        self.min_chunk_size = min_chunk_size
+        self.max_chunk_size = max_chunk_size
+        self.target_latency_ms = target_latency_ms
+        self.adaptation_rate = adaptation_rate
+        self.latency_history = deque(maxlen=100)
+        self.adjustment_cooldown = 0
+        self.last_adjustment_time = 0
+
+    def _overloaded(self, mean, var, buffer_size):
+        rec = {}
+        if self.chunk_size > self.min_chunk_size:
+            self.chunk_size = rec["chunk_size"] = max(self.min_chunk_size,
+                                                      int(self.chunk_size * (1 - self.adaptation_rate)))
+        rec["beam_width"] = 3
+        rec["use_beam_search"] = not mean > 2 * self.target_latency_ms
+        return rec
+
+    def _headroom(self, mean, var, buffer_size):
+        rec = {}
+        if self.chunk_size < self.max_chunk_size and buffer_size > 100:
+            self.chunk_size = rec["chunk_size"] = min(self.max_chunk_size,
+                                                      int(self.chunk_size * (1 + self.adaptation_rate)))
+        rec["beam_width"] = 6
+        rec["use_beam_search"] = True
+        return rec
+
+    def _jittery(self, mean, var, buffer_size):
+        return {"use_beam_search": False, "chunk_size": max(self.min_chunk_size, int(self.chunk_size * 0.9))}
+
+    _RULES = (
+        (lambda c, m, v: m > 1.2 * c.target_latency_ms, _overloaded),
+        (lambda c, m, v: m < 0.6 * c.target_latency_ms and v < 10.0, _headroom),
+        (lambda c, m, v: v > 25.0, _jittery),
+    )
+
+    def update(self, processing_time_ms: float, buffer_size: int) -> Dict[str, Any]:
+        self.latency_history.append(processing_time_ms)
+        now = time.time()
+        if now - self.last_adjustment_time < self.cooldown_s or len(self.latency_history) < self.min_history:
+            return {}
+        recent = torch.tensor(list(self.latency_history)[-self.window:])
+        mean, var = float(recent.mean()), float(recent.var())
+        rec = {}
+        for matches, rule in self._RULES:
+            if matches(self, mean, var):
+                rec = rule(self, mean, var, buffer_size)
+                break
+        if rec:
+            self.last_adjustment_time = now
+        return rec

@@ -148,3 +148,97 @@ def test_log_transition_cache_sees_data_writes_state_dicts_and_training():
     p.transition_logits.data.mul_(2.0)
     p.train(); p.eval()
     assert torch.equal(p._log_transitions(), want())
+
+
+def test_optimize_for_latency_steps():
+    """optimize_for_latency (reference streaming.py:444-483): one adjustment per call, from the
+    mean chunk time: above the target narrow the beam (not below 2), then greedy, then chunks
+    x0.8 (not below 80); below half the target beam search back on at width 4, then +1 up to 8;
+    in between nothing; without timing data a warning and nothing."""
+    import warnings as _w
+    from pytorch_hmm_amd.streaming import StreamingHMMProcessor
+    p = StreamingHMMProcessor(4, 3, chunk_size=160, beam_width=3)
+    with _w.catch_warnings(record=True) as rec:
+        _w.simplefilter("always")
+        p.optimize_for_latency(10.0)
+    assert any("No performance data" in str(x.message) for x in rec) and p.beam_width == 3
+    p.processing_times.extend([40.0, 60.0])         # mean 50 ms
+    seen = []
+    for _ in range(6):
+        p.optimize_for_latency(25.0)
+        seen.append((p.use_beam_search, p.beam_width, p.chunk_size))
+    assert seen == [(True, 2, 160), (False, 2, 160), (False, 2, 128), (False, 2, 102), (False, 2, 81),
+                    (False, 2, 80)]
+    p.optimize_for_latency(60.0)                    # 50 in [30, 60]: unchanged
+    assert (p.use_beam_search, p.beam_width, p.chunk_size) == (False, 2, 80)
+    for want in [(True, 4), (True, 5), (True, 6), (True, 7), (True, 8), (True, 8)]:
+        p.optimize_for_latency(200.0)
+        assert (p.use_beam_search, p.beam_width) == want
+
+
+def test_latency_breakdown_reports_measured_phases():
+    """get_latency_breakdown (reference streaming.py:485-503): {} before any chunk; then the
+    reference's keys, each the mean of the host-timed phase, and 'total' the mean chunk time."""
+    from pytorch_hmm_amd.streaming import StreamingHMMProcessor, _PHASES
+    p = StreamingHMMProcessor(4, 3, chunk_size=8)
+    assert p.get_latency_breakdown() == {}
+    for k, vals in zip(_PHASES, ([1.0, 3.0], [2.0, 2.0], [0.5, 0.5], [4.0, 6.0], [0.25, 0.75])):
+        p.phase_times[k].extend(vals)
+    p.processing_times.extend([8.0, 12.0])
+    got = p.get_latency_breakdown()
+    assert list(got) == ["feature_extraction", "emission_computation", "transition_computation",
+                         "viterbi_decoding", "bookkeeping", "total"]
+    assert got == {"feature_extraction": 2.0, "emission_computation": 2.0, "transition_computation": 0.5,
+                   "viterbi_decoding": 5.0, "bookkeeping": 0.5, "total": 10.0}
+
+
+def test_phase_clock_charges_marks():
+    """The per-chunk clock charges the time between marks to the named phase."""
+    import time as _t
+    from pytorch_hmm_amd.streaming import StreamingHMMProcessor
+    p = StreamingHMMProcessor(4, 3)
+    p._mark("viterbi_decoding")                      # no chunk in flight: ignored
+    p._clock = {"_last": _t.perf_counter()}
+    _t.sleep(0.02)
+    p._mark("viterbi_decoding")
+    p._mark("bookkeeping")
+    assert p._clock["viterbi_decoding"] >= 15.0 and p._clock["bookkeeping"] < 15.0
+
+
+def test_adaptive_latency_controller_rules(monkeypatch):
+    """AdaptiveLatencyController.update (reference streaming.py:506-592): nothing before ten
+    observations or within a second of the last recommendation; then from the last 20
+    latencies: overloaded (mean > 1.2 target) -> chunk x0.9 (adopted), beam width 3, beam search
+    iff mean <= 2 target; headroom (mean < 0.6 target, variance < 10) -> chunk x1.1 only with
+    > 100 frames buffered, width 6, beam on; jittery (variance > 25) -> greedy, chunk x0.9 (not
+    adopted)."""
+    import pytorch_hmm_amd as ph
+    from pytorch_hmm_amd import streaming as S
+    clock = [1000.0]
+    monkeypatch.setattr(S.time, "time", lambda: clock[0])
+    c = ph.AdaptiveLatencyController(initial_chunk_size=160, min_chunk_size=80, max_chunk_size=320,
+                                     target_latency_ms=30.0)
+    assert (c.chunk_size, c.min_chunk_size, c.max_chunk_size, c.target_latency_ms) == (160, 80, 320, 30.0)
+    for _ in range(9):
+        assert c.update(50.0, 100) == {}
+    assert c.update(50.0, 100) == {"chunk_size": 144, "beam_width": 3, "use_beam_search": True}
+    assert c.chunk_size == 144
+    clock[0] += 0.5
+    assert c.update(50.0, 100) == {}                 # cooldown
+    clock[0] += 1.0
+    for _ in range(20):
+        c.latency_history.append(70.0)
+    assert c.update(70.0, 100) == {"chunk_size": 129, "beam_width": 3, "use_beam_search": False}
+    # headroom: needs a full window of low, steady latencies
+    c2 = ph.AdaptiveLatencyController(target_latency_ms=30.0)
+    for _ in range(10):
+        r = c2.update(10.0, 50)
+    assert r == {"beam_width": 6, "use_beam_search": True} and c2.chunk_size == 160
+    assert c2.update(10.0, 50) == {}                # cooldown after a recommendation
+    clock[0] += 2.0
+    assert c2.update(10.0, 150) == {"chunk_size": 176, "beam_width": 6, "use_beam_search": True}
+    # jittery: mean inside the band, variance large
+    c3 = ph.AdaptiveLatencyController(target_latency_ms=30.0)
+    for v in [20.0, 40.0] * 5:
+        r = c3.update(v, 0)
+    assert r == {"use_beam_search": False, "chunk_size": 144} and c3.chunk_size == 160
