@@ -61,6 +61,15 @@ def parse():
     p.add_argument("--workload", default="ns", choices=["ns", "c1", "c2", "c3", "c5", "neural", "smk", "stream"],
                    help="ns: the BASELINE metric (default).  c1/c2/c3/c5: BASELINE configs 1, 2, 3, 5 "
                         "(HMMLayer, GaussianHMMLayer, MixtureGaussianHMMLayer, HSMMLayer) through the layers")
+    p.add_argument("--tv-static", action="store_true",
+                   help="neural workload, diagnostic: one (N,N) matrix for every step (L2-resident)")
+    p.add_argument("--tv-only", choices=["fb", "vit"], default=None,
+                   help="neural workload, diagnostic: run only the forward-backward or only the Viterbi call")
+    p.add_argument("--no-kernel-profile", action="store_true",
+                   help="layer workloads: skip the torch.profiler pass that finds the dominant kernel")
+    p.add_argument("--no-follow", action="store_true",
+                   help="ns workload, diagnostic: run the passes after the chains instead of the work "
+                        "beside them in the chains' launches (csrc/follow.h)")
     return p.parse_args()
 
 
@@ -300,26 +309,18 @@ def layer_workload(args, rank, world, dev):
         # forward_backward (posteriors, forward, backward) + viterbi_decode, on two streams.
         B, T, N = args.batch, args.T, args.N
         lo = torch.randn(B, T, N, device=dev, generator=gx) * 3 - 40
-        if os.environ.get("HMM355_TV_STATIC"):   # diagnostic: one matrix for every step (L2-resident)
+        if args.tv_static:   # diagnostic: one matrix for every step (L2-resident)
             lA = torch.log(torch.softmax(torch.randn(N, N, device=dev, generator=gx) * 2, dim=-1) + 1e-8)
         else:
             lA = torch.log(torch.softmax(torch.randn(B, T, N, N, device=dev, generator=gx) * 2, dim=-1) + 1e-8)
-        only = os.environ.get("HMM355_TV_ONLY", "")   # diagnostic: "fb" or "vit"
+        only = args.tv_only or ""   # diagnostic: "fb" or "vit"
         init = torch.full((N,), -math.log(N), device=dev)
         layer = (lo, lA, init)
         s_fb, s_vit = torch.cuda.Stream(dev), torch.cuda.Stream(dev)
         mask = ph.ops.FB_POSTERIOR | ph.ops.FB_FORWARD | ph.ops.FB_BACKWARD
 
-        # HMM355_TV_FUSED=1: one call, alpha + Viterbi sharing one stream of log_A (tv_fbv):
-        # less HBM traffic but slower (its CU is compute-bound); the default is
-        # the two calls on two streams
-        split = os.environ.get("HMM355_TV_FUSED", "") != "1" or only
-
+        # the two calls on two streams (one stream of log_A each)
         def step():
-            if not split:
-                # one call: the alpha and Viterbi recursions share one stream of log_A
-                # (tv_chain_av), beta beside them; the posterior, chunk-map and backtrace passes after
-                return ph.ops.tv_fb_viterbi(lo, lA, init, init, mask)
             cur = torch.cuda.current_stream(dev)
             s_fb.wait_stream(cur)
             s_vit.wait_stream(cur)
@@ -389,9 +390,13 @@ def layer_workload(args, rank, world, dev):
             return layer(x)                 # Gaussian emission + segment Viterbi
         desc = {"workload": "HSMMLayer(64,80,max_duration=40) forward (segment Viterbi)", "batch_per_gpu": B,
                 "seq_len": T, "num_states": S, "max_duration": Dm, "feature_dim": D}
-        # reorganised recursion: per start, S*S*Dmax (max over d') + S*S (candidates) adds/max
-        dom, flops, bytes_ = "hsmm_fwd_kernel", 2.0 * (S * S * Dm + S * S) * B * T, (4 * S + 8) * B * T
-        models = {"hsmm_fwd": ("valu", 2.0 * (S * S * Dm + S * S)), "gmm_score": ("valu64", 4.0 * S * D)}
+        # the reorganised recursion hsmm_fwd issues (csrc/hsmm.hip): per end time and state, each of
+        # the Dmax open segments takes its obs-sum add, the two delta adds and the max into Dm (4
+        # ops), and the predecessor maximum M adds and maxes S candidates: 4*S*Dmax + 2*S^2 per frame
+        # (rounds 3-5 priced 2(S^2 Dmax + S^2), the literal loop's count, 17x this)
+        hs_ops = 4.0 * S * Dm + 2.0 * S * S
+        dom, flops, bytes_ = "hsmm_fwd_kernel", hs_ops * B * T, (4 * S + 8) * B * T
+        models = {"hsmm_fwd": ("valu", hs_ops), "gmm_score": ("valu64", 4.0 * S * D)}
 
     # --overlap-steps: consecutive steps alternate between two HIP streams (each step's own
     # calls stay in order on its stream), so step k+1's full-chip emission scoring runs on the
@@ -449,7 +454,7 @@ def layer_workload(args, rank, world, dev):
     frames = desc["batch_per_gpu"] * desc["seq_len"]
     value = frames * world * args.steps / elapsed
     kroof = None
-    if os.environ.get("HMM355_BENCH_NO_KPROF") != "1":
+    if not args.no_kernel_profile:
         try:
             with torch.no_grad():
                 kroof = kernel_roofline(kernel_profile(step), models, frames)
@@ -741,8 +746,9 @@ def main():
     # the batch (+ the gather when world > 1).  The two ops are independent, so each runs on
     # its own stream, replayed from a HIP graph; consecutive steps pipeline across the streams
     # (no per-step join: a cross-stream join costs two cross-queue signal hops, ~35 us).
-    step = NsStep({"fb": lambda: ops.forward_backward(obs, lP, lp0, ops.OBS_PROB, 7, plan),
-                   "vit": lambda: ops.viterbi(obs, lP, lp0, ops.OBS_PROB, plan)},
+    follow = False if args.no_follow else None
+    step = NsStep({"fb": lambda: ops.forward_backward(obs, lP, lp0, ops.OBS_PROB, 7, plan, follow=follow),
+                   "vit": lambda: ops.viterbi(obs, lP, lp0, ops.OBS_PROB, plan, follow=follow)},
                   dev, gatherer, use_graph=not args.no_graph, serial=args.serial)
 
     for _ in range(args.warmup):
@@ -789,13 +795,20 @@ def main():
              "random": "random dense softmax(randn(N,N))",
              "trained": "trained HMMLayer(N) tables (3 Adam steps)"}[args.transition]
     # roofline of the dominant op, algorithmic bytes per SURVEY.md §8(d)
-    pair = plan is not None and getattr(plan, "_hmm355_banded", False) and ops._use_pair(B, dev)
+    banded = plan is not None and getattr(plan, "_hmm355_banded", False)
+    pair = banded and ops._use_pair(B, dev)
+    cus = torch.cuda.get_device_properties(dev).multi_processor_count
+    # (the C ABI's conditions for the work beside the chains: fb.hip, viterbi.hip vit_follow_ok)
+    fb_follow = banded and not pair and not args.no_follow and 3 * B <= cus
+    vit_follow = banded and not args.no_follow and N > 64 and 4 * B <= cus
     if fb_ms >= vit_ms:
         dom, dur_ms, bytes_per_launch = "forward_backward", fb_ms, 16 * N * B * T
-        kernels = "fb_pair_kernel" if pair else "fb_recur_kernel + fb_posterior_kernel"
+        kernels = ("fb_pair_kernel" if pair else
+                   "fb_recur_kernel (chains + posterior followers)" if fb_follow else "fb_recur_kernel + fb_posterior_kernel")
     else:
         dom, dur_ms, bytes_per_launch = "viterbi", vit_ms, (8 * N + 8) * B * T
-        kernels = "vit_fwd_kernel + vit_psi_kernel + vit_backtrace_kernel"
+        kernels = ("vit_fwd_kernel (chains + log leaders + decode followers)" if vit_follow else
+                   "vit_log_obs_kernel + vit_fwd_kernel + vit_psi_kernel + vit_backtrace_kernel")
     achieved = bytes_per_launch / (dur_ms * 1e-3) / 1e9
     dom_traffic = traffic_fields(*profiled_traffic(dom, B, T, N, args.transition))
     # both ops' fractions (north_star's target names forward-backward's)
@@ -820,7 +833,10 @@ def main():
                               "event-ordered)") if gather else (False if world == 1 else "skipped (--no-gather)"),
                    "hip_graph": step.use_graph, "step_pipelining": "per-op streams, no per-step join",
                    "transition_plan": plan is not None,
-                   "fb_kernel": "pair (both chains + outputs in one workgroup)" if pair else "two-kernel"},
+                   "fb_kernel": ("pair (both chains + outputs in one workgroup)" if pair else
+                                 "chains + posterior followers in one launch" if fb_follow else "two-kernel"),
+                   "viterbi_kernel": ("chains + log leaders + decode followers in one launch" if vit_follow else
+                                      "log pass + chain + psi pass + backtrace")},
         "op_ms": {"forward_backward": fb_ms, "viterbi": vit_ms},
         "roofline": {"bound": "hbm", "kernel": dom, "kernels": kernels, "achieved": achieved,
                      "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,

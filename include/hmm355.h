@@ -51,6 +51,13 @@ extern "C" {
  * written back in full, so the workspace does NOT hold U / V / LA / LB afterwards.  A wrong
  * hint still gives correct results (slower).  N <= 128; ignored otherwise. */
 #define HMM355_FB_PAIR 0x100u
+/* Hint (forward_backward with a plan): the caller read hmm355_plan_banded(plan) == 1.  The chains
+ * then publish their rows as they go and one extra workgroup per sequence forms the posterior
+ * (and the chain forms lik_ref) inside the chains' own launch, instead of a pass after them
+ * (csrc/follow.h).  Needs HMM355_FB_POSTERIOR; ignored when the 3B workgroups would not fit the
+ * device at once.  Passing it with a plan that is not banded is a caller error: posterior and
+ * lik_ref come back NaN. */
+#define HMM355_FB_PLAN_BANDED 0x200u
 
 const char* hmm355_strerror(int code);
 int hmm355_version(void);
@@ -87,6 +94,10 @@ size_t hmm355_fb_workspace_bytes(int B, int T, int N);
  * the chains use the shifted emissions e_t = exp(obs_t - M_t), M_t = max_j obs_t[j] (a row
  * without a finite maximum: M_t = 0), and LA / LB carry the shifts, so log-emissions far
  * below -87 do not underflow; U and V are the rows of that shifted recursion. */
+/* Byte offsets of the workspace pieces above, in order U, V, LA, LB, BandDesc, beta init, its
+ * scale, row maxima M, CA, CB (offsets[10]), for callers that read U / V / LA / LB / CA / CB back
+ * (pytorch_hmm_amd/autograd.py); 0 or an HMM355_E_* code. */
+int hmm355_fb_workspace_layout(int B, int T, int N, size_t* offsets);
 int hmm355_forward_backward_ex_f32(const float* obs, int obs_mode, const float* log_P,
                                    const float* log_p0, const float* log_beta_T, int B, int T, int N,
                                    unsigned out_mask, float* posterior, float* forward,
@@ -125,6 +136,11 @@ int hmm355_fb_adjoint_f32(const float* E, const float* log_P, const float* src_w
  * ------------------------------------------------------------------------------ */
 size_t hmm355_plan_bytes(int N);
 int hmm355_plan_f32(const float* log_P, int N, void* plan, void* stream);
+/* As hmm355_plan_f32 with flags.  HMM355_PLAN_DENSE: the plan selects the dense chains for every
+ * recursion whatever the matrix's structure (hmm355_plan_banded then reads 0): the two chain
+ * families give the same results, and parity tests run both on one matrix. */
+#define HMM355_PLAN_DENSE 0x1u
+int hmm355_plan_ex_f32(const float* log_P, int N, unsigned flags, void* plan, void* stream);
 /* 1 if the plan selects banded chains for both the forward and the backward recursion (the
  * condition for HMM355_FB_PAIR), 0 if not, < 0 on error.  Synchronous: waits for `stream`
  * and copies a few bytes of the plan to the host (call once per plan, not per step). */
@@ -139,10 +155,13 @@ int hmm355_viterbi_plan_f32(const float* obs, int obs_mode, const float* log_P, 
                             const void* plan, int B, int T, int N, int64_t* states,
                             float* log_delta, float* final_score, void* workspace,
                             size_t workspace_bytes, void* stream);
-/* Viterbi with flags.  HMM355_VIT_PLAN_BANDED: the caller read hmm355_plan_banded(plan) == 1
- * for this plan.  The chain kernel then finishes the decode itself (chunk maps composed while
- * the chain runs, the backtrace after it: one launch instead of three) when N > 64 and
- * T <= 262144; otherwise the flag is ignored.  Passing the flag with a plan that is not banded
+/* Viterbi with flags.  HMM355_VIT_PLAN_BANDED: the caller read hmm355_plan_banded(plan) == 1 for
+ * this plan.  For N > 64 the decode then finishes inside the chain's own launch (csrc/follow.h):
+ * one extra workgroup per sequence forms log(x + 1e-8) of the emissions ahead of the chain
+ * (OBS_PROB), composes the 64-step chunk maps from the psi rows the chain publishes, and
+ * backtraces the path once the chain is done -- one launch instead of four.  Ignored when the 2B
+ * workgroups would not fit the device at once or T exceeds what the follower's LDS holds
+ * (~32k steps at N <= 128, ~16k at N <= 256).  Passing the flag with a plan that is not banded
  * is a caller error: the states come back as -1 and the final score as NaN. */
 #define HMM355_VIT_PLAN_BANDED 0x1u
 /* HMM355_VIT_PLAN_DENSE: the caller read hmm355_plan_banded(plan) == 0.  Then, for N <= 128, the
@@ -150,27 +169,13 @@ int hmm355_viterbi_plan_f32(const float* obs, int obs_mode, const float* log_P, 
  * of the chain's own launch on the CUs the chain leaves idle (they follow the rows the chain
  * has flushed; a chunk they did not finish is computed by the pass after the chain, so the
  * result never depends on their timing).  Without the flag the pointers are computed after the
- * chain.  With HMM355_OBS_PROB the flag also forms log(x + 1e-8) in one full-tensor pass into
- * the workspace first (the dense chain's staging waves share their SIMDs with the chain and
- * would pay for the log on every step).  The flag with a banded plan only costs the idle launch
- * and that pass. */
+ * chain.  With HMM355_OBS_PROB the emissions' log(x + 1e-8) is formed in one full-tensor pass
+ * into the workspace first.  The flag with a banded plan only costs the idle launch. */
 #define HMM355_VIT_PLAN_DENSE 0x2u
 int hmm355_viterbi_plan_ex_f32(const float* obs, int obs_mode, const float* log_P, const float* init,
                                const void* plan, unsigned flags, int B, int T, int N, int64_t* states,
                                float* log_delta, float* final_score, void* workspace,
                                size_t workspace_bytes, void* stream);
-/* One time part of a Viterbi decode: trellis rows [q_lo, q_hi) (q_hi = 0: T), resuming from
- * row q_lo - 1 of log_delta written by the previous part.  Parts run in order on one stream
- * with the same workspace; the last part (q_hi == T) also forms the pointers and the path.
- * Then the emissions of rows >= q_hi need not exist until the part that reads them starts, so a
- * producer of the emissions (the GMM scorer, pytorch_hmm_amd/ops.py gmm_viterbi) runs ahead of
- * the chain on another stream.  q_lo a multiple of 64; a part (not the whole range) needs
- * HMM355_VIT_PLAN_DENSE with a dense plan, N <= 128 and HMM355_OBS_LOG (else HMM355_E_ARG).
- * Bit-identical to one hmm355_viterbi_plan_ex_f32 call. */
-int hmm355_viterbi_part_f32(const float* obs, int obs_mode, const float* log_P, const float* init,
-                            const void* plan, unsigned flags, int B, int T, int N, int q_lo, int q_hi,
-                            int64_t* states, float* log_delta, float* final_score, void* workspace,
-                            size_t workspace_bytes, void* stream);
 
 /* ---------------------------------------------------------------------------------
  * Viterbi.  Replaces HMMPyTorch.viterbi_decode (hmm.py:132-184) and
@@ -211,14 +216,6 @@ int hmm355_gmm_diag_logprob_f32(const float* x, const float* means, const float*
                                 const float* log_w, int B, int T, int D, int S, int C,
                                 int mix_lse, float* out, void* workspace,
                                 size_t workspace_bytes, void* stream);
-/* The same for the time slice [t0, t0 + L) of every sequence (x and out keep their (B,T,.)
- * shapes; other rows are not touched), for C in {1, 2, 4}: a producer of Viterbi time parts
- * (hmm355_viterbi_part_f32).  Bit-identical to the whole-tensor call on those rows. */
-int hmm355_gmm_diag_logprob_slice_f32(const float* x, const float* means, const float* log_vars,
-                                      const float* log_w, int B, int T, int D, int S, int C,
-                                      int mix_lse, int t0, int L, float* out, void* workspace,
-                                      size_t workspace_bytes, void* stream);
-
 /* ---------------------------------------------------------------------------------
  * HSMM segment Viterbi.  Replaces HSMMLayer.viterbi_decode_hsmm / _viterbi_decode_single
  * (hsmm.py:208-354), reproducing its candidate order (s' outer, d' inner, strict >), its
@@ -240,6 +237,17 @@ size_t hmm355_hsmm_workspace_bytes(int B, int T, int S, int Dmax);
 int hmm355_hsmm_viterbi_f32(const float* lp, const float* dur_lp, const float* log_T, int B,
                             int T, int S, int Dmax, int64_t* states, float* scores,
                             void* workspace, size_t workspace_bytes, void* stream);
+/* Kernel-form flags of the segment recursions (results are identical in every form; parity
+ * tests compare them):
+ *   HMM355_FORM_GENERAL      the general form (workspace tables) whatever the size
+ *   HMM355_FORM_SERIAL_WALK  HSMM only: the serial backtrace walk instead of the chunked one
+ * The _ex workspace queries take the same flags. */
+#define HMM355_FORM_GENERAL 0x1u
+#define HMM355_FORM_SERIAL_WALK 0x2u
+size_t hmm355_hsmm_workspace_bytes_ex(int B, int T, int S, int Dmax, unsigned flags);
+int hmm355_hsmm_viterbi_ex_f32(const float* lp, const float* dur_lp, const float* log_T, int B,
+                               int T, int S, int Dmax, unsigned flags, int64_t* states,
+                               float* scores, void* workspace, size_t workspace_bytes, void* stream);
 
 /* ---------------------------------------------------------------------------------
  * Recursions with one transition matrix per time step (NeuralHMM).  Replace
@@ -290,18 +298,6 @@ int hmm355_tv_viterbi_f32(const float* log_obs, const float* log_A, long long a_
                           long long a_tstride, const float* init, int B, int T, int N,
                           int64_t* states, float* log_delta, void* workspace,
                           size_t workspace_bytes, void* stream);
-/* Forward-backward AND Viterbi of the same time-varying model (NeuralHMM.forward +
- * viterbi_decode, neural.py:355-511) in one call: the alpha and Viterbi recursions run in one
- * workgroup per sequence and read each step's matrix once (the two calls above read it three
- * times in all).  Outputs and their bits as the two calls; no terminal vector (log_beta_T). */
-size_t hmm355_tv_fb_viterbi_workspace_bytes(int B, int T, int N);
-int hmm355_tv_fb_viterbi_f32(const float* log_obs, const float* log_A, long long a_bstride,
-                             long long a_tstride, const float* log_p0, const float* init, int B,
-                             int T, int N, unsigned out_mask, float* posterior, float* forward,
-                             float* backward, float* loglik, float* lik_ref, int64_t* states,
-                             float* log_delta, void* workspace, size_t workspace_bytes,
-                             void* stream);
-
 /* ---------------------------------------------------------------------------------
  * Explicit-duration (semi-Markov) HMM, indexed by segment END time.  Replace
  * SemiMarkovHMM.viterbi_decode (semi_markov.py:455-570), the segment observation score
@@ -347,6 +343,19 @@ int hmm355_semimarkov_forward_f32(const float* quad, const float* seg_const,
                                   const float* dur_lp, int B, int T, int S, int Dmax,
                                   float* log_alpha, float* log_prob, void* workspace,
                                   size_t workspace_bytes, void* stream);
+/* The same with kernel-form flags (HMM355_FORM_GENERAL). */
+size_t hmm355_semimarkov_workspace_bytes_ex(int B, int T, int S, int Dmax, unsigned flags);
+int hmm355_semimarkov_viterbi_ex_f32(const float* quad, const float* seg_const,
+                                     const float* log_init, const float* log_T,
+                                     const float* dur_lp, int B, int T, int S, int Dmax,
+                                     unsigned flags, int64_t* seg_states, int64_t* seg_durs,
+                                     int* seg_count, float* scores, void* workspace,
+                                     size_t workspace_bytes, void* stream);
+int hmm355_semimarkov_forward_ex_f32(const float* quad, const float* seg_const,
+                                     const float* log_init, const float* log_T,
+                                     const float* dur_lp, int B, int T, int S, int Dmax,
+                                     unsigned flags, float* log_alpha, float* log_prob,
+                                     void* workspace, size_t workspace_bytes, void* stream);
 
 /* ---------------------------------------------------------------------------------
  * Streaming decoders of StreamingHMMProcessor, one chunk of B independent streams.

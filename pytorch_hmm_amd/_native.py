@@ -15,26 +15,32 @@ OBS_PROB = 0
 OBS_LOG = 1
 FB_POSTERIOR = 1
 FB_PAIR = 0x100
+FB_PLAN_BANDED = 0x200  # HMM355_FB_PLAN_BANDED
 VIT_PLAN_BANDED = 0x1  # HMM355_VIT_PLAN_BANDED
 VIT_PLAN_DENSE = 0x2  # HMM355_VIT_PLAN_DENSE
+PLAN_DENSE = 0x1  # HMM355_PLAN_DENSE
+FORM_GENERAL = 0x1  # HMM355_FORM_GENERAL
+FORM_SERIAL_WALK = 0x2  # HMM355_FORM_SERIAL_WALK
 FB_FORWARD = 2
 FB_BACKWARD = 4
 
 # every symbol include/hmm355.h declares (checked by tests/test_native_abi.py)
 EXPORTS = (
     "hmm355_strerror", "hmm355_version",
-    "hmm355_fb_workspace_bytes", "hmm355_forward_backward_f32", "hmm355_forward_backward_ex_f32",
+    "hmm355_fb_workspace_bytes", "hmm355_fb_workspace_layout", "hmm355_forward_backward_f32",
+    "hmm355_forward_backward_ex_f32",
     "hmm355_viterbi_workspace_bytes", "hmm355_viterbi_f32",
     "hmm355_gmm_workspace_bytes", "hmm355_gmm_diag_logprob_f32",
-    "hmm355_hsmm_workspace_bytes", "hmm355_hsmm_viterbi_f32",
+    "hmm355_hsmm_workspace_bytes", "hmm355_hsmm_viterbi_f32", "hmm355_hsmm_workspace_bytes_ex",
+    "hmm355_hsmm_viterbi_ex_f32",
     "hmm355_tv_fb_workspace_bytes", "hmm355_tv_forward_backward_f32", "hmm355_tv_forward_backward_ex_f32",
     "hmm355_tv_viterbi_workspace_bytes", "hmm355_tv_viterbi_f32",
-    "hmm355_tv_fb_viterbi_workspace_bytes", "hmm355_tv_fb_viterbi_f32",
     "hmm355_semimarkov_workspace_bytes", "hmm355_semimarkov_quad_f32",
-    "hmm355_semimarkov_viterbi_f32", "hmm355_semimarkov_forward_f32",
+    "hmm355_semimarkov_viterbi_f32", "hmm355_semimarkov_forward_f32", "hmm355_semimarkov_workspace_bytes_ex",
+    "hmm355_semimarkov_viterbi_ex_f32", "hmm355_semimarkov_forward_ex_f32",
     "hmm355_stream_greedy_f32", "hmm355_stream_beam_f32",
-    "hmm355_plan_bytes", "hmm355_plan_f32", "hmm355_plan_banded", "hmm355_forward_backward_plan_f32", "hmm355_viterbi_plan_f32",
-    "hmm355_viterbi_plan_ex_f32", "hmm355_viterbi_part_f32", "hmm355_gmm_diag_logprob_slice_f32",
+    "hmm355_plan_bytes", "hmm355_plan_f32", "hmm355_plan_ex_f32", "hmm355_plan_banded",
+    "hmm355_forward_backward_plan_f32", "hmm355_viterbi_plan_f32", "hmm355_viterbi_plan_ex_f32",
     "hmm355_fb_adjoint_f32", "hmm355_tv_fb_adjoint_f32",
 )
 
@@ -59,6 +65,7 @@ def lib():
     L.hmm355_strerror.argtypes, L.hmm355_strerror.restype = [I], ctypes.c_char_p
     L.hmm355_version.argtypes, L.hmm355_version.restype = [], I
     L.hmm355_fb_workspace_bytes.argtypes, L.hmm355_fb_workspace_bytes.restype = [I, I, I], S
+    L.hmm355_fb_workspace_layout.argtypes, L.hmm355_fb_workspace_layout.restype = [I, I, I, P], I
     L.hmm355_forward_backward_f32.argtypes = [P, I, P, P, I, I, I, U, P, P, P, P, P, P, S, P]
     L.hmm355_forward_backward_f32.restype = I
     L.hmm355_forward_backward_ex_f32.argtypes = [P, I, P, P, P, I, I, I, U, P, P, P, P, P, P, S, P]
@@ -72,6 +79,9 @@ def lib():
     L.hmm355_hsmm_workspace_bytes.argtypes, L.hmm355_hsmm_workspace_bytes.restype = [I, I, I, I], S
     L.hmm355_hsmm_viterbi_f32.argtypes = [P, P, P, I, I, I, I, P, P, P, S, P]
     L.hmm355_hsmm_viterbi_f32.restype = I
+    L.hmm355_hsmm_workspace_bytes_ex.argtypes, L.hmm355_hsmm_workspace_bytes_ex.restype = [I, I, I, I, U], S
+    L.hmm355_hsmm_viterbi_ex_f32.argtypes = [P, P, P, I, I, I, I, U, P, P, P, S, P]
+    L.hmm355_hsmm_viterbi_ex_f32.restype = I
     LL = ctypes.c_longlong
     L.hmm355_tv_fb_workspace_bytes.argtypes, L.hmm355_tv_fb_workspace_bytes.restype = [I, I, I], S
     L.hmm355_tv_forward_backward_f32.argtypes = [P, P, LL, LL, P, I, I, I, U, P, P, P, P, P, P, S, P]
@@ -80,10 +90,6 @@ def lib():
     L.hmm355_tv_forward_backward_ex_f32.restype = I
     L.hmm355_tv_viterbi_workspace_bytes.argtypes, L.hmm355_tv_viterbi_workspace_bytes.restype = [I, I, I], S
     L.hmm355_tv_viterbi_f32.argtypes = [P, P, LL, LL, P, I, I, I, P, P, P, S, P]
-    L.hmm355_tv_fb_viterbi_workspace_bytes.argtypes = [I, I, I]
-    L.hmm355_tv_fb_viterbi_workspace_bytes.restype = S
-    L.hmm355_tv_fb_viterbi_f32.argtypes = [P, P, LL, LL, P, P, I, I, I, U, P, P, P, P, P, P, P, P, S, P]
-    L.hmm355_tv_fb_viterbi_f32.restype = I
     L.hmm355_tv_viterbi_f32.restype = I
     L.hmm355_semimarkov_workspace_bytes.argtypes = [I, I, I, I]
     L.hmm355_semimarkov_workspace_bytes.restype = S
@@ -92,9 +98,16 @@ def lib():
     L.hmm355_semimarkov_viterbi_f32.restype = I
     L.hmm355_semimarkov_forward_f32.argtypes = [P, P, P, P, P, I, I, I, I, P, P, P, S, P]
     L.hmm355_semimarkov_forward_f32.restype = I
+    L.hmm355_semimarkov_workspace_bytes_ex.argtypes = [I, I, I, I, U]
+    L.hmm355_semimarkov_workspace_bytes_ex.restype = S
+    L.hmm355_semimarkov_viterbi_ex_f32.argtypes = [P, P, P, P, P, I, I, I, I, U, P, P, P, P, P, S, P]
+    L.hmm355_semimarkov_viterbi_ex_f32.restype = I
+    L.hmm355_semimarkov_forward_ex_f32.argtypes = [P, P, P, P, P, I, I, I, I, U, P, P, P, S, P]
+    L.hmm355_semimarkov_forward_ex_f32.restype = I
     F = ctypes.c_float
     L.hmm355_plan_bytes.argtypes, L.hmm355_plan_bytes.restype = [I], S
     L.hmm355_plan_f32.argtypes, L.hmm355_plan_f32.restype = [P, I, P, P], I
+    L.hmm355_plan_ex_f32.argtypes, L.hmm355_plan_ex_f32.restype = [P, I, U, P, P], I
     L.hmm355_plan_banded.argtypes, L.hmm355_plan_banded.restype = [P, P], I
     L.hmm355_forward_backward_plan_f32.argtypes = [P, I, P, P, P, P, I, I, I, U, P, P, P, P, P, P, S, P]
     L.hmm355_forward_backward_plan_f32.restype = I
@@ -102,10 +115,6 @@ def lib():
     L.hmm355_viterbi_plan_f32.restype = I
     L.hmm355_viterbi_plan_ex_f32.argtypes = [P, I, P, P, P, U, I, I, I, P, P, P, P, S, P]
     L.hmm355_viterbi_plan_ex_f32.restype = I
-    L.hmm355_viterbi_part_f32.argtypes = [P, I, P, P, P, U, I, I, I, I, I, P, P, P, P, S, P]
-    L.hmm355_viterbi_part_f32.restype = I
-    L.hmm355_gmm_diag_logprob_slice_f32.argtypes = [P, P, P, P, I, I, I, I, I, I, I, I, P, P, S, P]
-    L.hmm355_gmm_diag_logprob_slice_f32.restype = I
     L.hmm355_stream_greedy_f32.argtypes, L.hmm355_stream_greedy_f32.restype = [P, P, P, F, I, I, I, P, P, P], I
     L.hmm355_stream_beam_f32.argtypes = [P, P, I, I, I, I, I, P, P, P, P, P, P, P, P]
     L.hmm355_stream_beam_f32.restype = I

@@ -40,6 +40,17 @@ def _pad(N):
     return 64 if N <= 64 else (128 if N <= 128 else 256)
 
 
+FB_PIECES = ("U", "V", "LA", "LB", "band", "binit", "bscale", "rmax", "CA", "CB")
+
+
+def fb_layout(B, T, N):
+    """{piece: byte offset} of the forward-backward workspace (hmm355_fb_workspace_layout)."""
+    import ctypes
+    out = (ctypes.c_size_t * len(FB_PIECES))()
+    nat.check(nat.lib().hmm355_fb_workspace_layout(B, T, N, out))
+    return dict(zip(FB_PIECES, out))
+
+
 def _run_fb(obs, log_P, log_p0, obs_mode, log_beta_T=None, posterior=False, out_mask=None, plan=None):
     """One hmm355_forward_backward_plan_f32 call; returns (posterior|None, loglik, lik_ref, U, V,
     LA, LB), or with `out_mask` ((posterior, forward, backward) per the mask, loglik, lik_ref, U,
@@ -60,19 +71,16 @@ def _run_fb(obs, log_P, log_p0, obs_mode, log_beta_T=None, posterior=False, out_
             mask, nat.ptr(post), nat.ptr(fwd), nat.ptr(bwd), nat.ptr(loglik), nat.ptr(lik_ref),
             nat.ptr(ws), ws.numel(), nat.stream_of(dev)))
     rows = B * T
-    # workspace layout (hmm355.h): U | V (B,T,NP) | LA | LB (B,T) | BandDesc | (B,NP) | (B) |
-    # (B,T) | CA | CB (B,T), pieces 256-B aligned
-    al = lambda n: ((n + 255) // 256) * 256
+    # the workspace pieces, at the offsets the library reports (hmm355_fb_workspace_layout)
+    o = fb_layout(B, T, N)
     fl = ws.view(torch.float32)
-    U = fl[: rows * NP].view(B, T, NP)[..., :N]
-    V = fl[rows * NP: 2 * rows * NP].view(B, T, NP)[..., :N]
-    off = al(2 * rows * NP * 4) // 4
-    LA = fl[off: off + rows].view(B, T)
-    LB = fl[off + rows: off + 2 * rows].view(B, T)
-    offc = (al(2 * rows * NP * 4) + al(2 * rows * 4) + al(L.hmm355_plan_bytes(N)) + al(B * NP * 4) + al(B * 4)
-            + al(rows * 4)) // 4
-    CA = fl[offc: offc + rows].view(B, T)
-    CB = fl[offc + rows: offc + 2 * rows].view(B, T)
+    piece = lambda name, n: fl[o[name] // 4: o[name] // 4 + n]
+    U = piece("U", rows * NP).view(B, T, NP)[..., :N]
+    V = piece("V", rows * NP).view(B, T, NP)[..., :N]
+    LA = piece("LA", rows).view(B, T)
+    LB = piece("LB", rows).view(B, T)
+    CA = piece("CA", rows).view(B, T)
+    CB = piece("CB", rows).view(B, T)
     if out_mask is not None:
         return (post, fwd, bwd), loglik, lik_ref, U, V, LA, LB, CA, CB
     return post, loglik, lik_ref, U, V, LA, LB, CA, CB
@@ -93,19 +101,19 @@ class SequenceLogLik(torch.autograd.Function):
     log_P and log_p0."""
 
     @staticmethod
-    def forward(ctx, obs, log_P, log_p0, obs_mode, kind):
+    def forward(ctx, obs, log_P, log_p0, obs_mode, kind, plan=None):
         nat.require_gpu(obs, log_P, log_p0)
         obs_c, lP, l0 = (t.detach().to(torch.float32).contiguous() for t in (obs, log_P, log_p0))
-        _, loglik, lik_ref, *_ = _run_fb(obs_c, lP, l0, obs_mode)
+        _, loglik, lik_ref, *_ = _run_fb(obs_c, lP, l0, obs_mode, plan=plan)
         ctx.save_for_backward(obs_c, lP, l0)
-        ctx.obs_mode, ctx.kind = obs_mode, kind
+        ctx.obs_mode, ctx.kind, ctx.plan = obs_mode, kind, plan
         return lik_ref if kind == "ref" else loglik
 
     @staticmethod
     def backward(ctx, gout):
         obs, lP, l0 = ctx.saved_tensors
         B, T, N = obs.shape
-        _, _, _, U, _, LA, _, _, _ = _run_fb(obs, lP, l0, ctx.obs_mode)
+        _, _, _, U, _, LA, _, _, _ = _run_fb(obs, lP, l0, ctx.obs_mode, plan=ctx.plan)
         a_last = torch.log(U[:, -1]) + LA[:, -1:]                 # log alpha_{T-1}  (B,N)
         if ctx.kind == "ref":
             f = torch.exp(a_last)                                 # the reference's forward[:, -1]
@@ -118,7 +126,7 @@ class SequenceLogLik(torch.autograd.Function):
             log_mu = torch.zeros_like(a_last)
         G = g.sum(-1) * gout                                      # (B,)
         post, _, _, U, V, _, _, CA, _ = _run_fb(obs, lP, l0, ctx.obs_mode, log_beta_T=log_mu.contiguous(),
-                                         posterior=True)
+                                                posterior=True, plan=ctx.plan)
         grad_lo = G[:, None, None] * post
         if ctx.obs_mode == nat.OBS_PROB:
             grad_obs = grad_lo / (obs + 1e-8)
@@ -139,7 +147,7 @@ class SequenceLogLik(torch.autograd.Function):
             Y = e[:, 1:] * V[:, 1:]
             M = torch.einsum("bti,btj->ij", X, Y)
             grad_lP = torch.exp(lP) * M
-        return grad_obs, grad_lP, grad_l0, None, None
+        return grad_obs, grad_lP, grad_l0, None, None, None
 
 
 def _run_tv_fb(log_obs, A, sb, st, log_p0, log_beta_T=None, posterior=False, out_mask=None):

@@ -230,16 +230,15 @@ static __global__ void __launch_bounds__(kPrepThreads) band_prep_kernel(const fl
   }
 }
 
-// HMM355_DENSE=1 in the environment disables the banded chains (read per call; parity
-// tests compare the two paths on the same inputs).
-inline bool use_band() {
-  const char* e = getenv("HMM355_DENSE");
-  return !(e && e[0] == '1');
-}
-
-inline hipError_t launch_band_prep(const float* log_P, int N, BandDesc* d, hipStream_t st) {
+// force_dense (a plan made with HMM355_PLAN_DENSE): both window widths are set beyond kBandMax
+// after the measurement, so every recursion of that plan takes the dense chains (parity tests
+// compare the two paths on the same inputs; the plan's tables are left as measured).
+inline hipError_t launch_band_prep(const float* log_P, int N, BandDesc* d, hipStream_t st, bool force_dense = false) {
   hipLaunchKernelGGL(band_prep_kernel, dim3(1), dim3(kPrepThreads), 0, st, log_P, N, d);
-  return hipGetLastError();
+  hipError_t e = hipGetLastError();
+  if (e == hipSuccess && force_dense)
+    e = hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(d), 0x7fffffff, 2, st);  // wc, wr
+  return e;
 }
 
 }  // namespace hmm355

@@ -210,8 +210,25 @@ inline hipError_t allow_lds(K kernel, size_t bytes) {
 
 constexpr size_t kExclusiveLds = 160 * 1024;  // a workgroup that owns its CU
 
+// ---- hand-offs between workgroups of one launch (MI355X_MICROARCH.md, inter-workgroup
+// visibility; cdna_hip_programming.md Guideline 16, R1): payload stored write-through (sc1),
+// every storing wave's stores complete before a workgroup barrier, then ONE lane stores the
+// count (relaxed, agent scope: an sc1 store); the consumer polls the count relaxed and loads the
+// payload with sc1 loads only (no L1 copy can be stale), so neither side needs a fence.
+typedef unsigned u32x4_t __attribute__((ext_vector_type(4)));
+constexpr int kAuxSc1 = 16;  // buffer instruction cache-policy bits: sc1
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* p, size_t bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, (int)bytes, 0x00020000);
+}
+__device__ __forceinline__ int poll_count(const int* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void publish_count(int* p, int v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 inline int pad_states(int N) { return N <= 64 ? 64 : (N <= 128 ? 128 : 256); }
 
-inline size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
+__host__ __device__ inline size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
 
 }  // namespace hmm355

@@ -22,6 +22,8 @@
 //   posterior = (u*v)/sum(u*v) (scale-invariant) and the reference's compute_likelihood value
 //   (forward = exp(log u + LA) and backward = exp(log v + LB) are written by kernel 1's flushes)
 //   logsumexp_j(log(forward_{T-1}[j] + 1e-8)) (hmm.py:206) for t = T-1.
+#include <atomic>
+
 #include "recur.h"
 #include "post.h"
 #include "fbpair.h"
@@ -56,6 +58,7 @@ __global__ void __launch_bounds__(256) row_max_kernel(const float* __restrict__ 
 struct FbWs {
   float *U, *V, *LA, *LB, *binit, *bscale, *rmax, *CA, *CB;
   BandDesc* band;
+  int* pub;  // (2B) the chains' published block counts (posterior followers, follow.h)
 };
 static size_t fb_ws_layout(int B, int T, int N, char* base, FbWs* w) {
   const size_t NP = pad_states(N);
@@ -69,6 +72,7 @@ static size_t fb_ws_layout(int B, int T, int N, char* base, FbWs* w) {
   const size_t oS = take((size_t)B * sizeof(float));
   const size_t oM = take(rows * sizeof(float));
   const size_t oC = take(2 * rows * sizeof(float));
+  const size_t oP = take(align_up((size_t)2 * B * sizeof(int), 16));
   if (w && base) {
     w->U = reinterpret_cast<float*>(base + oU);
     w->V = w->U + rows * NP;
@@ -80,8 +84,22 @@ static size_t fb_ws_layout(int B, int T, int N, char* base, FbWs* w) {
     w->rmax = reinterpret_cast<float*>(base + oM);
     w->CA = reinterpret_cast<float*>(base + oC);
     w->CB = w->CA + rows;
+    w->pub = reinterpret_cast<int*>(base + oP);
   }
   return off;
+}
+
+// CUs of the current device, queried once per device (a relaxed atomic per slot)
+static int fb_device_cus() {
+  static std::atomic<int> cus[64];
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 0;
+  int n = cus[dev].load(std::memory_order_relaxed);
+  if (n == 0) {
+    if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0) n = -1;
+    cus[dev].store(n, std::memory_order_relaxed);
+  }
+  return n > 0 ? n : 0;
 }
 
 }  // namespace hmm355
@@ -93,13 +111,29 @@ HMM355_API size_t hmm355_fb_workspace_bytes(int B, int T, int N) {
   return fb_ws_layout(B, T, N, nullptr, nullptr);
 }
 
+HMM355_API int hmm355_fb_workspace_layout(int B, int T, int N, size_t* offsets) {
+  if (B < 0 || T < 1 || N < 1 || N > 256) return HMM355_E_SHAPE;
+  if (!offsets) return HMM355_E_ARG;
+  FbWs w;
+  char* base = reinterpret_cast<char*>((uintptr_t)1 << 20);  // any 256-B aligned base: offsets only
+  fb_ws_layout(B, T, N, base, &w);
+  const void* piece[10] = {w.U, w.V, w.LA, w.LB, w.band, w.binit, w.bscale, w.rmax, w.CA, w.CB};
+  for (int i = 0; i < 10; ++i) offsets[i] = (size_t)(reinterpret_cast<const char*>(piece[i]) - base);
+  return HMM355_OK;
+}
+
 HMM355_API size_t hmm355_plan_bytes(int N) { return (N >= 1 && N <= 256) ? sizeof(BandDesc) : 0; }
 
-HMM355_API int hmm355_plan_f32(const float* log_P, int N, void* plan, void* stream) {
+HMM355_API int hmm355_plan_ex_f32(const float* log_P, int N, unsigned flags, void* plan, void* stream) {
   if (N < 1 || N > 256) return HMM355_E_STATES;
-  if (!log_P || !plan) return HMM355_E_ARG;
-  const hipError_t e = launch_band_prep(log_P, N, static_cast<BandDesc*>(plan), static_cast<hipStream_t>(stream));
+  if (!log_P || !plan || (flags & ~HMM355_PLAN_DENSE)) return HMM355_E_ARG;
+  const hipError_t e = launch_band_prep(log_P, N, static_cast<BandDesc*>(plan), static_cast<hipStream_t>(stream),
+                                        (flags & HMM355_PLAN_DENSE) != 0);
   return e == hipSuccess ? HMM355_OK : (int)e;
+}
+
+HMM355_API int hmm355_plan_f32(const float* log_P, int N, void* plan, void* stream) {
+  return hmm355_plan_ex_f32(log_P, N, 0u, plan, stream);
 }
 
 HMM355_API int hmm355_plan_banded(const void* plan, void* stream) {
@@ -130,7 +164,7 @@ HMM355_API int hmm355_forward_backward_plan_f32(const float* obs, int obs_mode, 
   const int NP = pad_states(N);
   FbWs w;
   fb_ws_layout(B, T, N, static_cast<char*>(workspace), &w);
-  BandDesc* band = use_band() ? (plan ? static_cast<BandDesc*>(const_cast<void*>(plan)) : w.band) : nullptr;
+  BandDesc* band = plan ? static_cast<BandDesc*>(const_cast<void*>(plan)) : w.band;
   hipStream_t st = static_cast<hipStream_t>(stream);
   const float* binit = nullptr;
   const float* bscale = nullptr;
@@ -171,8 +205,16 @@ HMM355_API int hmm355_forward_backward_plan_f32(const float* obs, int obs_mode, 
   // LDS rows; the posterior pass then reads U / V and writes the posterior only
   fa.out_exp = (out_mask & HMM355_FB_FORWARD) ? forward : nullptr;
   fb.out_exp = (out_mask & HMM355_FB_BACKWARD) ? backward : nullptr;
+  // HMM355_FB_PLAN_BANDED (the caller read hmm355_plan_banded(plan) == 1): the posterior and the
+  // reference's likelihood are formed inside the chains' launch (follow.h) -- one follower
+  // workgroup per sequence beside the 2B chains, while all 3B fit the chip at once
+  if ((out_mask & HMM355_FB_PLAN_BANDED) && plan && (out_mask & HMM355_FB_POSTERIOR) && 3 * B <= fb_device_cus() &&
+      (size_t)T * NP * 4 < ((size_t)1 << 31)) {
+    fa.pub = fb.pub = w.pub;
+    fa.lik_ref = lik_ref;
+  }
   PostArgs pa{w.U, w.V, w.LA, w.LB, posterior, forward, backward, lik_ref, B, T, N,
-              out_mask & ~(HMM355_FB_FORWARD | HMM355_FB_BACKWARD)};
+              out_mask & (HMM355_FB_POSTERIOR)};
   hipError_t e;
   switch (NP) {
     case 64: e = launch_fb<64>(fa, fb, pa, plan == nullptr, st); break;

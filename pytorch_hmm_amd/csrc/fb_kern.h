@@ -4,13 +4,20 @@
 #include "recur.h"
 #include "post.h"
 #include "fbpair.h"
+#include "follow.h"
 
 namespace hmm355 {
 
 
+// blockIdx.x = 2b + direction: the chains; with publishing chains (fa.pub) blockIdx.x = 2B + b
+// is sequence b's posterior follower (follow.h)
 template <int NP>
-__global__ void __launch_bounds__(kFbNT<NP>) fb_recur_kernel(RecArgs fa, RecArgs fb) {
+__global__ void __launch_bounds__(kFbNT<NP>) fb_recur_kernel(RecArgs fa, RecArgs fb, float* posterior) {
   extern __shared__ __attribute__((aligned(16))) float lds[];
+  if ((int)blockIdx.x >= 2 * fa.B) {
+    fb_post_follow<NP>(fa, fb, posterior, (int)blockIdx.x - 2 * fa.B, lds);
+    return;
+  }
   const int b = blockIdx.x >> 1;
   if (blockIdx.x & 1) {
     if (!(kAbl & (1 << 20))) rec_dispatch<NP, kFbBeta>(fb, lds, b);  // diagnostic: alpha only
@@ -27,7 +34,14 @@ hipError_t launch_fb(const RecArgs& fa, const RecArgs& fb, const PostArgs& pa, b
     e = launch_band_prep(fa.mat, fa.N, const_cast<BandDesc*>(fa.band), st);
     if (e != hipSuccess) return e;
   }
-  hipLaunchKernelGGL(fb_recur_kernel<NP>, dim3(2 * fa.B), dim3(kFbNT<NP>), kExclusiveLds, st, fa, fb);
+  if (fa.pub) {
+    // posterior followers beside the banded chains (follow.h): 2B chains + B followers, no pass after
+    e = hipMemsetAsync(fa.pub, 0, align_up((size_t)2 * fa.B * sizeof(int), 16), st);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(fb_recur_kernel<NP>, dim3(3 * fa.B), dim3(kFbNT<NP>), kExclusiveLds, st, fa, fb, pa.posterior);
+    return hipGetLastError();
+  }
+  hipLaunchKernelGGL(fb_recur_kernel<NP>, dim3(2 * fa.B), dim3(kFbNT<NP>), kExclusiveLds, st, fa, fb, pa.posterior);
   e = hipGetLastError();
   if (e != hipSuccess) return e;
   const size_t rows = (size_t)pa.B * pa.T;

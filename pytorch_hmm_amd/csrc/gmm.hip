@@ -423,8 +423,12 @@ static int gmm_v2_group(size_t P) { return P > 128 ? 256 : (P > 64 ? 128 : 64); 
 // scorer runs (it needs the fp64 frame tiles in the workspace: the size query and the launch
 // read the same variable)
 static int gmm_cfg() {
-  const char* ev = getenv("HMM355_GMM_CFG");
+#ifdef HMM355_DIAG
+  const char* ev = getenv("HMM355_GMM_CFG");  // (diagnostic builds only)
   return ev ? atoi(ev) : -1;
+#else
+  return -1;
+#endif
 }
 static bool gmm_use_v1(int C) { return !gmm_v2(C) || gmm_cfg() == 0; }
 static size_t gmm_ws_layout(int B, int T, int D, int S, int C, char* base, GmmWs* w) {
@@ -467,14 +471,6 @@ HMM355_API int hmm355_gmm_diag_logprob_f32(const float* x, const float* means, c
                                            const float* log_w, int B, int T, int D, int S, int C, int mix_lse,
                                            float* out, void* workspace, size_t workspace_bytes, void* stream) {
   return gmm_run(x, means, log_vars, log_w, B, T, D, S, C, mix_lse, 0, T, out, workspace, workspace_bytes, stream);
-}
-
-HMM355_API int hmm355_gmm_diag_logprob_slice_f32(const float* x, const float* means, const float* log_vars,
-                                                 const float* log_w, int B, int T, int D, int S, int C, int mix_lse,
-                                                 int t0, int L, float* out, void* workspace, size_t workspace_bytes,
-                                                 void* stream) {
-  if (t0 < 0 || L < 1 || t0 + L > T || !gmm_v2(C) || gmm_cfg() == 0) return HMM355_E_ARG;
-  return gmm_run(x, means, log_vars, log_w, B, T, D, S, C, mix_lse, t0, L, out, workspace, workspace_bytes, stream);
 }
 
 static int gmm_run(const float* x, const float* means, const float* log_vars, const float* log_w, int B, int T,

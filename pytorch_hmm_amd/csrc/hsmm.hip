@@ -754,10 +754,14 @@ __global__ void __launch_bounds__(64) hsmm_backtrace_kernel(HsArgs a) {
 //   profiles/r3u_warm.log.)
 constexpr int kHsChunk = 64;
 constexpr int kHsWarmMax = 256;
-inline int hsmm_warm() {  // frames walked above a chunk before it (HMM355_HSMM_WARM, diagnostic)
-  const char* e = getenv("HMM355_HSMM_WARM");
+inline int hsmm_warm() {  // frames walked above a chunk before it
+#ifdef HMM355_DIAG
+  const char* e = getenv("HMM355_HSMM_WARM");  // (diagnostic builds only)
   const int w = e ? atoi(e) : 128;
   return w < 0 ? 0 : (w > kHsWarmMax ? kHsWarmMax : w);
+#else
+  return 128;
+#endif
 }
 constexpr int kHsCap = kHsChunk + kHsWarmMax + 2;  // segments per record (each >= 1 frame)
 struct HsChunks {
@@ -935,19 +939,14 @@ __global__ void __launch_bounds__(64) hsmm_stitch_kernel(HsArgs a, HsChunks c) {
 
 // Geometries (S <= SMAX, Dmax < R).  The config-5 class S <= 64, Dmax <= 63 takes the
 // 4-lane form (256 threads: one wave per SIMD, 16 slots per lane; 0.81 ms at config 5 vs 0.83
-// for 8 lanes and 1.00 for 16, profiles/r3q_c5_sub*.log) unless HMM355_HSMM_SUB=8 or =16
-// asks for another.  The larger geometries run 512 threads (8 waves) so a lane has 256 VGPRs
-// for its 16 slots.  (S <= 128 with 64 <= Dmax <= 127 would need 32 slots per lane: beyond
-// the register file; rejected.)
-enum HsCfg : int { kHs16x4 = 0, kHs8x8s64 = 1, kHs8x16 = 2, kHs4x16 = 3, kHs4x16s64 = 4, kHsNone = -1 };
+// for 8 lanes and 1.00 for 16, profiles/r3q_c5_sub*.log: those two geometries were removed in
+// round 6).  The larger geometries run 512 threads (8 waves) so a lane has 256 VGPRs for its
+// 16 slots.  (S <= 128 with 64 <= Dmax <= 127 would need 32 slots per lane: beyond the register
+// file; rejected.)
+enum HsCfg : int { kHs8x16 = 2, kHs4x16 = 3, kHs4x16s64 = 4, kHsNone = -1 };
 inline int hsmm_cfg(int S, int Dm) {
   if (S < 1 || Dm < 1) return kHsNone;
-  if (S <= 64 && Dm < 64) {
-    const char* e = getenv("HMM355_HSMM_SUB");
-    if (e && e[0] == '1' && e[1] == '6') return kHs16x4;
-    if (e && e[0] == '8') return kHs8x8s64;
-    return kHs4x16s64;
-  }
+  if (S <= 64 && Dm < 64) return kHs4x16s64;
   // Dm <= 71: from 72 frames on torch's cascade step changes the segment-sum order (tsum.h);
   // its extra per-slot accumulators do not fit this geometry's registers (measured: 189 VGPRs
   // spilled), so longer durations take the general form (hsmm_wide.hip), which has it
@@ -957,14 +956,13 @@ inline int hsmm_cfg(int S, int Dm) {
 }
 
 inline int hsmm_chunks(int T) { return (T + kHsChunk - 1) / kHsChunk; }
-// the chunked backtrace from 3 chunks up (HMM355_HSMM_SERIAL=1: always the serial walk)
-inline bool hsmm_use_chunks(int T) {
-  const char* e = getenv("HMM355_HSMM_SERIAL");
-  return hsmm_chunks(T) >= 3 && !(e && e[0] == '1');
+// the chunked backtrace from 3 chunks up (HMM355_FORM_SERIAL_WALK: always the serial walk)
+inline bool hsmm_use_chunks(int T, unsigned flags) {
+  return hsmm_chunks(T) >= 3 && !(flags & HMM355_FORM_SERIAL_WALK);
 }
 
 template <int SUB, int NJ, int SMAX>
-static hipError_t launch_hsmm(const HsArgs& ha, const HsChunks& hc, hipStream_t st) {
+static hipError_t launch_hsmm(const HsArgs& ha, const HsChunks& hc, unsigned flags, hipStream_t st) {
   using G = HsG<SUB, NJ, SMAX>;
   const size_t lds = sizeof(HsLds<SMAX, G::DW>);
   hipError_t e = allow_lds(hsmm_fwd_kernel<SUB, NJ, SMAX>, lds);
@@ -974,7 +972,7 @@ static hipError_t launch_hsmm(const HsArgs& ha, const HsChunks& hc, hipStream_t 
   if (e != hipSuccess) return e;
   if constexpr (kAbl & (1 << 22)) return hipSuccess;  // ablation: forward only (timing)
   const size_t blds = hsmm_walk_lds(ha.S, ha.Dm, G::R);
-  if (hsmm_use_chunks(ha.T)) {
+  if (hsmm_use_chunks(ha.T, flags)) {
     const size_t wlds = align16(blds) + kHsCap * sizeof(int4);
     if ((e = allow_lds(hsmm_chunk_walk_kernel<G::R, SMAX>, wlds)) != hipSuccess) return e;
     HsChunks hs = hc;
@@ -1013,10 +1011,9 @@ size_t hsmm_wide_workspace_bytes(int B, int T, int S, int Dm);
 bool hsmm_wide_fits(int S, int Dm);
 hipError_t launch_hsmm_wide(const float* lp, const float* dur, const float* logT, int B, int T, int S, int Dm,
                             int64_t* states, float* scores, void* workspace, hipStream_t st);
-// HMM355_HSMM_WIDE=1 takes the general form for every size (tests / comparison)
-inline bool hsmm_wide(int S, int Dm) {
-  const char* e = getenv("HMM355_HSMM_WIDE");
-  return hsmm_wide_fits(S, Dm) && (hsmm_cfg(S, Dm) == kHsNone || (e && e[0] == '1'));
+// HMM355_FORM_GENERAL takes the general form for every size (tests / comparison)
+inline bool hsmm_wide(int S, int Dm, unsigned flags) {
+  return hsmm_wide_fits(S, Dm) && (hsmm_cfg(S, Dm) == kHsNone || (flags & HMM355_FORM_GENERAL));
 }
 
 }  // namespace hmm355
@@ -1032,18 +1029,23 @@ HMM355_API int hmm355_diag_hsmm_stamp(unsigned long long* out) {
 }
 #endif
 
-HMM355_API size_t hmm355_hsmm_workspace_bytes(int B, int T, int S, int Dmax) {
+HMM355_API size_t hmm355_hsmm_workspace_bytes_ex(int B, int T, int S, int Dmax, unsigned flags) {
   if (B < 0 || T < 1) return 0;
-  if (hsmm_wide(S, Dmax)) return hsmm_wide_workspace_bytes(B, T, S, Dmax);
+  if (hsmm_wide(S, Dmax, flags)) return hsmm_wide_workspace_bytes(B, T, S, Dmax);
   if (hsmm_cfg(S, Dmax) == kHsNone) return 0;
   const size_t n = (size_t)B * T * S, nc = (size_t)B * hsmm_chunks(T);
   return 2 * align_up(n * 4, 256) + align_up((size_t)B * 8, 256) + align_up(nc * kHsCap * sizeof(int4), 256) +
          align_up((nc + B) * 4, 256);
 }
 
-HMM355_API int hmm355_hsmm_viterbi_f32(const float* lp, const float* dur_lp, const float* log_T, int B, int T,
-                                       int S, int Dmax, int64_t* states, float* scores, void* workspace,
-                                       size_t workspace_bytes, void* stream) {
+HMM355_API size_t hmm355_hsmm_workspace_bytes(int B, int T, int S, int Dmax) {
+  return hmm355_hsmm_workspace_bytes_ex(B, T, S, Dmax, 0u);
+}
+
+HMM355_API int hmm355_hsmm_viterbi_ex_f32(const float* lp, const float* dur_lp, const float* log_T, int B, int T,
+                                          int S, int Dmax, unsigned flags, int64_t* states, float* scores,
+                                          void* workspace, size_t workspace_bytes, void* stream) {
+  if (flags & ~(HMM355_FORM_GENERAL | HMM355_FORM_SERIAL_WALK)) return HMM355_E_ARG;
   if (B < 0 || S < 0 || Dmax < 0) return HMM355_E_ARG;
   if (S < 1 || S > 1024) return HMM355_E_STATES;
   if (Dmax < 1 || Dmax > 1024) return HMM355_E_DURATION;
@@ -1051,8 +1053,8 @@ HMM355_API int hmm355_hsmm_viterbi_f32(const float* lp, const float* dur_lp, con
   if (B == 0) return HMM355_OK;
   if (!lp || !dur_lp || !log_T || !states || !scores || !workspace) return HMM355_E_ARG;
   if ((size_t)B * T * S * Dmax > ((size_t)1 << 40)) return HMM355_E_SHAPE;
-  if (workspace_bytes < hmm355_hsmm_workspace_bytes(B, T, S, Dmax)) return HMM355_E_WORKSPACE;
-  if (hsmm_wide(S, Dmax) && S > 1) {
+  if (workspace_bytes < hmm355_hsmm_workspace_bytes_ex(B, T, S, Dmax, flags)) return HMM355_E_WORKSPACE;
+  if (hsmm_wide(S, Dmax, flags) && S > 1) {
     const hipError_t e = launch_hsmm_wide(lp, dur_lp, log_T, B, T, S, Dmax, states, scores, workspace,
                                           static_cast<hipStream_t>(stream));
     return e == hipSuccess ? HMM355_OK : (int)e;
@@ -1078,11 +1080,16 @@ HMM355_API int hmm355_hsmm_viterbi_f32(const float* lp, const float* dur_lp, con
   // reference's torch.zeros initial value (hsmm.py:332)
   if ((e = hipMemsetAsync(states, 0, (size_t)B * T * sizeof(int64_t), st)) != hipSuccess) return (int)e;
   switch (hsmm_cfg(S, Dmax)) {
-    case kHs16x4: e = launch_hsmm<16, 4, 64>(ha, hc, st); break;
-    case kHs8x8s64: e = launch_hsmm<8, 8, 64>(ha, hc, st); break;
-    case kHs4x16s64: e = launch_hsmm<4, 16, 64>(ha, hc, st); break;
-    case kHs8x16: e = launch_hsmm<8, 16, 64>(ha, hc, st); break;
-    default: e = launch_hsmm<4, 16, 128>(ha, hc, st); break;
+    case kHs4x16s64: e = launch_hsmm<4, 16, 64>(ha, hc, flags, st); break;
+    case kHs8x16: e = launch_hsmm<8, 16, 64>(ha, hc, flags, st); break;
+    default: e = launch_hsmm<4, 16, 128>(ha, hc, flags, st); break;
   }
   return e == hipSuccess ? HMM355_OK : (int)e;
+}
+
+HMM355_API int hmm355_hsmm_viterbi_f32(const float* lp, const float* dur_lp, const float* log_T, int B, int T,
+                                       int S, int Dmax, int64_t* states, float* scores, void* workspace,
+                                       size_t workspace_bytes, void* stream) {
+  return hmm355_hsmm_viterbi_ex_f32(lp, dur_lp, log_T, B, T, S, Dmax, 0u, states, scores, workspace,
+                                    workspace_bytes, stream);
 }

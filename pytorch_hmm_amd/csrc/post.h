@@ -167,15 +167,16 @@ struct VitArgs {
   uint8_t* G;            // (B,nchunks,NP) workspace
   int B, T, N, obs_mode, nchunks;
   const BandDesc* band;  // banded decomposition (band.h) or null
-  int vdiag;             // diagnostic bits for RecArgs::vtail (timing only)
   // psi followers (HMM355_VIT_PLAN_DENSE): workgroups beside the chain, their progress and
   // finished-chunk words (RecArgs::prog / done), zeroed before each launch
   int nfollow;
   int* prog;
   uint8_t* done;
-  // a time part (dense plans): trellis rows [q_lo, q_hi) of this launch (q_hi = 0: T); the psi
-  // pass and the backtrace run with the last part (hmm355_viterbi_part_f32)
-  int q_lo, q_hi;
+  // the decode beside a banded chain (HMM355_VIT_PLAN_BANDED, follow.h): published psi blocks
+  // (B), and with OBS_PROB the log leaders' rows and counts (RecArgs::lobuf / lready)
+  int* pub;
+  const float* lobuf;
+  const int* lready;
 };
 
 // chunk map: G[j] = state at t_lo - 1 given state j at t_hi (psi rows of the chunk in LDS)

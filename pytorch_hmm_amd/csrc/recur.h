@@ -55,13 +55,11 @@ struct RC {
   static constexpr int OFF_LOGT = OFF_M + MRING;           // [256] doubles: Viterbi log table (logcr.h)
   static constexpr int LDS_FLOATS = OFF_LOGT + 512;
   static_assert(LDS_FLOATS * 4 <= kExclusiveLds, "LDS layout too large");
-  // fused Viterbi decode only (RecArgs::vtail; the chain kernel owns all 160 KiB): the psi rows
-  // of the last 64 steps (bytes [64][NP]) and the composer's running chunk map F (bytes [NP])
+  // fused-psi Viterbi (kVitFused; the chain kernel owns all 160 KiB): the psi rows of the last
+  // 64 steps (bytes [64][NP]), written by the psi waves, copied to HBM by the staging helpers
   static constexpr int PSR = 64;
   static constexpr int OFF_PSR = LDS_FLOATS;
-  static constexpr int OFF_FMAP = OFF_PSR + PSR * NP / 4;
-  static constexpr int OFF_GMAP = OFF_FMAP + NP / 4;  // chunk maps for the tail's walk (as many as fit)
-  static_assert(OFF_GMAP * 4 <= kExclusiveLds, "fused Viterbi LDS layout too large");
+  static_assert((OFF_PSR + PSR * NP / 4) * 4 <= kExclusiveLds, "fused Viterbi LDS layout too large");
 };
 
 // threads of a launch that may run the register-blocked dense chain (rec_run_rb, NP <= 128):
@@ -269,13 +267,11 @@ struct RecArgs {
   uint8_t* psi;          // Viterbi, fused banded chain only: (B,T,NP) argmax pointers (kVitFused)
   const float* rmax;     // FB with OBS_LOG: (B,T) row maxima M_t (e_t = exp(lo_t - M_t)), else null
   float* out_exp;        // FB: (B,T,N) forward (alpha) / backward (beta) output written at flush, or null
-  // Viterbi with vtail = 1 (fused banded chain only, kVitFused): the chain kernel finishes the
-  // decode itself -- chunk maps composed during the chain, then the backtrace (rec_band)
+  // Viterbi with psi followers (dense chains, vit_kern.h): chunk maps, path, final score
   uint8_t* G;            // (B, nchunks, NP) chunk maps
   int64_t* states;       // (B,T) decoded path
   float* final_score;    // (B) max of the last trellis row, or null
   int nchunks;
-  int vtail;
   // Viterbi, dense chain with psi followers (HMM355_VIT_PLAN_DENSE, vit_kern.h): the helpers
   // publish the blocks they have flushed in prog[b * kProgSlots + h]; the follower workgroups
   // (blockIdx >= B) mark the chunks they finished in done[b * nchunks + c]
@@ -285,10 +281,19 @@ struct RecArgs {
   // beta: cs[t] = c with v_{t-1} = A (e_t v_t) / c), written beside LS for the adjoint
   // (autograd.py), or null
   float* cs;
-  // Viterbi, dense chain (rec_run_rb) only: compute rows [q_lo, q_hi) of the trellis, row q_lo - 1
-  // read back from `rows` (a previous part's); q_lo a multiple of 64, q_hi = 0 means T.  (Time
-  // parts let a producer of the emissions run ahead of the chain: ops.gmm_viterbi)
-  int q_lo, q_hi;
+  // Banded chains with followers (follow.h): the helpers' row flushes (FB: U / V rows) and psi
+  // row copies (fused Viterbi) are write-through (sc1) stores, and one lane publishes how many
+  // 16-step blocks of them are complete in pub[b * 2 + direction] (FB) / pub[b] (Viterbi):
+  // blocks [0, pub) done while the chain runs, nblocks + 1 once everything (rows, psi, the last
+  // trellis row) is stored.  Null: no publishing.
+  int* pub;
+  // Viterbi with OBS_PROB emissions and log leaders (follow.h vit_lead): lobuf (B,T,N) holds
+  // log(x + 1e-8) of 16-step blocks [4, lready[b]) of sequence b, written by the leaders; the
+  // staging helpers load a block from there when it is ready (checked two blocks ahead), else
+  // the raw emissions, and take the log themselves
+  const float* lobuf;
+  const int* lready;
+  float* lik_ref;        // FB alpha with publishing: (B) the reference's compute_likelihood value
 };
 constexpr int kProgSlots = 8;  // >= kRbHelpers<NP>::NH
 
@@ -323,18 +328,41 @@ __device__ __forceinline__ void rec_logt_fill(float* lds, int l) {
 // ---- emission staging: lane l of wave w holds 4 consecutive states of one step
 // r[0..3]: the emissions; r[4]: the step's row maximum M_t (FB with OBS_LOG; the load reads an
 // address of the same row otherwise, so the staging stays branch-free, and is not used)
-template <int NP, int KIND, bool FULL = false>
-__device__ __forceinline__ void rec_load(const RecArgs& a, int b, int blk, int w, int l, float (&r)[5]) {
+// Viterbi: r[4] is the block's emission form, 1 = log-emissions (OBS_LOG, or rows the log
+// leaders converted: `obs` = RecArgs::lobuf), 0 = probabilities (the staging takes the log);
+// vmode < 0: from a.obs_mode.
+// SC1 (the fused Viterbi chain, whose rows may come from the log leaders in this launch,
+// follow.h): every load is an sc1 load (L1 bypassed: no stale line of a row another workgroup
+// wrote), from a buffer resource over the sequence's rows of `obs`.
+template <int NP, int KIND, bool FULL = false, bool SC1 = false>
+__device__ __forceinline__ void rec_load(const RecArgs& a, int b, int blk, int w, int l, float (&r)[5],
+                                         const float* obs = nullptr, float vmode = -1.f) {
   const int q = blk * 16 + (l >> 2);
   const int col = 16 * w + 4 * (l & 3);
   const bool qok = q < a.T;
-  const size_t bt = (size_t)b * a.T + (qok ? rec_tau<KIND>(q, a.T) : 0);
-  const float* src = a.obs + bt * a.N;
+  const int tq = qok ? rec_tau<KIND>(q, a.T) : 0;
+  const size_t bt = (size_t)b * a.T + tq;
+  const float* src = (obs ? obs : a.obs) + bt * a.N;
   if constexpr (KIND != kVit) {
     const float* mp = a.rmax ? a.rmax + bt : src;  // a pointer select, not a branch
     r[4] = *mp;
   } else {
-    r[4] = 0.f;
+    r[4] = vmode >= 0.f ? vmode : (a.obs_mode == HMM355_OBS_LOG ? 1.f : 0.f);
+  }
+  if constexpr (SC1) {
+    const __amdgpu_buffer_rsrc_t rs = make_rsrc((obs ? obs : a.obs) + (size_t)b * a.T * a.N, (size_t)a.T * a.N * 4);
+    const int off = (tq * a.N + col) * 4;
+    if constexpr (FULL) {
+      const float4 v = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, kAuxSc1));
+      r[0] = v.x; r[1] = v.y; r[2] = v.z; r[3] = v.w;
+    } else {
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const bool ok = qok && col + k < a.N;
+        r[k] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rs, ok ? off + 4 * k : 0, 0, kAuxSc1));
+      }
+    }
+    return;
   }
   if constexpr (FULL) {  // full 16-B aligned rows (the caller checked): one 16-B load
     const float4 v = *reinterpret_cast<const float4*>(src + col);
@@ -348,7 +376,9 @@ __device__ __forceinline__ void rec_load(const RecArgs& a, int b, int blk, int w
   }
 }
 
-template <int NP, int KIND>
+// PERBLK (the fused Viterbi chain with log leaders): the emission form is r[4] of the block's
+// registers (rec_load); otherwise a.obs_mode
+template <int NP, int KIND, bool PERBLK = false>
 __device__ __forceinline__ void rec_stage(const RecArgs& a, float* lds, int blk, int w, int l, const float (&r)[5]) {
   using C = RC<NP>;
   const int sq = l >> 2;
@@ -358,7 +388,9 @@ __device__ __forceinline__ void rec_stage(const RecArgs& a, float* lds, int blk,
   // bloat the helpers' unrolled code (three block copies x HV virtual waves) and end in
   // waitcnt joins
   float e[4];
-  const bool lg = a.obs_mode == HMM355_OBS_LOG;
+  // (Viterbi: the form travels with the block's registers, r[4]; uniform across the wave)
+  const bool lg = (KIND == kVit && PERBLK) ? __builtin_amdgcn_readfirstlane(__builtin_bit_cast(int, r[4])) != 0
+                                          : a.obs_mode == HMM355_OBS_LOG;
   if (lg) {
     // FB: e = exp(lo - M_t) with the row maximum M_t (log-emissions of -100 .. -400 would
     // underflow exp); M_t is carried into the log-scales by rec_flush
@@ -436,7 +468,17 @@ __device__ __forceinline__ void rec_flush(const RecArgs& a, const float* lds, in
     // ends in an s_waitcnt vmcnt(0) join that drains the helper's emission prefetches
     const float4 v = *reinterpret_cast<const float4*>(lds + C::OFF_RING + (q & (C::RING - 1)) * NP + c4);
     const size_t tr = (size_t)b * a.T + rec_tau<KIND>(q, a.T);
-    if (q < a.T) *reinterpret_cast<float4*>(a.rows + tr * NP + c4) = v;
+    if (q < a.T) {
+      if (a.pub) {
+        // followers read these rows in this launch: write-through (sc1) 16-B stores (follow.h)
+        const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+            a.rows + (size_t)b * a.T * NP, (short)0, (int)((size_t)a.T * NP * 4), 0x00020000);
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4_t, v), rs,
+                                               (rec_tau<KIND>(q, a.T) * NP + c4) * 4, 0, kAuxSc1);
+      } else {
+        *reinterpret_cast<float4*>(a.rows + tr * NP + c4) = v;
+      }
+    }
     if constexpr (KIND != kVit) {
       if (a.out_exp) {
         const float ls = __shfl(lsv, row);
@@ -459,9 +501,12 @@ __device__ __forceinline__ void rec_flush(const RecArgs& a, const float* lds, in
     for (int idx = tid; idx < 16 * a.N; idx += C::NT) {
       const int row = idx / a.N, col = idx - row * a.N;
       const int q = q_base + row;
-      if (q < a.T)
-        a.rows[((size_t)b * a.T + rec_tau<KIND>(q, a.T)) * a.row_stride + col] =
-            lds[C::OFF_RING + (q & (C::RING - 1)) * NP + col];
+      float* dst = a.rows + ((size_t)b * a.T + rec_tau<KIND>(q, a.T)) * a.row_stride + col;
+      const float v = lds[C::OFF_RING + (q & (C::RING - 1)) * NP + col];
+      if (q < a.T) {
+        if (a.pub) __hip_atomic_store(dst, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // (sc1)
+        else *dst = v;
+      }
     }
   }
 }
@@ -891,9 +936,8 @@ __device__ __forceinline__ void rec_rb_helper(const RecArgs& a, float* lds, int 
   const int tid = threadIdx.x;
   const int h = (tid >> 6) - C::NW, l = tid & 63, th = tid - C::NT;
   const int T = a.T;
-  // blocks kb0 .. nblocks - 1 of this launch (a time part: rec_run_rb)
-  const int kb0 = KIND == kVit ? a.q_lo / 16 : 0;
-  const int nblocks = ((KIND == kVit && a.q_hi > 0 ? a.q_hi : T) + 15) / 16;
+  const int kb0 = 0;
+  const int nblocks = (T + 15) / 16;
   // register sets: [set = block & 1][slice 0/1][5]
   float er[2][2][5];
   if (KIND == kVit) rec_logt_fill<NP>(lds, l);
@@ -1043,26 +1087,19 @@ __device__ __forceinline__ void rec_run_rb(const RecArgs& a, float* lds, int b) 
         Mk[k][m][e >> 1][e & 1] = FB ? __expf(in ? v : -INFINITY) : (in ? v : -INFINITY);
       }
 
-  // rows [q_lo, q_hi) of this launch (Viterbi time parts; FB: the whole sequence)
-  const int q_lo = KIND == kVit ? a.q_lo : 0;
-  const int kb0 = q_lo / 16;
-  const int qend = KIND == kVit && a.q_hi > 0 ? a.q_hi : T;
+  const int qend = T;
   const int nblocks = (qend + 15) / 16;
   {
     float er0[5];
     if (KIND == kVit) rec_logt_fill<NP>(lds, l);
-    rec_load<NP, KIND>(a, b, kb0, w, l, er0);
-    rec_stage<NP, KIND>(a, lds, kb0, w, l, er0);
+    rec_load<NP, KIND>(a, b, 0, w, l, er0);
+    rec_stage<NP, KIND>(a, lds, 0, w, l, er0);
   }
   lds_barrier();  // (block 1 on: the helpers stage)
 
   auto emis = [&](int rho, int idx) { return lds[C::OFF_EMIS + (((rho >> 4) % 3) * 16 + (rho & 15)) * NP + idx]; };
   const bool writer = (c & 3) == 0;
-  if (q_lo > 0) {
-    // a later part: row q_lo - 1 is the previous part's last trellis row (delta, row stride N)
-    const float v0 = o < N ? a.rows[((size_t)b * T + (q_lo - 1)) * a.row_stride + o] : -INFINITY;
-    if (writer) ring[((q_lo - 1) & (C::RING - 1)) * NP + o] = v0;
-  } else {
+  {
     float v0;
     const int oo = o < N ? o : 0;
     if (KIND == kFbAlpha) v0 = o < N ? __expf(a.init[oo]) * emis(0, o) : 0.f;  // alpha_0 = p0 * e_0
@@ -1174,7 +1211,7 @@ __device__ __forceinline__ void rec_run_rb(const RecArgs& a, float* lds, int b) 
       for (int q = q0; q < q1; ++q) stepq(q);
     }
   };
-  for (int k = kb0; k < nblocks; ++k) run_block(k);
+  for (int k = 0; k < nblocks; ++k) run_block(k);
   if (kStamp && (tid & 63) == 0) {
     const unsigned long long t1 = stamp();
     const long long rt1 = __builtin_amdgcn_s_memrealtime();
@@ -1464,18 +1501,15 @@ __device__ __forceinline__ void rec_band(const RecArgs& a, float* lds, int b, co
   const int grp = (w >> 3) * 3 + (w & 3) - 1;  // WIDE: waves 1,2,3 / 5,6,7 -> 0,1,2; 9,.. / 13,.. -> 3,4,5
   const bool stager = WIDE ? ((w & 4) == 0 && (w & 3) != 0) : (w > 0 && w <= NH);
   const bool psiw = WIDE && (w & 4) != 0 && (w & 3) != 0;
-  // fused decode (a.vtail): wave 4 (the chain's SIMD, otherwise idle) composes the chunk maps
-  // while the chain runs, and every live wave joins the backtrace after it (vit_tail below)
-  const bool composer = FUSE && a.vtail && w == 4;
   const int hi = WIDE ? grp : w - 1;
   auto vw_of = [&](int h) -> int { return hi + h * NH; };  // virtual staging wave h of this helper
   constexpr bool FB = KIND != kVit;
-  if (w != 0 && !stager && !psiw && !composer) return;  // ended waves take no part in s_barrier
+  if (w != 0 && !stager && !psiw) return;  // ended waves take no part in s_barrier
   const int T = a.T, N = a.N;
   const int nblocks = (T + 15) / 16;
   double base = (KIND == kFbBeta && a.bscale) ? (double)a.bscale[b] : 0.0;
 
-  // prologue: the helpers stage block 0 and load block 1
+  // prologue: the helpers stage block 0 and load blocks 1 and 2
   // three register sets: the loads of block kb+3 are issued during block kb, so each has two
   // blocks (~3 us) to land before it is staged
   float er0[HV][5], er1[HV][5], er2[HV][5];
@@ -1487,7 +1521,7 @@ __device__ __forceinline__ void rec_band(const RecArgs& a, float* lds, int b, co
       if (vw < C::NW) {
         float er[5];
         rec_load<NP, KIND>(a, b, 0, vw, l, er);
-        rec_stage<NP, KIND>(a, lds, 0, vw, l, er);
+        rec_stage<NP, KIND, FUSE>(a, lds, 0, vw, l, er);
         if (nblocks > 1) rec_load<NP, KIND>(a, b, 1, vw, l, er1[h]);
         if (nblocks > 2) rec_load<NP, KIND>(a, b, 2, vw, l, er2[h]);
       }
@@ -1495,204 +1529,20 @@ __device__ __forceinline__ void rec_band(const RecArgs& a, float* lds, int b, co
   }
   lds_barrier();
 
-  // ---- fused decode (vtail): chunk maps and the backtrace inside the chain kernel.
-  // The psi waves also keep the last 64 psi rows in LDS (OFF_PSR); the composer wave folds each
-  // block's rows into the running map of its 64-step chunk, F_t[s] = F_{t-1}[psi_t[s]] (F = the
-  // state at the chunk's first step - 1 given state s at t; one dependent LDS gather per row),
-  // three blocks behind the chain, and stores the chunk map G_c = F_{t_hi} (post.h
-  // compose_chunk_map's map, built forward instead of backward).  After the chain: wave 0 walks
-  // the maps from the final state (first argmax of delta_{T-1}, hmm.py:174) down to chunk 0,
-  // then every live wave expands whole chunks, walking psi rows held in registers with
-  // v_readlane (hmm.py:177-178).  Replaces vit_psi_kernel + vit_backtrace_kernel and their two
-  // launches.
-  // chunk maps kept in LDS for the tail's walk (OFF_GMAP, map c at index c - 1) while they fit;
-  // beyond that the walk stages them from G in batches
-  constexpr int GMAP_CAP = ((int)(kExclusiveLds / 4) - C::OFF_GMAP) * 4 / NP < 256
-                               ? ((int)(kExclusiveLds / 4) - C::OFF_GMAP) * 4 / NP : 256;
-  [[maybe_unused]] unsigned fr = 0;  // the composer's running map F: NB bytes, states NB*l + j
-  [[maybe_unused]] auto compose_block = [&](int bk) {
-    if constexpr (FUSE) {
-      if (bk < 0 || (a.vtail & 2)) return;  // (vtail bit 1: diagnostic, no composition)
-      const uint8_t* psr = reinterpret_cast<const uint8_t*>(lds + C::OFF_PSR);
-      const int t0 = 16 * bk;
-      // the block's psi bytes of this lane's states: 16 independent LDS reads, one wait
-      unsigned pr[16];
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int t = t0 + r < T ? t0 + r : T - 1;
-        const uint8_t* src = psr + (t & (C::PSR - 1)) * NP + NB * l;
-        pr[r] = NB == 2 ? (unsigned)*reinterpret_cast<const uint16_t*>(src) : *reinterpret_cast<const unsigned*>(src);
-      }
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int t = t0 + r;
-        if (t < T && t >= kPsiChunk) {  // (chunk 0 has no map)
-          unsigned nf = 0;
-          if ((t & (kPsiChunk - 1)) == 0) {
-            nf = pr[r];  // F at the chunk's first step is psi itself
-          } else {
-            // F_t[s] = F_{t-1}[psi_t[s]]: F_{t-1}[p] is byte p % NB of lane p / NB's register
-#pragma unroll
-            for (int j = 0; j < NB; ++j) {
-              const unsigned p = (pr[r] >> (8 * j)) & 0xffu;
-              const unsigned v = (unsigned)__builtin_amdgcn_ds_bpermute((int)((p / NB) * 4), (int)fr);
-              nf |= ((v >> (8 * (p % NB))) & 0xffu) << (8 * j);
-            }
-          }
-          fr = nf;
-          if ((t & (kPsiChunk - 1)) == kPsiChunk - 1 || t == T - 1) {
-            const int c = t >> 6;
-            uint8_t* gdst = a.G + ((size_t)b * a.nchunks + c) * NP + NB * l;
-            uint8_t* ldst = reinterpret_cast<uint8_t*>(lds + C::OFF_GMAP) + (c - 1) * NP + NB * l;
-            if constexpr (NB == 2) {
-              *reinterpret_cast<uint16_t*>(gdst) = (uint16_t)nf;
-              if (c - 1 < GMAP_CAP) *reinterpret_cast<uint16_t*>(ldst) = (uint16_t)nf;
-            } else {
-              *reinterpret_cast<uint32_t*>(gdst) = nf;
-              if (c - 1 < GMAP_CAP) *reinterpret_cast<uint32_t*>(ldst) = nf;
-            }
-          }
-        }
-      }
-    }
-  };
-  [[maybe_unused]] auto vit_tail = [&]() {
-    if constexpr (FUSE) {
-      // every psi row (global + LDS) and chunk map stored before the barriers that publish them
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      lds_barrier();  // the psi waves' last rows are in the LDS ring
-      if (composer) {
-        compose_block(nblocks - 2);
-        compose_block(nblocks - 1);
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      }
-      lds_barrier();  // every chunk map is in G (and in LDS while they fit)
-      const int nc = a.nchunks;
-      constexpr int GB = 64;  // chunk maps staged per LDS batch (when they are not all in LDS)
-      uint8_t* gl = reinterpret_cast<uint8_t*>(lds);      // [GB][NP] (the chain's staging area: free now)
-      int* send = reinterpret_cast<int*>(gl + GB * NP);   // [nc] the state at each chunk's last step
-      if (w == 0 && !(a.vtail & 8)) {  // (vtail bit 3: diagnostic, no map walk)
-        const float* drow = lds + C::OFF_RING + ((T - 1) & (C::RING - 1)) * NP;
-        float bv = -INFINITY;
-        int bi = 0x7fffffff;
-#pragma unroll
-        for (int k = 0; k < NB; ++k) {
-          const int j = l + 64 * k;
-          if (j < N) argmax_combine(bv, bi, drow[j], j);
-        }
-        wave_argmax_dpp(bv, bi);
-        if (l == 0 && a.final_score) a.final_score[b] = bv;
-        int s = bi < N ? bi : 0;
-        if (l == 0) send[nc - 1] = s;
-        if (nc - 1 <= GMAP_CAP) {
-          const uint8_t* gm = reinterpret_cast<const uint8_t*>(lds + C::OFF_GMAP);
-          for (int c = nc - 1; c >= 1; --c) {
-            s = gm[(c - 1) * NP + s];
-            if (l == 0) send[c - 1] = s;
-          }
-        } else {
-          for (int chi = nc - 1; chi >= 1; chi -= GB) {
-            const int clo = chi - GB + 1 > 1 ? chi - GB + 1 : 1;
-            const int cnt = chi - clo + 1;
-            const unsigned* gsrc = reinterpret_cast<const unsigned*>(a.G + ((size_t)b * nc + clo) * NP);
-            for (int i0 = 0; i0 < cnt * NP / 4; i0 += 64 * 8) {  // 8 loads per lane in flight
-              unsigned v[8];
-#pragma unroll
-              for (int k = 0; k < 8; ++k) {
-                const int i = i0 + 64 * k + l;
-                v[k] = i < cnt * NP / 4 ? __hip_atomic_load(gsrc + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0u;
-              }
-#pragma unroll
-              for (int k = 0; k < 8; ++k) {
-                const int i = i0 + 64 * k + l;
-                if (i < cnt * NP / 4) reinterpret_cast<unsigned*>(gl)[i] = v[k];
-              }
-            }
-            for (int c = chi; c >= clo; --c) {
-              s = gl[(c - clo) * NP + s];
-              if (l == 0) send[c - 1] = s;
-            }
-          }
-        }
-      }
-      lds_barrier();
-      if (a.vtail & 4) return;  // (diagnostic: no expansion)
-      // expansion: live waves 0..7, 9..11, 13..15 (8 and 12 ended at the start) take whole
-      // chunks; a chunk is two groups of GR = 32 rows, walked from the top, the next group's
-      // psi rows loaded while the current one is walked
-      const int widx = w - (w > 8) - (w > 12);
-      constexpr int NAL = 14;
-      constexpr int RPV = 256 / NP;  // psi rows per VGPR (one row = NP bytes = NP/4 lanes)
-      constexpr int LPR = NP / 4;
-      constexpr int GR = 32;         // rows per register group
-      constexpr int NV = GR / RPV;
-      const uint8_t* pb = a.psi + (size_t)b * T * NP;
-      int64_t* sb = a.states + (size_t)b * T;
-      const int nitems = widx < nc ? 2 * ((nc - widx + NAL - 1) / NAL) : 0;
-      auto group = [&](int i, int& c, int& ghi, int& glo) {
-        c = widx + NAL * (i >> 1);
-        const int t_lo = c * kPsiChunk;
-        const int t_hi = (t_lo + kPsiChunk < T ? t_lo + kPsiChunk : T) - 1;
-        ghi = t_hi - GR * (i & 1);
-        glo = ghi - GR + 1 > t_lo ? ghi - GR + 1 : t_lo;
-      };
-      auto load = [&](int i, unsigned(&pv)[NV]) {
-        int c = 0, ghi = -1, glo = 0;
-        if (i < nitems) group(i, c, ghi, glo);
-#pragma unroll
-        for (int v = 0; v < NV; ++v) {
-          const int t = glo + v * RPV + l / LPR;
-          pv[v] = (i < nitems && t <= ghi)
-                      ? __hip_atomic_load(reinterpret_cast<const unsigned*>(pb + (size_t)t * NP) + (l % LPR),
-                                          __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
-                      : 0u;
-        }
-      };
-      int s = 0;
-      auto walk = [&](int i, const unsigned(&pv)[NV]) {
-        if (i >= nitems) return;
-        int c, ghi, glo;
-        group(i, c, ghi, glo);
-        if ((i & 1) == 0) s = send[c];
-        if (ghi < glo) return;  // (the lower group of a short last chunk)
-        int stv = 0;
-        static_for<0, GR>([&](auto KK) {
-          constexpr int k = GR - 1 - decltype(KK)::value;
-          if (glo + k <= ghi) {
-            const int su = __builtin_amdgcn_readfirstlane(s);  // (uniform: keeps it in an SGPR)
-            asm("v_writelane_b32 %0, %1, %2" : "+v"(stv) : "s"(su), "i"(k));
-            const unsigned word = __builtin_amdgcn_readlane(pv[k / RPV], (k % RPV) * LPR + (su >> 2));
-            s = (int)((word >> ((su & 3) * 8)) & 0xffu);
-          }
-        });
-        if (l < GR && glo + l <= ghi) sb[glo + l] = stv;
-      };
-      unsigned pa[NV], pq[NV];
-      load(0, pa);
-      for (int i = 0; i < nitems; i += 2) {
-        load(i + 1, pq);
-        walk(i, pa);
-        load(i + 2, pa);
-        walk(i + 1, pq);
-      }
-    }
-  };
-
   if (w == 0) {
     band_chain<NP, KIND, WP, TD0, TW>(a, lds, b, d);
-    if constexpr (FUSE) {
-      if (a.vtail) vit_tail();
-    }
-  } else {
-    // ---------------------------------------------------------------- helper waves
-    // Fused psi (vit_psi_kernel's banded rule, psi_band_rows in viterbi.hip), on the
-    // psi-only waves 5..7 (SIMDs 1..3, so neither the chain nor the staging helpers lose issue
-    // slots).  With g_i = fl(delta_{t-1,i} + r_i) and M = max g (the chain's own floor term,
-    // left in LDS), i1 = first index with g_i == M is a ballot + s_ff1, and psi_t[o] is the
-    // first index attaining max(M, window values), i1 when M attains it.  The window is the
-    // chain's: Toeplitz offsets TD0.. (TW > 0) or the column windows clo_o .. clo_o + WP.
-    // Lane l owns outputs o = NB*l + j (one 16/32-bit store per row).  Rows r == w-5 (mod 3)
-    // of the block; a wave's rows are computed without branches so their latencies overlap.
+    return;
+  }
+  // ---------------------------------------------------------------- helper waves
+  // Fused psi (vit_psi_kernel's banded rule, psi_band_rows in viterbi.hip), on the
+  // psi-only waves 5..7 and 13..15 (SIMDs 1..3, so neither the chain nor the staging helpers
+  // lose issue slots).  With g_i = fl(delta_{t-1,i} + r_i) and M = max g (the chain's own floor
+  // term, left in LDS), i1 = first index with g_i == M is a ballot + s_ff1, and psi_t[o] is the
+  // first index attaining max(M, window values), i1 when M attains it.  The window is the
+  // chain's: Toeplitz offsets TD0.. (TW > 0) or the column windows clo_o .. clo_o + WP.
+  // Lane l owns outputs o = NB*l + j.  Rows r == grp (mod 6) of the block; a wave's rows are
+  // computed without branches so their latencies overlap.  The rows go to the LDS ring OFF_PSR
+  // (the last 64 steps); the staging helpers copy each block of them to HBM (psi_copy).
     constexpr int PWN = TW > 0 ? TW : WP;  // window slots per output
     [[maybe_unused]] float prf[NB];
     [[maybe_unused]] int plo[NB];
@@ -1774,38 +1624,79 @@ __device__ __forceinline__ void rec_band(const RecArgs& a, float* lds, int b, co
             pk |= (unsigned)arg << (8 * j);
           }
           if (r < 16 && 16 * bk + r < T) {
-            uint8_t* gdst = a.psi + ((size_t)b * T + t) * NP + NB * l;
-            // and the LDS ring of the last 64 rows, for the composer (fused decode)
+            // the LDS ring of the last 64 rows; the staging helpers copy whole blocks of it to
+            // HBM with 16-B stores (psi_copy)
             uint8_t* ldst = reinterpret_cast<uint8_t*>(lds + C::OFF_PSR) + (t & (C::PSR - 1)) * NP + NB * l;
-            if constexpr (NB == 2) {
-              *reinterpret_cast<uint16_t*>(gdst) = (uint16_t)pk;
-              *reinterpret_cast<uint16_t*>(ldst) = (uint16_t)pk;
-            } else {
-              *reinterpret_cast<uint32_t*>(gdst) = pk;
-              *reinterpret_cast<uint32_t*>(ldst) = pk;
-            }
+            if constexpr (NB == 2) *reinterpret_cast<uint16_t*>(ldst) = (uint16_t)pk;
+            else *reinterpret_cast<uint32_t*>(ldst) = pk;
           }
         }
+      }
+    };
+    // Publishing (a.pub, follow.h): the flushes of the rows (FB: U / V, Viterbi: delta) and the
+    // copies of the psi rows are write-through stores issued BEFORE the block's global loads, and
+    // a wave's vector-memory counter retires in issue order, so the compiler's wait for the loads
+    // of block k + 1 (at their staging in block_work(k)) also retires every store issued before
+    // them: the flush of block k - 4 and the psi copy of block k - 5.  After the barrier that ends
+    // block_work(k) those are complete in every helper, and in block_work(k + 1) one lane
+    // publishes the count -- no fence, no explicit drain of the prefetches.
+    const bool pubon = a.pub != nullptr;
+    int* const pubp = pubon ? a.pub + (FB ? 2 * b + (KIND == kFbBeta) : b) : nullptr;
+    [[maybe_unused]] const __amdgpu_buffer_rsrc_t psi_rs =
+        FUSE ? make_rsrc(a.psi + (size_t)b * T * NP, (size_t)T * NP) : make_rsrc(a.obs, 0);
+    // copy the 16 psi rows of block bk from the LDS ring to HBM, one 16-B sc1 store per lane
+    // (the last helpers' lanes: 16 * NP / 16 of them)
+    [[maybe_unused]] auto psi_copy = [&](int bk) {
+      if constexpr (FUSE) {
+        constexpr int PER = NP / 16;  // 16-B pieces per row
+        const int hidx = (NH - 1 - hi) * 64 + l;
+        const int r = hidx / PER, pc = hidx % PER;
+        const int t = 16 * bk + r;
+        const u32x4_t v = *reinterpret_cast<const u32x4_t*>(reinterpret_cast<const uint8_t*>(lds + C::OFF_PSR) +
+                                                            (t & (C::PSR - 1)) * NP + 16 * pc);
+        if (bk >= 0 && hidx < 16 * PER && t < T)
+          __builtin_amdgcn_raw_buffer_store_b128(v, psi_rs, t * NP + 16 * pc, 0, kAuxSc1);
       }
     };
     // Straight-line block work (no branch around the staging or the loads: the tail stages
     // a block past the end as padding and re-loads the last block), so the waitcnt pass
     // keeps exact counts and never drains the in-flight prefetches or the flush stores.
-    auto block_work = [&](int kb, float(&ernext)[HV][5], float(&erfree)[HV][5], auto FULLC) {
+    // Order: publish, log-scales, staging of block kb+1 (waits for its loads), flush of block
+    // kb-2 and psi copy of block kb-3 (stores), the leaders' poll, the loads of block kb+3.
+    // Viterbi with log leaders: the poll issued here is read two blocks later (`pold`), where the
+    // staging's wait has already retired it, so the poll never stalls the helper.
+    auto block_work = [&](int kb, float(&ernext)[HV][5], float(&erfree)[HV][5], int& pnew, int pold, auto FULLC) {
       const int kload = kb + 3 < nblocks ? kb + 3 : nblocks - 1;
+      if (pubon && hi == 0 && l == 0) {
+        const int cnt = FB ? kb - 4 : kb - 5;
+        if (cnt > 0) publish_count(pubp, cnt);
+      }
       // the block's log-scales once per helper (its own base); helper 1 writes LA / LB
       float lsv = 0.f;
       if (!(kAbl & 32) && kb >= 2) lsv = rec_ls_scan<NP, KIND>(a, lds, b, kb - 2, base, w == 1);
 #pragma unroll
       for (int h = 0; h < HV; ++h) {
         const int vw = vw_of(h);
-        if (vw < C::NW && !(kAbl & 32768)) {
-          if (!(kAbl & 64)) {
-            rec_stage<NP, KIND>(a, lds, kb + 1, vw, l, ernext[h]);
-            rec_load<NP, KIND, decltype(FULLC)::value>(a, b, kload, vw, l, erfree[h]);
-          }
-          if (!(kAbl & 32) && kb >= 2) rec_flush<NP, KIND>(a, lds, b, kb - 2, l + 64 * vw, lsv);
-        }
+        if (vw < C::NW && !(kAbl & 32768) && !(kAbl & 64)) rec_stage<NP, KIND, FUSE>(a, lds, kb + 1, vw, l, ernext[h]);
+      }
+#pragma unroll
+      for (int h = 0; h < HV; ++h) {
+        const int vw = vw_of(h);
+        if (vw < C::NW && !(kAbl & 32768) && !(kAbl & 32) && kb >= 2) rec_flush<NP, KIND>(a, lds, b, kb - 2, l + 64 * vw, lsv);
+      }
+      psi_copy(kb - 3);
+      asm volatile("" ::: "memory");  // (the stores stay ahead of the loads below)
+      if (KIND == kVit && a.lready) pnew = poll_count(a.lready + b);
+      // Viterbi: the block's source -- the leaders' log rows when they are ready, else the raw
+      // emissions (the staging takes the log)
+      const bool fromlog = KIND == kVit && a.lobuf && kload >= 4 && pold >= kload + 1;
+      const float* src = fromlog ? a.lobuf : a.obs;
+      const float vmode = (fromlog || a.obs_mode == HMM355_OBS_LOG) ? 1.f : 0.f;
+#pragma unroll
+      for (int h = 0; h < HV; ++h) {
+        const int vw = vw_of(h);
+        if (vw < C::NW && !(kAbl & 32768) && !(kAbl & 64))
+          rec_load<NP, KIND, decltype(FULLC)::value, FUSE>(a, b, kload, vw, l, erfree[h], src, vmode);
       }
       if (!(kAbl & 16384)) lds_barrier();
     };
@@ -1818,29 +1709,23 @@ __device__ __forceinline__ void rec_band(const RecArgs& a, float* lds, int b, co
         lds_barrier();  // the chain's last row
         psi_rows(nblocks - 2);
         psi_rows(nblocks - 1);
-        if (a.vtail) vit_tail();
-        return;
-      }
-      if (composer) {  // block kb - 3's psi rows were written during block kb - 1
-        for (int kb = 0; kb < nblocks; ++kb) {
-          compose_block(kb - 3);
-          if (!(kAbl & 16384)) lds_barrier();
-        }
-        lds_barrier();  // the chain's last row (block nblocks - 3's psi rows are in the ring)
-        compose_block(nblocks - 3);
-        vit_tail();
+        lds_barrier();  // the last psi rows are in the ring (the helpers copy them)
         return;
       }
     }
+    int lp0 = 0, lp1 = 0, lp2 = 0;  // the leaders' poll ring (block kb's poll is read at kb + 2)
     auto helper_loop = [&](auto FULLC) {
       for (int kb = 0; kb < nblocks; kb += 3) {
-        block_work(kb, er1, er0, FULLC);
-        if (kb + 1 < nblocks) block_work(kb + 1, er2, er1, FULLC);
-        if (kb + 2 < nblocks) block_work(kb + 2, er0, er2, FULLC);
+        block_work(kb, er1, er0, lp0, lp1, FULLC);
+        if (kb + 1 < nblocks) block_work(kb + 1, er2, er1, lp1, lp2, FULLC);
+        if (kb + 2 < nblocks) block_work(kb + 2, er0, er2, lp2, lp0, FULLC);
       }
     };
-    if (a.N == NP && (reinterpret_cast<uintptr_t>(a.obs) & 15) == 0) helper_loop(std::true_type{});
-    else helper_loop(std::false_type{});
+    if (a.N == NP && (reinterpret_cast<uintptr_t>(a.obs) & 15) == 0 &&
+        (!a.lobuf || (reinterpret_cast<uintptr_t>(a.lobuf) & 15) == 0))
+      helper_loop(std::true_type{});
+    else
+      helper_loop(std::false_type{});
     lds_barrier();  // the chain's last row and c_{T-1}
     const float lsv2 = nblocks >= 2 ? rec_ls_scan<NP, KIND>(a, lds, b, nblocks - 2, base, w == 1) : 0.f;
     const float lsv1 = rec_ls_scan<NP, KIND>(a, lds, b, nblocks - 1, base, w == 1);
@@ -1854,10 +1739,40 @@ __device__ __forceinline__ void rec_band(const RecArgs& a, float* lds, int b, co
           a.loglik[b] = (float)(base + (double)__logf(lds[C::OFF_SC + 64 * ((T - 1) & (C::RING - 1))]));
       }
     }
-    if constexpr (FUSE) {
-      if (a.vtail) vit_tail();
+    if constexpr (KIND == kFbAlpha) {
+      // the reference's compute_likelihood, logsumexp_j log(forward_{T-1}[j] + 1e-8)
+      // (hmm.py:206), from the last row in LDS and its log-scale: post.h's arithmetic
+      if (a.lik_ref && hi == 0) {
+        const float ls = __shfl(lsv1, (T - 1) & 15);
+        const float* u = lds + C::OFF_RING + ((T - 1) & (C::RING - 1)) * NP;
+        float lv[NB], m = -INFINITY;
+#pragma unroll
+        for (int k = 0; k < NB; ++k) {
+          const int j = l + 64 * k;
+          lv[k] = j < N ? __logf(__expf(__logf(u[j]) + ls) + 1e-8f) : -INFINITY;
+          m = fmaxf(m, lv[k]);
+        }
+        m = wave_max(m);
+        float e = 0.f;
+#pragma unroll
+        for (int k = 0; k < NB; ++k) e += (l + 64 * k < N) ? __expf(lv[k] - m) : 0.f;
+        e = wave_sum(e);
+        if (l == 0) a.lik_ref[b] = m + __logf(e);
+      }
     }
-  }
+    if constexpr (FUSE) {
+      // the psi rows of the last three blocks (the loop copied up to block nblocks - 4)
+      psi_copy(nblocks - 3);
+      lds_barrier();  // the psi waves' last rows
+      psi_copy(nblocks - 2);
+      psi_copy(nblocks - 1);
+    }
+    if (pubon) {
+      // everything stored: every helper's stores retired, then one lane publishes completion
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();  // (the chain and psi waves have ended: the helpers alone)
+      if (hi == 0 && l == 0) publish_count(pubp, nblocks + 1);
+    }
 }
 
 // Which chain serves a recursion (band.h): Toeplitz register windows when the window is a
@@ -1884,9 +1799,7 @@ __device__ __forceinline__ int rec_band_code(const RecArgs& a) {
 
 template <int NP, int KIND>
 __device__ __forceinline__ void rec_dispatch(const RecArgs& a, float* lds, int b) {
-  // (a Viterbi time part runs the register-blocked chain whatever the plan: only it resumes from
-  // a stored row; the C ABI takes parts for host-known dense plans only)
-  const int code = (KIND == kVit && (a.q_lo > 0 || a.q_hi > 0)) ? 0 : rec_band_code<KIND, NP>(a);
+  const int code = rec_band_code<KIND, NP>(a);
   // the banded chains are written for RC<NP>::NT threads (the fused Viterbi form for 1024)
   constexpr int kBandNT = (KIND == kVit && kVitFused<NP>) ? 1024 : RC<NP>::NT;
   if (code != 0 && threadIdx.x >= kBandNT) return;
@@ -1901,15 +1814,6 @@ __device__ __forceinline__ void rec_dispatch(const RecArgs& a, float* lds, int b
     case 16 * 3 - 1 + 2: rec_band<NP, KIND, 2, -1, 3>(a, lds, b, a.band); break;
     case 16 * 3 + 0 + 2: rec_band<NP, KIND, 2, 0, 3>(a, lds, b, a.band); break;
     default:
-      if constexpr (KIND == kVit) {
-        // a fused-decode launch (vtail) on a plan that is not banded: the caller's hint
-        // (HMM355_VIT_PLAN_BANDED) was wrong.  No psi pass follows this kernel, so the path is
-        // marked invalid (states -1, final score NaN) instead of left stale.
-        if (a.vtail) {
-          for (int t = threadIdx.x; t < a.T; t += blockDim.x) a.states[(size_t)b * a.T + t] = -1;
-          if (threadIdx.x == 0 && a.final_score) a.final_score[b] = __builtin_nanf("");
-        }
-      }
       // (diagnostic ablation bits: 1 << 25 the round-2 register-operand chain (NP <= 128),
       // 1 << 24 the DPP-broadcast chain)
       // (NP = 256 keeps the DPP-broadcast chain: 16 waves leave 128 VGPRs a lane, too few for

@@ -589,18 +589,21 @@ __global__ void __launch_bounds__(kSwNT) smk_wide_kernel(SwArgs a) {
 
 using namespace hmm355;
 
-// the register form holds S <= 64, Dmax <= 63; the general form the rest (HMM355_SMK_WIDE=1
+// the register form holds S <= 64, Dmax <= 63; the general form the rest (HMM355_FORM_GENERAL
 // forces it, for tests and comparison)
-static bool smk_wide(int S, int Dmax) {
-  const char* e = getenv("HMM355_SMK_WIDE");
-  return (S > kSmS || Dmax >= kSmR) || (e && e[0] == '1');
+static bool smk_wide(int S, int Dmax, unsigned flags) {
+  return (S > kSmS || Dmax >= kSmR) || (flags & HMM355_FORM_GENERAL);
+}
+
+HMM355_API size_t hmm355_semimarkov_workspace_bytes_ex(int B, int T, int S, int Dmax, unsigned flags) {
+  if (B < 0 || T < 1 || S < 1 || S > kSwS || Dmax < 1 || Dmax > kSwD) return 0;
+  const size_t n = (size_t)B * T * S;
+  if (smk_wide(S, Dmax, flags)) return align_up(n * 4, 256) + align_up(n * (size_t)Dmax * 4, 256);
+  return align_up(n * 4, 256) + align_up(n * 4, 256) + align_up(n, 256) + align_up((size_t)B * 8, 256);
 }
 
 HMM355_API size_t hmm355_semimarkov_workspace_bytes(int B, int T, int S, int Dmax) {
-  if (B < 0 || T < 1 || S < 1 || S > kSwS || Dmax < 1 || Dmax > kSwD) return 0;
-  const size_t n = (size_t)B * T * S;
-  if (smk_wide(S, Dmax)) return align_up(n * 4, 256) + align_up(n * (size_t)Dmax * 4, 256);
-  return align_up(n * 4, 256) + align_up(n * 4, 256) + align_up(n, 256) + align_up((size_t)B * 8, 256);
+  return hmm355_semimarkov_workspace_bytes_ex(B, T, S, Dmax, 0u);
 }
 
 static int smk_check(int B, int T, int S, int Dmax) {
@@ -626,17 +629,18 @@ HMM355_API int hmm355_semimarkov_quad_f32(const float* x, const float* means_t, 
 
 static int smk_run(bool viterbi, const float* quad, const float* seg_const, const float* log_init,
                    const float* log_T, const float* dur_lp, int B, int T, int S, int Dmax, int64_t* seg_states,
-                   int64_t* seg_durs, int* seg_count, float* alpha, float* scores, void* workspace,
-                   size_t workspace_bytes, void* stream) {
+                   int64_t* seg_durs, int* seg_count, float* alpha, float* scores, unsigned flags,
+                   void* workspace, size_t workspace_bytes, void* stream) {
+  if (flags & ~HMM355_FORM_GENERAL) return HMM355_E_ARG;
   int rc = smk_check(B, T, S, Dmax);
   if (rc != HMM355_OK) return rc;
   if (B == 0) return HMM355_OK;
   if (!quad || !log_init || !log_T || !dur_lp || !scores || !workspace) return HMM355_E_ARG;
   if (viterbi && (!seg_states || !seg_durs || !seg_count)) return HMM355_E_ARG;
-  if (workspace_bytes < hmm355_semimarkov_workspace_bytes(B, T, S, Dmax)) return HMM355_E_WORKSPACE;
+  if (workspace_bytes < hmm355_semimarkov_workspace_bytes_ex(B, T, S, Dmax, flags)) return HMM355_E_WORKSPACE;
   const size_t n = (size_t)B * T * S;
   char* ws = static_cast<char*>(workspace);
-  if (smk_wide(S, Dmax)) {
+  if (smk_wide(S, Dmax, flags)) {
     SwArgs wa{quad, seg_const, log_init, log_T, dur_lp, reinterpret_cast<float*>(ws),
               reinterpret_cast<float*>(ws + align_up(n * 4, 256)), scores, alpha, seg_states, seg_durs, seg_count,
               B, T, S, Dmax};
@@ -678,18 +682,35 @@ static int smk_run(bool viterbi, const float* quad, const float* seg_const, cons
   return e == hipSuccess ? HMM355_OK : (int)e;
 }
 
+HMM355_API int hmm355_semimarkov_viterbi_ex_f32(const float* quad, const float* seg_const, const float* log_init,
+                                                const float* log_T, const float* dur_lp, int B, int T, int S,
+                                                int Dmax, unsigned flags, int64_t* seg_states, int64_t* seg_durs,
+                                                int* seg_count, float* scores, void* workspace,
+                                                size_t workspace_bytes, void* stream) {
+  return smk_run(true, quad, seg_const, log_init, log_T, dur_lp, B, T, S, Dmax, seg_states, seg_durs, seg_count,
+                 nullptr, scores, flags, workspace, workspace_bytes, stream);
+}
+
+HMM355_API int hmm355_semimarkov_forward_ex_f32(const float* quad, const float* seg_const, const float* log_init,
+                                                const float* log_T, const float* dur_lp, int B, int T, int S,
+                                                int Dmax, unsigned flags, float* log_alpha, float* log_prob,
+                                                void* workspace, size_t workspace_bytes, void* stream) {
+  return smk_run(false, quad, seg_const, log_init, log_T, dur_lp, B, T, S, Dmax, nullptr, nullptr, nullptr,
+                 log_alpha, log_prob, flags, workspace, workspace_bytes, stream);
+}
+
 HMM355_API int hmm355_semimarkov_viterbi_f32(const float* quad, const float* seg_const, const float* log_init,
                                              const float* log_T, const float* dur_lp, int B, int T, int S, int Dmax,
                                              int64_t* seg_states, int64_t* seg_durs, int* seg_count, float* scores,
                                              void* workspace, size_t workspace_bytes, void* stream) {
-  return smk_run(true, quad, seg_const, log_init, log_T, dur_lp, B, T, S, Dmax, seg_states, seg_durs, seg_count,
-                 nullptr, scores, workspace, workspace_bytes, stream);
+  return hmm355_semimarkov_viterbi_ex_f32(quad, seg_const, log_init, log_T, dur_lp, B, T, S, Dmax, 0u, seg_states,
+                                          seg_durs, seg_count, scores, workspace, workspace_bytes, stream);
 }
 
 HMM355_API int hmm355_semimarkov_forward_f32(const float* quad, const float* seg_const, const float* log_init,
                                              const float* log_T, const float* dur_lp, int B, int T, int S, int Dmax,
                                              float* log_alpha, float* log_prob, void* workspace,
                                              size_t workspace_bytes, void* stream) {
-  return smk_run(false, quad, seg_const, log_init, log_T, dur_lp, B, T, S, Dmax, nullptr, nullptr, nullptr,
-                 log_alpha, log_prob, workspace, workspace_bytes, stream);
+  return hmm355_semimarkov_forward_ex_f32(quad, seg_const, log_init, log_T, dur_lp, B, T, S, Dmax, 0u, log_alpha,
+                                          log_prob, workspace, workspace_bytes, stream);
 }

@@ -466,204 +466,6 @@ __device__ void tv_chain(const TvArgs& a, float* lds, int b) {
   }
 }
 
-// Alpha and Viterbi of one sequence in ONE workgroup (round 4).  Both recursions walk time
-// forward with matrix k = q - 1 at step q in the same (alpha) layout, so each step's slice of
-// log_A is loaded once and feeds the sum-product (u_q = (u_{q-1} exp(lA)) E_q / c_{q-1}) and
-// the max-plus with the first-index argmax (delta_q = fl(max_i fl(delta_{q-1,i} + lA) + lo_q)):
-// one stream of the (B,T,N,N) matrices for the two recursions instead of two.  The arithmetic of
-// each recursion is tv_chain's, operation for operation (same order, same bits).  LDS: alpha's
-// two parity buffers, then Viterbi's.
-template <int NP, bool VEC>
-__device__ void tv_chain_av(const TvArgs& fa, const TvArgs& va, float* lds, int b) {
-  using G = TvGeo<NP>;
-  // one step fewer in flight than the single chains: the second recursion's registers (PD = 3
-  // at NP = 128 spilled 51 VGPRs)
-  constexpr int PD = G::PD > 4 ? 4 : (G::PD > 1 ? G::PD - 1 : 1);
-  const int tid = threadIdx.x, w = tid >> 6, l = tid & 63;
-  const int T = fa.T, N = fa.N;
-  const int part = w / G::CB, r8 = l >> 3;
-  const int cc = 2 * (l >> 5) + ((l >> 4) & 1);
-  const int jo = 32 * (w % G::CB) + 4 * (l & 7) + cc;
-  const bool writer = (l & 8) == 0;
-  auto perm = [&](int i) { return (i / G::RPP) * G::RPP + (i % 8) * G::KA + (i % G::RPP) / 8; };
-  const bool rowout = (w % G::CB) == 0 && (l & 7) < G::KA;
-  float* ldsV = lds + 2 * G::BUF;
-  auto PbufA = [&](int par) { return lds + par * G::BUF; };
-  auto SbufA = [&](int par) { return lds + par * G::BUF + 2 * G::RH * NP; };
-  auto PbufV = [&](int par) { return ldsV + par * G::BUF; };
-  auto IbufV = [&](int par) { return reinterpret_cast<int*>(ldsV + par * G::BUF + G::RH * NP); };
-  const int jc = jo < N ? jo : N - 1;
-  auto emis_a = [&](int q) { return fa.E[((size_t)b * T + (q < T ? q : T - 1)) * NP + jo]; };
-  auto emis_v = [&](int q) { return fa.lo[((size_t)b * T + (q < T ? q : T - 1)) * N + jc]; };
-  auto prefetch = [&](int q, float4 (&rw)[G::NV]) {
-    __builtin_amdgcn_sched_barrier(0);
-    tv_load<NP, kTvAlpha, VEC>(fa, b, (q < T ? q : T - 1) - 1, rw);
-    __builtin_amdgcn_sched_barrier(0);
-  };
-  auto read_rows = [&](const float* Pb, bool vit, float (&y)[G::KA]) {
-    const float* P = Pb + part * G::RPP + r8 * G::KA;
-#pragma unroll
-    for (int h = 0; h < G::RH; ++h) {
-      float x[G::KA];
-      if constexpr (G::KA % 4 == 0) {
-#pragma unroll
-        for (int k4 = 0; k4 < G::KA / 4; ++k4) {
-          const float4 v = *reinterpret_cast<const float4*>(P + h * NP + 4 * k4);
-          x[4 * k4] = v.x; x[4 * k4 + 1] = v.y; x[4 * k4 + 2] = v.z; x[4 * k4 + 3] = v.w;
-        }
-      } else {
-#pragma unroll
-        for (int k2 = 0; k2 < G::KA / 2; ++k2) {
-          const float2 v = *reinterpret_cast<const float2*>(P + h * NP + 2 * k2);
-          x[2 * k2] = v.x; x[2 * k2 + 1] = v.y;
-        }
-      }
-#pragma unroll
-      for (int k = 0; k < G::KA; ++k) y[k] = h == 0 ? x[k] : (vit ? fmaxf(y[k], x[k]) : y[k] + x[k]);
-    }
-  };
-  auto publish_rows = [&](int par, int t) {
-#pragma unroll
-    for (int kq = 0; kq < (G::KA + 7) / 8; ++kq) {
-      const int k = (l & 7) + 8 * kq;
-      if (k < G::KA) {
-        const int off = part * G::RPP + r8 * G::KA + k;
-        const int i = part * G::RPP + r8 + 8 * k;
-        {
-          const float* P = PbufA(par) + off;
-          float u = P[0];
-#pragma unroll
-          for (int h = 1; h < G::RH; ++h) u += P[h * NP];
-          fa.rows[((size_t)b * T + t) * NP + i] = u;
-        }
-        {
-          const float* P = PbufV(par) + off;
-          const int* I = IbufV(par) + off;
-          float m = P[0];
-          int arg = I[0];
-#pragma unroll
-          for (int h = 1; h < G::RH; ++h) {
-            const float x = P[h * NP];
-            arg = x > m ? I[h * NP] : arg;
-            m = fmaxf(m, x);
-          }
-          if (i < N) va.rows[((size_t)b * T + t) * N + i] = m;
-          va.psi[((size_t)b * T + t) * NP + i] = (uint8_t)arg;
-        }
-      }
-    }
-  };
-
-  float4 raw[PD][G::NV];
-  float eA[PD], eV[PD];
-  if (T > 1) {
-#pragma unroll
-    for (int s = 0; s < PD; ++s) {
-      prefetch(1 + s, raw[s]);
-      eA[s] = emis_a(1 + s);
-      eV[s] = emis_v(1 + s);
-    }
-  }
-  {
-    const int jj = jo < N ? jo : 0;
-    const float a0 = jo < N ? __expf(fa.init[jj]) * fa.E[(size_t)b * T * NP + jo] : 0.f;
-    const float v0 = jo < N ? va.init[jj] + fa.lo[(size_t)b * T * N + jo] : -INFINITY;
-    const float pa = part == 0 ? a0 : 0.f;
-    const float pv = part == 0 ? v0 : -INFINITY;
-    if (writer) {
-      PbufA(0)[part * NP + perm(jo)] = pa;
-      PbufV(0)[part * NP + perm(jo)] = pv;
-      IbufV(0)[part * NP + perm(jo)] = 0;
-    }
-    const float sw = wave_sum_pairs(pa);
-    if (l == 0) SbufA(0)[w] = sw;
-  }
-  lds_barrier();
-
-  auto step = [&](int q, float4 (&rw)[G::NV], float& ea, float& ev) {
-    const int pp = (q - 1) & 1, cp = q & 1;
-    float y[G::KA], yv[G::KA];
-    read_rows(PbufA(pp), false, y);
-    read_rows(PbufV(pp), true, yv);
-    const float4 s0 = *reinterpret_cast<const float4*>(SbufA(pp));
-    const float4 s1 = *reinterpret_cast<const float4*>(SbufA(pp) + 4);
-    const float cs = ((s0.x + s0.y) + (s0.z + s0.w)) + ((s1.x + s1.y) + (s1.z + s1.w));  // c_{q-1}
-    float acc[4] = {0.f, 0.f, 0.f, 0.f};
-    const int i0 = part * G::RPP + r8;
-    float bv[4];
-    int bi[4];
-    {
-      const float4 A = rw[0];
-      acc[0] = fmaf(y[0], __expf(A.x), acc[0]);
-      acc[1] = fmaf(y[0], __expf(A.y), acc[1]);
-      acc[2] = fmaf(y[0], __expf(A.z), acc[2]);
-      acc[3] = fmaf(y[0], __expf(A.w), acc[3]);
-      bv[0] = yv[0] + A.x; bv[1] = yv[0] + A.y; bv[2] = yv[0] + A.z; bv[3] = yv[0] + A.w;
-      bi[0] = bi[1] = bi[2] = bi[3] = i0;
-    }
-#pragma unroll
-    for (int k = 1; k < G::KA; ++k) {
-      const float4 A = rw[k];
-      acc[0] = fmaf(y[k], __expf(A.x), acc[0]);
-      acc[1] = fmaf(y[k], __expf(A.y), acc[1]);
-      acc[2] = fmaf(y[k], __expf(A.z), acc[2]);
-      acc[3] = fmaf(y[k], __expf(A.w), acc[3]);
-      const int ii = i0 + 8 * k;
-#pragma unroll
-      for (int c = 0; c < 4; ++c) {
-        const float sv = yv[k] + f4(A, c);
-        bi[c] = sv > bv[c] ? ii : bi[c];
-        bv[c] = fmaxf(bv[c], sv);
-      }
-    }
-    prefetch(q + PD, rw);
-    const float z = rowlanes_transpose_sum<8>(acc);
-    const float u = z * (ea * __builtin_amdgcn_rcpf(cs));
-    float v;
-    int vi;
-    rowlanes_transpose_argmax<8>(bv, bi, v, vi);
-    const float d = v + (jo < N ? ev : -INFINITY);
-    if (writer) {
-      PbufA(cp)[part * NP + perm(jo)] = u;
-      PbufV(cp)[part * NP + perm(jo)] = d;
-      IbufV(cp)[part * NP + perm(jo)] = vi;
-    }
-    const float sw = wave_sum_pairs(u);
-    if (l == 0) SbufA(cp)[w] = sw;
-    if (rowout) publish_rows(pp, q - 1);
-    if (tid == 0) fa.cs[(size_t)b * T + q] = cs;
-    ea = emis_a(q + PD);
-    ev = emis_v(q + PD);
-    lds_barrier();
-  };
-  int q0 = 1;
-  for (; q0 + PD <= T; q0 += PD) {
-#pragma unroll
-    for (int s = 0; s < PD; ++s) step(q0 + s, raw[s], eA[s], eV[s]);
-  }
-#pragma unroll
-  for (int s = 0; s < PD; ++s)
-    if (q0 + s < T) step(q0 + s, raw[s], eA[s], eV[s]);
-  const int pl = (T - 1) & 1;
-  if (rowout) publish_rows(pl, T - 1);
-  if (tid == 0) {
-    const float* S = SbufA(pl);
-    fa.cs[(size_t)b * T] = ((S[0] + S[1]) + (S[2] + S[3])) + ((S[4] + S[5]) + (S[6] + S[7]));
-  }
-}
-
-// forward-backward and Viterbi together: block 2b the alpha + Viterbi chains of sequence b
-// (tv_chain_av), block 2b + 1 its beta chain
-template <int NP, bool VEC>
-__global__ void __launch_bounds__(512) tv_fbv_kernel(TvArgs fa, TvArgs fb, TvArgs va) {
-  extern __shared__ __attribute__((aligned(16))) float lds[];
-  const int b = blockIdx.x >> 1;
-  if (blockIdx.x & 1)
-    tv_chain<NP, kTvBeta, VEC>(fb, lds, b);
-  else
-    tv_chain_av<NP, VEC>(fa, va, lds, b);
-}
-
 template <int NP, bool VEC>
 __global__ void __launch_bounds__(512) tv_fb_kernel(TvArgs fa, TvArgs fb) {
   extern __shared__ __attribute__((aligned(16))) float lds[];
@@ -1063,40 +865,6 @@ static hipError_t launch_tv_vit(const TvArgs& ta, const VitArgs& va, bool vec, h
   return hipGetLastError();
 }
 
-// forward-backward + Viterbi in one pass over the matrices (tv_fbv_kernel)
-template <int NP>
-static hipError_t launch_tv_fbv(const TvArgs& fa, const TvArgs& fb, const TvArgs& ta, const PostArgs& pa,
-                                const VitArgs& va, const TvFbWs& w, float* loglik, bool vec, hipStream_t st) {
-  const size_t rows = (size_t)fa.B * fa.T;
-  {
-    const size_t waves = rows < 16384 ? rows : 16384;
-    hipLaunchKernelGGL(tv_emis_kernel<NP>, dim3((unsigned)((waves + 3) / 4)), dim3(256), 0, st, fa.lo, w.E, w.M,
-                       rows, fa.N);
-    const hipError_t e = hipGetLastError();
-    if (e != hipSuccess) return e;
-  }
-  hipError_t e;
-  if (vec) {
-    e = allow_lds(tv_fbv_kernel<NP, true>, kExclusiveLds);
-    if (e != hipSuccess) return e;
-    hipLaunchKernelGGL((tv_fbv_kernel<NP, true>), dim3(2 * fa.B), dim3(512), kExclusiveLds, st, fa, fb, ta);
-  } else {
-    e = allow_lds(tv_fbv_kernel<NP, false>, kExclusiveLds);
-    if (e != hipSuccess) return e;
-    hipLaunchKernelGGL((tv_fbv_kernel<NP, false>), dim3(2 * fa.B), dim3(512), kExclusiveLds, st, fa, fb, ta);
-  }
-  if ((e = hipGetLastError()) != hipSuccess) return e;
-  hipLaunchKernelGGL(tv_scan_kernel, dim3(2 * fa.B), dim3(64), 0, st, w.CA, w.CB, w.M, w.LA, w.LB, loglik, nullptr,
-                     fa.T);
-  if ((e = hipGetLastError()) != hipSuccess) return e;
-  const size_t waves = rows < 8192 ? rows : 8192;
-  hipLaunchKernelGGL(fb_posterior_kernel<NP>, dim3((unsigned)((waves + 3) / 4)), dim3(256), 0, st, pa);
-  if ((e = hipGetLastError()) != hipSuccess) return e;
-  hipLaunchKernelGGL(tv_chunkmap_kernel<NP>, dim3(va.nchunks, va.B), dim3(NP), 0, st, va);
-  if ((e = hipGetLastError()) != hipSuccess) return e;
-  hipLaunchKernelGGL(vit_backtrace_kernel<NP>, dim3(va.nchunks, va.B), dim3(64), 0, st, va);
-  return hipGetLastError();
-}
 
 }  // namespace hmm355
 
@@ -1220,55 +988,6 @@ HMM355_API int hmm355_tv_fb_adjoint_f32(const float* E, const float* log_A, long
     case 64: vec ? go(tv_adjoint_kernel<64, true>) : go(tv_adjoint_kernel<64, false>); break;
     case 128: vec ? go(tv_adjoint_kernel<128, true>) : go(tv_adjoint_kernel<128, false>); break;
     default: vec ? go(tv_adjoint_kernel<256, true>) : go(tv_adjoint_kernel<256, false>); break;
-  }
-  return e == hipSuccess ? HMM355_OK : (int)e;
-}
-
-// forward-backward and Viterbi of the same time-varying model in one call: the alpha and
-// Viterbi recursions share one stream of the (B,T,N,N) matrices (tv_chain_av)
-HMM355_API size_t hmm355_tv_fb_viterbi_workspace_bytes(int B, int T, int N) {
-  const size_t a = hmm355_tv_fb_workspace_bytes(B, T, N), v = hmm355_tv_viterbi_workspace_bytes(B, T, N);
-  return (a == 0 || v == 0) ? 0 : align_up(a, 256) + v;
-}
-
-HMM355_API int hmm355_tv_fb_viterbi_f32(const float* log_obs, const float* log_A, long long a_bstride,
-                                        long long a_tstride, const float* log_p0, const float* init, int B, int T,
-                                        int N, unsigned out_mask, float* posterior, float* forward, float* backward,
-                                        float* loglik, float* lik_ref, int64_t* states, float* log_delta,
-                                        void* workspace, size_t workspace_bytes, void* stream) {
-  if (B < 0 || N < 0 || a_bstride < 0 || a_tstride < 0) return HMM355_E_ARG;
-  if (N < 1 || N > 256) return HMM355_E_STATES;
-  if (T < 1) return HMM355_E_SHAPE;
-  if (B == 0) return HMM355_OK;
-  if (!log_obs || !log_A || !log_p0 || !init || !states || !log_delta || !workspace) return HMM355_E_ARG;
-  if ((out_mask & HMM355_FB_POSTERIOR) && !posterior) return HMM355_E_ARG;
-  if ((out_mask & HMM355_FB_FORWARD) && !forward) return HMM355_E_ARG;
-  if ((out_mask & HMM355_FB_BACKWARD) && !backward) return HMM355_E_ARG;
-  if ((size_t)B * T > (size_t)1 << 40 || B > 65535) return HMM355_E_SHAPE;
-  if (workspace_bytes < hmm355_tv_fb_viterbi_workspace_bytes(B, T, N)) return HMM355_E_WORKSPACE;
-  const int NP = pad_states(N);
-  TvFbWs w;
-  tv_fb_ws_layout(B, T, N, static_cast<char*>(workspace), &w);
-  uint8_t* psi = static_cast<uint8_t*>(workspace) + align_up(hmm355_tv_fb_workspace_bytes(B, T, N), 256);
-  const int nc = (T + kChunk - 1) / kChunk;
-  uint8_t* G = psi + align_up((size_t)B * T * NP, 256);
-  TvArgs fa{log_obs, log_A, a_bstride, a_tstride, log_p0, w.E, w.U, w.CA, nullptr, nullptr, B, T, N};
-  TvArgs fb{log_obs, log_A, a_bstride, a_tstride, log_p0, w.E, w.V, w.CB, nullptr, nullptr, B, T, N};
-  TvArgs ta{log_obs, log_A, a_bstride, a_tstride, init, nullptr, log_delta, nullptr, psi, nullptr, B, T, N};
-  PostArgs pa{w.U, w.V, w.LA, w.LB, posterior, forward, backward, lik_ref, B, T, N, out_mask};
-  VitArgs va{log_obs, log_A, init, log_delta, nullptr, states, psi, G, B, T, N, HMM355_OBS_LOG, nc, nullptr};
-  const bool vec = tv_vec_ok(log_A, a_bstride, a_tstride, N);
-  hipStream_t st = static_cast<hipStream_t>(stream);
-  hipError_t e;
-  switch (NP) {
-    case 64: e = launch_tv_fbv<64>(fa, fb, ta, pa, va, w, loglik, vec, st); break;
-    case 128: e = launch_tv_fbv<128>(fa, fb, ta, pa, va, w, loglik, vec, st); break;
-    default:
-      // NP = 256: the two recursions' registers do not fit one wave (76 VGPRs spilled), so the
-      // matrices are streamed by the separate chains, one after the other
-      e = launch_tv_fb<256>(fa, fb, pa, w, loglik, nullptr, vec, st);
-      if (e == hipSuccess) e = launch_tv_vit<256>(ta, va, vec, st);
-      break;
   }
   return e == hipSuccess ? HMM355_OK : (int)e;
 }

@@ -3,6 +3,7 @@
 #pragma once
 #include "recur.h"
 #include "post.h"
+#include "follow.h"
 
 namespace hmm355 {
 
@@ -13,8 +14,16 @@ __device__ __forceinline__ void vit_psi_follow(const RecArgs& ra, float* lds);
 template <int NP>
 __global__ void __launch_bounds__(kVitNT<NP>) vit_fwd_kernel(RecArgs ra) {
   extern __shared__ __attribute__((aligned(16))) float lds[];
-  if ((int)blockIdx.x >= ra.B) {  // psi followers (HMM355_VIT_PLAN_DENSE)
-    if constexpr (NP <= 128) vit_psi_follow<NP>(ra, lds);
+  if ((int)blockIdx.x >= ra.B) {
+    if (ra.pub) {  // the decode beside a banded chain (HMM355_VIT_PLAN_BANDED, follow.h)
+      if constexpr (kVitFused<NP>) {
+        const int b = (int)blockIdx.x - ra.B;
+        vit_lead<NP>(ra, b);
+        vit_decode_follow<NP>(ra, b, lds);
+      }
+      return;
+    }
+    if constexpr (NP <= 128) vit_psi_follow<NP>(ra, lds);  // psi followers (HMM355_VIT_PLAN_DENSE)
     return;
   }
   rec_dispatch<NP, kVit>(ra, lds, blockIdx.x);
@@ -269,19 +278,13 @@ __device__ __forceinline__ void vit_psi_follow(const RecArgs& ra, float* lds) {
   if (rec_band_code<kVit, NP>(ra) != 0) return;  // banded: the psi pass after the chain
   if (threadIdx.x >= C::NT) return;              // the dense psi layout's waves
   const VitArgs a{ra.obs, ra.mat, ra.init, ra.rows, ra.final_score, ra.states, ra.psi, ra.G,
-                  ra.B, ra.T, ra.N, ra.obs_mode, ra.nchunks, ra.band, 0, 0, ra.prog, ra.done};
+                  ra.B, ra.T, ra.N, ra.obs_mode, ra.nchunks, ra.band, 0, ra.prog, ra.done};
   uint8_t(*prow)[NP] = reinterpret_cast<uint8_t(*)[NP]>(lds);
   int* ok_slot = reinterpret_cast<int*>(lds + kChunk * NP / 4);
   float M[C::NBLK][16];
   psi_dense_matrix<NP>(a, M);
   const int nf = (int)gridDim.x - a.B;
-  // the chunks of this launch (a time part [q_lo, q_hi), both multiples of kChunk but the last
-  // q_hi): a part leaves its last chunk to the next part's followers (its rows are complete when
-  // that part starts), so no part's launch waits for followers still on its last rows; the last
-  // part takes the rest, and the psi pass after it every chunk not marked done
-  const bool last_part = ra.q_hi == 0 || ra.q_hi >= a.T;
-  const int c_lo = ra.q_lo > 0 ? ra.q_lo / kChunk - 1 : 0;
-  const int c_hi = last_part ? a.nchunks : ra.q_hi / kChunk - 1;
+  const int c_lo = 0, c_hi = a.nchunks;
   const int ntask = a.B * (c_hi - c_lo);
   int last_have = -1;
   long long t0 = __builtin_amdgcn_s_memrealtime();
@@ -323,7 +326,7 @@ __device__ __forceinline__ void vit_psi_follow(const RecArgs& ra, float* lds) {
 }
 
 template <int NP>
-hipError_t launch_vit(const VitArgs& va, bool prep, bool tail, hipStream_t sm) {
+hipError_t launch_vit(const VitArgs& va, bool prep, hipStream_t sm) {
   hipError_t e = allow_lds(vit_fwd_kernel<NP>, kExclusiveLds);  // own the CU (recur.h)
   if (e != hipSuccess) return e;
   if (va.band && prep) {
@@ -332,36 +335,30 @@ hipError_t launch_vit(const VitArgs& va, bool prep, bool tail, hipStream_t sm) {
   }
   RecArgs ra{va.obs, va.log_P, va.init, va.delta, nullptr, nullptr, va.B, va.T, va.N, va.obs_mode, va.N, va.band,
              nullptr, nullptr, va.psi};
-  ra.q_lo = va.q_lo;
-  ra.q_hi = va.q_hi;
-  const bool first = va.q_lo == 0, last = va.q_hi == 0 || va.q_hi == va.T;
-  if (tail) {  // the fused decode: chunk maps and backtrace inside the chain kernel (recur.h vtail)
-    ra.G = va.G;
-    ra.states = va.states;
-    ra.final_score = va.final_score;
-    ra.nchunks = va.nchunks;
-    ra.vtail = 1 | va.vdiag;
+  ra.G = va.G;
+  ra.states = va.states;
+  ra.final_score = va.final_score;
+  ra.nchunks = va.nchunks;
+  if (va.pub) {
+    // the decode beside the banded chain (follow.h): B chains + B decode workgroups, nothing after
+    ra.pub = va.pub;
+    ra.lobuf = va.lobuf;
+    ra.lready = va.lready;
+    hipLaunchKernelGGL(vit_fwd_kernel<NP>, dim3(2 * va.B), dim3(kVitNT<NP>), kExclusiveLds, sm, ra);
+    return hipGetLastError();
   }
   // psi followers beside a dense chain (NP <= 128: the chain with block-work helpers publishes)
-  const int nfollow = (!tail && NP <= 128 && va.prog && va.done) ? va.nfollow : 0;
+  const int nfollow = (NP <= 128 && va.prog && va.done) ? va.nfollow : 0;
   if (nfollow > 0) {
-    // (the first part clears the followers' words for every chunk; later parts keep counting)
-    if (first) {
-      e = hipMemsetAsync(va.prog, 0, (size_t)va.B * kProgSlots * sizeof(int), sm);
-      if (e == hipSuccess) e = hipMemsetAsync(va.done, 0, (size_t)va.B * va.nchunks, sm);
-      if (e != hipSuccess) return e;
-    }
-    ra.G = va.G;
-    ra.states = va.states;
-    ra.final_score = va.final_score;
-    ra.nchunks = va.nchunks;
+    e = hipMemsetAsync(va.prog, 0, (size_t)va.B * kProgSlots * sizeof(int), sm);
+    if (e == hipSuccess) e = hipMemsetAsync(va.done, 0, (size_t)va.B * va.nchunks, sm);
+    if (e != hipSuccess) return e;
     ra.prog = va.prog;
     ra.done = va.done;
   }
   hipLaunchKernelGGL(vit_fwd_kernel<NP>, dim3(va.B + nfollow), dim3(kVitNT<NP>), kExclusiveLds, sm, ra);
   e = hipGetLastError();
   if (e != hipSuccess) return e;
-  if (tail || !last) return hipSuccess;
   // banded psi stages the chunk's delta rows in LDS (dynamic, kChunk x NP floats)
   const size_t psi_lds = va.band ? (size_t)kChunk * NP * sizeof(float) : 0;
   VitArgs vp = va;

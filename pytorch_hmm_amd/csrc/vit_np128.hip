@@ -2,7 +2,7 @@
 #include "vit_kern.h"
 
 namespace hmm355 {
-template hipError_t launch_vit<128>(const VitArgs& va, bool prep, bool tail, hipStream_t sm);
+template hipError_t launch_vit<128>(const VitArgs& va, bool prep, hipStream_t sm);
 }  // namespace hmm355
 
 // diagnostic builds: the stamps live in this translation unit's code object (recur.h)

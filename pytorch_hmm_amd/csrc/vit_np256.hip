@@ -2,5 +2,5 @@
 #include "vit_kern.h"
 
 namespace hmm355 {
-template hipError_t launch_vit<256>(const VitArgs& va, bool prep, bool tail, hipStream_t sm);
+template hipError_t launch_vit<256>(const VitArgs& va, bool prep, hipStream_t sm);
 }  // namespace hmm355

@@ -28,14 +28,17 @@
 //   (first index, hmm.py:174), the chain of chunk maps from the last chunk down to this one
 //   (LDS lookups), then this chunk's 64-step walk (hmm.py:177-178).  The serial depth is
 //   T/64 + 64 lookups instead of T dependent gathers.
+#include <atomic>
+
 #include "recur.h"
 #include "post.h"
+#include "follow.h"
 
 namespace hmm355 {
 
 // per-NP launcher (vit_kern.h, instantiated in vit_np64/128/256.hip)
 template <int NP>
-hipError_t launch_vit(const VitArgs& va, bool prep, bool tail, hipStream_t sm);
+hipError_t launch_vit(const VitArgs& va, bool prep, hipStream_t sm);
 
 }  // namespace hmm355
 
@@ -72,41 +75,41 @@ HMM355_API size_t hmm355_viterbi_workspace_bytes(int B, int T, int N) {
          align_up((size_t)B * nc, 256);
 }
 
-// CUs of the current device (cached per device): the psi followers take the ones the chain
-// leaves, at most one workgroup per CU (the launch owns a CU's LDS)
+// CUs of the current device, queried once per device (a relaxed atomic per slot: concurrent
+// first calls may both query, and store the same value).  The psi followers take the CUs the
+// chain leaves, at most one workgroup per CU (the launch owns a CU's LDS).
 static constexpr int kFollowPerSeq = 2;
 
 static int device_cus() {
-  static int cus[64] = {0};
+  static std::atomic<int> cus[64];
   int dev = 0;
   if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 0;
-  if (cus[dev] == 0) {
-    int n = 0;
-    if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) n = 0;
-    cus[dev] = n > 0 ? n : -1;
+  int n = cus[dev].load(std::memory_order_relaxed);
+  if (n == 0) {
+    if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0) n = -1;
+    cus[dev].store(n, std::memory_order_relaxed);
   }
-  return cus[dev] > 0 ? cus[dev] : 0;
+  return n > 0 ? n : 0;
 }
 
-// OBS_PROB emissions go through the log pass for every chain (HMM355_VIT_LOGPASS=0: the banded
-// chain's staging helpers take the log themselves, the round-4 form, diagnostic)
-static bool vit_logpass() {
-  const char* e = getenv("HMM355_VIT_LOGPASS");
-  return !(e && e[0] == '0');
+// The decode beside a banded chain (HMM355_VIT_PLAN_BANDED, follow.h): the fused-psi chain
+// (NP >= 128), one extra workgroup per sequence, and room for both on the chip with CUs to spare
+// for a concurrent forward-backward (2B <= CUs / 2); the follower's chunk maps must fit its LDS and
+// every per-sequence byte offset an int.
+static bool vit_follow_ok(unsigned flags, const void* plan, int B, int T, int N) {
+  const int NP = pad_states(N);
+  return (flags & HMM355_VIT_PLAN_BANDED) && plan && NP >= 128 && 4 * B <= device_cus() &&
+         vit_follow_lds_bytes(T, NP) <= kExclusiveLds && (size_t)T * NP * 4 < ((size_t)1 << 31) &&
+         (size_t)T * N * 4 < ((size_t)1 << 31);
 }
 
 static int viterbi_run(const float* obs, int obs_mode, const float* log_P, const float* init, const void* plan,
-                       unsigned flags, int B, int T, int N, int q_lo, int q_hi, int64_t* states, float* log_delta,
-                       float* final_score, void* workspace, size_t workspace_bytes, void* stream) {
+                       unsigned flags, int B, int T, int N, int64_t* states, float* log_delta, float* final_score,
+                       void* workspace, size_t workspace_bytes, void* stream) {
   if (B < 0 || N < 0) return HMM355_E_ARG;
   if (N < 1 || N > 256) return HMM355_E_STATES;
   if (T < 1) return HMM355_E_SHAPE;
-  if (q_hi == 0) q_hi = T;
-  if (q_lo < 0 || q_lo % kChunk || q_lo >= q_hi || q_hi > T) return HMM355_E_ARG;
-  const bool part = q_lo > 0 || q_hi < T;
-  // time parts: the register-blocked dense chain (host-known dense plan, N <= 128) on log-emissions
-  if (part && (!(flags & HMM355_VIT_PLAN_DENSE) || !plan || N > 128 || obs_mode != HMM355_OBS_LOG))
-    return HMM355_E_ARG;
+  if (flags & ~(HMM355_VIT_PLAN_BANDED | HMM355_VIT_PLAN_DENSE)) return HMM355_E_ARG;
   if (B == 0) return HMM355_OK;
   if (!obs || !log_P || !init || !states || !log_delta || !workspace) return HMM355_E_ARG;
   if (obs_mode != HMM355_OBS_PROB && obs_mode != HMM355_OBS_LOG) return HMM355_E_ARG;
@@ -120,33 +123,34 @@ static int viterbi_run(const float* obs, int obs_mode, const float* log_P, const
   float* lobuf = reinterpret_cast<float*>(bandp + align_up(sizeof(BandDesc), 256));
   int* prog = reinterpret_cast<int*>(reinterpret_cast<uint8_t*>(lobuf) + align_up((size_t)B * T * N * sizeof(float), 256));
   uint8_t* done = reinterpret_cast<uint8_t*>(prog) + align_up((size_t)B * kProgSlots * sizeof(int), 256);
-  BandDesc* band = use_band() ? (plan ? static_cast<BandDesc*>(const_cast<void*>(plan))
-                                      : reinterpret_cast<BandDesc*>(bandp))
-                               : nullptr;
-  // (OBS_PROB: the log pass below, or with HMM355_VIT_LOGPASS=0 on a plan that is not dense the
-  // chain's staging helpers take log(x + 1e-8) themselves, ~12 fp64 operations per element)
+  BandDesc* band = plan ? static_cast<BandDesc*>(const_cast<void*>(plan)) : reinterpret_cast<BandDesc*>(bandp);
   VitArgs va{obs, log_P, init, log_delta, final_score, states, psi, G, B, T, N, obs_mode, nc, band};
-  // (the whole range stays q_lo = q_hi = 0: the chain kernel then picks the banded chain where the
-  // plan is banded; a part always runs the register-blocked dense chain, recur.h rec_dispatch)
-  va.q_lo = part ? q_lo : 0;
-  va.q_hi = part ? q_hi : 0;
   hipStream_t sm = static_cast<hipStream_t>(stream);
-  // the fused decode needs the fused banded chain (NP >= 128) and the plan's word that it is
-  // banded (the caller read it once per plan, hmm355_plan_banded); its tail keeps at most
-  // 4096 chunk end states in LDS (T <= 262144)
-  const bool tail = (flags & HMM355_VIT_PLAN_BANDED) && plan && band && NP >= 128 && nc <= 4096 && !part;
-#ifdef HMM355_DIAG
-  // (HMM355_VIT_TAIL_DIAG: diagnostic bits of RecArgs::vtail, timing only -- results are wrong;
-  // read only in diagnostic builds, build_native.build(defines=["HMM355_DIAG"]))
-  const char* diag = getenv("HMM355_VIT_TAIL_DIAG");
-  va.vdiag = diag ? (atoi(diag) & ~1) : 0;
-#endif
+  hipError_t e;
+  if (vit_follow_ok(flags, plan, B, T, N)) {
+    // one launch: the chains, and per sequence a workgroup that first forms log(x + 1e-8) of
+    // the sequence's emissions ahead of its chain (OBS_PROB) and then composes the chunk maps and
+    // backtraces the path (follow.h).  The counts live in prog: [0, B) published psi blocks, [B, 2B)
+    // the leaders' blocks, zeroed first (a 16-B multiple inside prog's block).
+    if ((e = hipMemsetAsync(prog, 0, align_up((size_t)2 * B * sizeof(int), 16), sm)) != hipSuccess) return (int)e;
+    va.pub = prog;
+    if (obs_mode == HMM355_OBS_PROB) {
+      va.lobuf = lobuf;
+      va.lready = prog + B;
+    }
+    va.nfollow = B;
+    switch (NP) {
+      case 128: e = launch_vit<128>(va, false, sm); break;
+      default: e = launch_vit<256>(va, false, sm); break;
+    }
+    return e == hipSuccess ? HMM355_OK : (int)e;
+  }
   // psi followers: the caller's word that the plan is dense, N <= 128, and CUs beside the chain.
   // A chain publishes a 64-step chunk every ~17 us (dense step ~270 ns) and a follower takes
   // ~25-30 us per chunk, so two followers per sequence keep up; more would only hold CUs (each
   // owns one: the launch asks for the CU's whole LDS) that a concurrent op on another stream
   // could use.  With nfollow = 2B follower f serves sequence f mod B, every other chunk.
-  if ((flags & HMM355_VIT_PLAN_DENSE) && plan && NP <= 128 && !tail) {
+  if ((flags & HMM355_VIT_PLAN_DENSE) && plan && NP <= 128) {
     const long room = (long)device_cus() - B;
     const long tasks = (long)B * nc;
     long nf = room < tasks ? room : tasks;
@@ -155,8 +159,8 @@ static int viterbi_run(const float* obs, int obs_mode, const float* log_P, const
     va.prog = prog;
     va.done = done;
   }
-  hipError_t e;
-  if (obs_mode == HMM355_OBS_PROB && (((flags & HMM355_VIT_PLAN_DENSE) && plan) || vit_logpass())) {
+  // OBS_PROB emissions otherwise: the full-chip log pass before the chain (vit_log_obs_kernel)
+  if (obs_mode == HMM355_OBS_PROB) {
     const size_t n = (size_t)B * T * N;
     size_t blocks = (n / 4 + 255) / 256;
     blocks = blocks < 8192 ? (blocks > 0 ? blocks : 1) : 8192;
@@ -167,9 +171,9 @@ static int viterbi_run(const float* obs, int obs_mode, const float* log_P, const
     va.obs_mode = HMM355_OBS_LOG;
   }
   switch (NP) {
-    case 64: e = launch_vit<64>(va, plan == nullptr, false, sm); break;
-    case 128: e = launch_vit<128>(va, plan == nullptr, tail, sm); break;
-    default: e = launch_vit<256>(va, plan == nullptr, tail, sm); break;
+    case 64: e = launch_vit<64>(va, plan == nullptr, sm); break;
+    case 128: e = launch_vit<128>(va, plan == nullptr, sm); break;
+    default: e = launch_vit<256>(va, plan == nullptr, sm); break;
   }
   return e == hipSuccess ? HMM355_OK : (int)e;
 }
@@ -178,16 +182,8 @@ HMM355_API int hmm355_viterbi_plan_ex_f32(const float* obs, int obs_mode, const 
                                           const void* plan, unsigned flags, int B, int T, int N, int64_t* states,
                                           float* log_delta, float* final_score, void* workspace,
                                           size_t workspace_bytes, void* stream) {
-  return viterbi_run(obs, obs_mode, log_P, init, plan, flags, B, T, N, 0, T, states, log_delta, final_score,
-                     workspace, workspace_bytes, stream);
-}
-
-HMM355_API int hmm355_viterbi_part_f32(const float* obs, int obs_mode, const float* log_P, const float* init,
-                                       const void* plan, unsigned flags, int B, int T, int N, int q_lo, int q_hi,
-                                       int64_t* states, float* log_delta, float* final_score, void* workspace,
-                                       size_t workspace_bytes, void* stream) {
-  return viterbi_run(obs, obs_mode, log_P, init, plan, flags, B, T, N, q_lo, q_hi, states, log_delta, final_score,
-                     workspace, workspace_bytes, stream);
+  return viterbi_run(obs, obs_mode, log_P, init, plan, flags, B, T, N, states, log_delta, final_score, workspace,
+                     workspace_bytes, stream);
 }
 
 HMM355_API int hmm355_viterbi_plan_f32(const float* obs, int obs_mode, const float* log_P, const float* init,

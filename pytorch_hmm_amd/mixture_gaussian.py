@@ -157,14 +157,15 @@ class MixtureGaussianHMMLayer(nn.Module):
         matrix is measured once, not on every forward."""
         src = self.transition_logits if self.learnable_transitions else self.transition_matrix
         c = self.__dict__.get("_plan_cache")
-        if (c is not None and c[0] is src and c[1] == src._version and c[2] == log_transitions.device
+        if (c is not None and c[0] is src and c[1] == (src._version, src.data_ptr()) and c[2] == log_transitions.device
                 and c[3] == tuple(log_transitions.shape)):
             return c[4]
         # (a trainable matrix under autograd changes every step: skip the plan's host read, so
         # a training forward makes no synchronous device -> host copy; ops.make_plan)
         plan = ops.make_plan(log_transitions.detach(),
                              read_banded=not (torch.is_grad_enabled() and src.requires_grad))
-        self.__dict__["_plan_cache"] = (src, src._version, log_transitions.device, tuple(log_transitions.shape), plan)
+        self.__dict__["_plan_cache"] = (src, (src._version, src.data_ptr()), log_transitions.device,
+                                        tuple(log_transitions.shape), plan)
         return plan
 
     def _viterbi_decode(self, obs_log_probs: torch.Tensor,
@@ -185,10 +186,13 @@ class MixtureGaussianHMMLayer(nn.Module):
         the reference's expressions (mixture_gaussian.py:130-135, :141-155, :305) and cached while
         the parameters they come from are unchanged (same tensors, same versions): a decode of a
         fixed model launches no per-call softmax / log / clamp kernels (~10 small launches,
-        ~80 us of serial latency before the scorer at config 3, profiles/r5m_c3)."""
+        ~80 us of serial latency before the scorer at config 3, profiles/r5m_c3).  Writes through
+        ``.data`` (``p.data.copy_(...)``, ``p.data -= ...``) bump no version counter: call
+        refresh_tables() after them (load_state_dict, train()/eval(), in-place ops on the
+        parameters and replacing them are all seen)."""
         src = self.transition_logits if self.learnable_transitions else self.transition_matrix
         wl = self.mixture_weights_logits
-        key = (id(src), src._version, id(wl), wl._version, str(device))
+        key = (id(src), src._version, src.data_ptr(), id(wl), wl._version, wl.data_ptr(), str(device))
         c = self.__dict__.get("_inf_cache")
         if c is not None and c[0] == key and c[1] is src and c[2] is wl:
             return c[3]
@@ -200,20 +204,33 @@ class MixtureGaussianHMMLayer(nn.Module):
         self.__dict__["_inf_cache"] = (key, src, wl, tabs)
         return tabs
 
+    def refresh_tables(self):
+        """Drop the cached inference tables and transition plans (after writes through ``.data``,
+        which the cache cannot see); the next forward re-forms them."""
+        self.__dict__.pop("_inf_cache", None)
+        self.__dict__.pop("_plan_cache", None)
+
+    def train(self, mode: bool = True):
+        self.refresh_tables()
+        return super().train(mode)
+
+    def _load_from_state_dict(self, *args, **kwargs):
+        self.refresh_tables()
+        return super()._load_from_state_dict(*args, **kwargs)
+
     def forward(self, observations: torch.Tensor,
                 return_log_probs: bool = False) -> Tuple[torch.Tensor, Optional[torch.Tensor]]:
         if self.covariance_type != "full" and not needs_grad(observations, *self.parameters()):
-            # inference: the emission scorer runs beside the decode (ops.gmm_viterbi: time slices
-            # of the scores on a side stream, the chain on the slices already scored); the same
-            # bits as get_observation_log_probs followed by _viterbi_decode
+            # inference: the cached tables (_inference_tables), the GMM scorer, then the decode;
+            # the same bits as get_observation_log_probs followed by _viterbi_decode
             B, T, _ = observations.shape
             if T > self.max_sequence_length:
                 warnings.warn(f"Sequence length {T} exceeds recommended maximum "
                               f"{self.max_sequence_length}. Consider chunked processing.")
             with torch.no_grad():
                 log_T, log_w, init, plan = self._inference_tables(observations.device)
-                _, states, _, scores = ops.gmm_viterbi(observations, self.means, self._component_log_vars(), log_w,
-                                                       1, log_T, init, plan)
+                lp = ops.gmm_diag_logprob(observations, self.means, self._component_log_vars(), log_w, 1)
+                states, _, scores = ops.viterbi(lp, log_T, init, ops.OBS_LOG, plan)
             return (states, scores) if return_log_probs else (states, None)
         log_transitions = self._safe_log(self.get_transition_matrix())
         obs_log_probs = self.get_observation_log_probs(observations)

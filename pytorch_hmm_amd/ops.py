@@ -16,8 +16,6 @@ shape-only fake implementations; their only real implementation is the HIP libra
 """
 from typing import Optional, Tuple
 
-import os
-
 import torch
 from torch import Tensor
 
@@ -27,9 +25,11 @@ OBS_PROB = nat.OBS_PROB
 OBS_LOG = nat.OBS_LOG
 FB_POSTERIOR = nat.FB_POSTERIOR
 FB_PAIR = nat.FB_PAIR
+FB_PLAN_BANDED = nat.FB_PLAN_BANDED
 VIT_PLAN_BANDED = nat.VIT_PLAN_BANDED
 VIT_PLAN_DENSE = nat.VIT_PLAN_DENSE
-_VIT_FOLLOW_DEFAULT = "1"  # psi followers for dense plans (config 3: 65.2 -> 68.2 M frames/s)
+FORM_GENERAL = nat.FORM_GENERAL
+FORM_SERIAL_WALK = nat.FORM_SERIAL_WALK
 FB_FORWARD = nat.FB_FORWARD
 FB_BACKWARD = nat.FB_BACKWARD
 
@@ -45,9 +45,11 @@ def _workspace(nbytes, device):
 
 
 # ------------------------------------------------------------------ forward-backward
-def make_plan(log_P: Tensor, read_banded: bool = True) -> Tensor:
-    """Measure log_P's banded structure once (hmm355_plan_f32) into a device byte tensor that
-    forward_backward / viterbi accept as `plan` (valid while log_P is unchanged).
+def make_plan(log_P: Tensor, read_banded: bool = True, dense: bool = False) -> Tensor:
+    """Measure log_P's banded structure once (hmm355_plan_ex_f32) into a device byte tensor that
+    forward_backward / viterbi accept as `plan` (valid while log_P is unchanged).  dense=True
+    (HMM355_PLAN_DENSE) makes a plan that selects the dense chains whatever the structure (the
+    parity tests run both chain families on one matrix).
 
     The kernels read the structure from the plan on the device; the host only needs it to
     choose between launch shapes (the pair kernel, the psi followers), and reading it back is
@@ -62,7 +64,8 @@ def make_plan(log_P: Tensor, read_banded: bool = True) -> Tensor:
     L = nat.lib()
     plan = torch.empty(L.hmm355_plan_bytes(N), dtype=torch.uint8, device=log_P.device)
     with torch.cuda.device(log_P.device):
-        nat.check(L.hmm355_plan_f32(nat.ptr(log_P), N, nat.ptr(plan), nat.stream_of(log_P.device)))
+        nat.check(L.hmm355_plan_ex_f32(nat.ptr(log_P), N, nat.PLAN_DENSE if dense else 0, nat.ptr(plan),
+                                       nat.stream_of(log_P.device)))
         if not read_banded:
             plan._hmm355_banded = None
             return plan
@@ -76,11 +79,10 @@ def make_plan(log_P: Tensor, read_banded: bool = True) -> Tensor:
 
 
 def plan_info(plan: Optional[Tensor]) -> dict:
-    """Which chains a plan selects (band.h BandDesc: wc/wr window widths, Toeplitz windows);
-    with no plan or HMM355_DENSE=1 the dense chains run.  Reads a few ints back to the host."""
-    import os
-    if plan is None or os.environ.get("HMM355_DENSE", "") == "1":
-        return {"forward": "dense", "backward": "dense", "viterbi": "dense"}
+    """Which chains a plan selects (band.h BandDesc: wc/wr window widths, Toeplitz windows).
+    Reads a few ints back to the host."""
+    if plan is None:
+        return {"forward": "detected per call", "backward": "detected per call", "viterbi": "detected per call"}
     h = plan[: 4 * 7177].cpu().view(torch.int32).tolist()
     wc, wr = h[0], h[1]
     tcd0, tcw, trd0, trw = h[7172:7176]
@@ -102,10 +104,7 @@ def _use_pair(B: int, dev) -> bool:
     batch is larger than half the CUs: the two-kernel path then needs more CU-owning
     workgroups (2B) than the chip has and runs in two rounds, while the pair kernel needs B.
     Measured: B=32 two-kernel 0.24 ms vs pair 0.38 ms; B=256 FB op 0.90 vs 0.51
-    ms.  HMM355_PAIR=1 / 0 forces it on / off."""
-    env = os.environ.get("HMM355_PAIR")
-    if env in ("0", "1"):
-        return env == "1"
+    ms.  (forward_backward's `pair` argument overrides it.)"""
     key = str(dev)
     if key not in _CUS:
         _CUS[key] = torch.cuda.get_device_properties(dev).multi_processor_count
@@ -114,7 +113,11 @@ def _use_pair(B: int, dev) -> bool:
 
 @torch.library.custom_op("hmm355::forward_backward", mutates_args=())
 def forward_backward(obs: Tensor, log_P: Tensor, log_p0: Tensor, obs_mode: int,
-                     out_mask: int, plan: Optional[Tensor] = None) -> Tuple[Tensor, Tensor, Tensor, Tensor, Tensor]:
+                     out_mask: int, plan: Optional[Tensor] = None, pair: Optional[bool] = None,
+                     follow: Optional[bool] = None) -> Tuple[Tensor, Tensor, Tensor, Tensor, Tensor]:
+    """pair / follow (None = chosen from the batch and the plan): with a host-known banded plan,
+    `pair` runs both chains of a sequence in one workgroup (HMM355_FB_PAIR, large batches) and
+    otherwise `follow` forms the posterior inside the chains' launch (HMM355_FB_PLAN_BANDED)."""
     nat.require_gpu(obs, log_P, log_p0)
     obs, log_P, log_p0 = _f32c(obs), _f32c(log_P), _f32c(log_p0)
     B, T, N = obs.shape
@@ -129,8 +132,12 @@ def forward_backward(obs: Tensor, log_P: Tensor, log_p0: Tensor, obs_mode: int,
         return post, fwd, bwd, loglik, lik_ref
     nbytes = L.hmm355_fb_workspace_bytes(B, T, N)
     ws = _workspace(nbytes, dev)
-    if plan is not None and getattr(plan, "_hmm355_banded", False) is True and _use_pair(B, dev):
+    banded = plan is not None and getattr(plan, "_hmm355_banded", False) is True
+    use_pair = banded and (_use_pair(B, dev) if pair is None else pair)
+    if use_pair:
         out_mask |= FB_PAIR
+    elif banded and (out_mask & FB_POSTERIOR) and follow is not False:
+        out_mask |= FB_PLAN_BANDED
     with torch.cuda.device(dev):
         nat.check(L.hmm355_forward_backward_plan_f32(
             nat.ptr(obs), obs_mode, nat.ptr(log_P), nat.ptr(log_p0), nat.ptr(plan), None, B, T, N, out_mask,
@@ -142,7 +149,7 @@ def forward_backward(obs: Tensor, log_P: Tensor, log_p0: Tensor, obs_mode: int,
 
 
 @forward_backward.register_fake
-def _(obs, log_P, log_p0, obs_mode, out_mask, plan=None):
+def _(obs, log_P, log_p0, obs_mode, out_mask, plan=None, pair=None, follow=None):
     B, T, N = obs.shape
     mk = lambda bit: obs.new_empty((B, T, N) if out_mask & bit else _EMPTY)
     return mk(FB_POSTERIOR), mk(FB_FORWARD), mk(FB_BACKWARD), obs.new_empty(B), obs.new_empty(B)
@@ -151,7 +158,10 @@ def _(obs, log_P, log_p0, obs_mode, out_mask, plan=None):
 # ---------------------------------------------------------------------------- Viterbi
 @torch.library.custom_op("hmm355::viterbi", mutates_args=())
 def viterbi(obs: Tensor, log_P: Tensor, init: Tensor, obs_mode: int,
-            plan: Optional[Tensor] = None) -> Tuple[Tensor, Tensor, Tensor]:
+            plan: Optional[Tensor] = None, follow: Optional[bool] = None) -> Tuple[Tensor, Tensor, Tensor]:
+    """follow (None = on): with a plan, the work beside the chain inside its launch -- for a
+    host-known banded plan the log leaders and the decode follower (HMM355_VIT_PLAN_BANDED), for a
+    dense one the psi followers (HMM355_VIT_PLAN_DENSE)."""
     nat.require_gpu(obs, log_P, init)
     obs, log_P, init = _f32c(obs), _f32c(log_P), _f32c(init)
     B, T, N = obs.shape
@@ -163,19 +173,15 @@ def viterbi(obs: Tensor, log_P: Tensor, init: Tensor, obs_mode: int,
     if B == 0:
         return states, delta, final
     ws = _workspace(L.hmm355_viterbi_workspace_bytes(B, T, N), dev)
-    # HMM355_VIT_TAIL=1 with a banded plan: the chain kernel finishes the decode itself (one
-    # launch instead of three).  Off by default: measured 10 us slower per op at the north-star
-    # shape (profiles/r4b_*), its composer and in-kernel backtrace cost more
-    # than the two launches they replace.
-    flags = VIT_PLAN_BANDED if (plan is not None and getattr(plan, "_hmm355_banded", False) is True
-                                and os.environ.get("HMM355_VIT_TAIL", "0") == "1") else 0
-    # a dense plan: the argmax pointers computed beside the chain, on the CUs it leaves
-    # (HMM355_VIT_FOLLOW; _VIT_FOLLOW_DEFAULT: DESIGN.md round 4 item 15)
-    # (a plan whose structure the host never read, make_plan(read_banded=False), asks for them
-    # too: on a banded matrix they return at once)
-    if (plan is not None and getattr(plan, "_hmm355_banded", True) is not True
-            and os.environ.get("HMM355_VIT_FOLLOW", _VIT_FOLLOW_DEFAULT) != "0"):
-        flags |= VIT_PLAN_DENSE
+    flags = 0
+    if plan is not None and follow is not False:
+        if getattr(plan, "_hmm355_banded", False) is True:
+            flags = VIT_PLAN_BANDED   # the decode beside the banded chain (csrc/follow.h)
+        else:
+            # a dense plan: the argmax pointers computed beside the chain, on the CUs it leaves
+            # (a plan whose structure the host never read,
+            # make_plan(read_banded=False), asks for them too: on a banded matrix they return at once)
+            flags = VIT_PLAN_DENSE
     with torch.cuda.device(dev):
         nat.check(L.hmm355_viterbi_plan_ex_f32(
             nat.ptr(obs), obs_mode, nat.ptr(log_P), nat.ptr(init), nat.ptr(plan), flags, B, T, N,
@@ -184,7 +190,7 @@ def viterbi(obs: Tensor, log_P: Tensor, init: Tensor, obs_mode: int,
 
 
 @viterbi.register_fake
-def _(obs, log_P, init, obs_mode, plan=None):
+def _(obs, log_P, init, obs_mode, plan=None, follow=None):
     B, T, N = obs.shape
     return (obs.new_empty((B, T), dtype=torch.int64), obs.new_empty((B, T, N)), obs.new_empty(B))
 
@@ -215,101 +221,10 @@ def _(x, means, log_vars, log_w, mix_lse):
     return x.new_empty((x.shape[0], x.shape[1], means.shape[0]))
 
 
-# ------------------------------------------- GMM emission feeding a dense Viterbi chain
-_SIDE = {}
-
-
-def _side_stream(dev):
-    """One side stream per device (the emission producer of gmm_viterbi)."""
-    key = str(dev)
-    if key not in _SIDE:
-        _SIDE[key] = torch.cuda.Stream(dev)
-    return _SIDE[key]
-
-
-def time_parts(T: int) -> list:
-    """Part boundaries [0, t1, t2, T] of gmm_viterbi (multiples of 64): a short first part so
-    the chain starts early, then parts that grow so the scorer, on the CUs the chain leaves,
-    stays ahead of the chain (config 3: a 2000-step chain ~0.6 ms, the scorer ~0.3 ms alone).
-    Few parts: each is a launch with its own prologue (profiles/r5m_*: five parts cost more than
-    they hid)."""
-    t1, t2 = (T * 16 // 100) // 64 * 64, (T * 48 // 100) // 64 * 64
-    if T < 640 or t1 < 64:
-        return [0, T]
-    return [0, t1, t2, T]
-
-
-def gmm_viterbi(x: Tensor, means: Tensor, log_vars: Tensor, log_w: Tensor, mix_lse: int, log_T: Tensor,
-                init: Tensor, plan: Optional[Tensor]) -> Tuple[Tensor, Tensor, Tensor, Tensor]:
-    """gmm_diag_logprob + viterbi (OBS_LOG) of the same batch with the two overlapped
-    (MixtureGaussianHMMLayer.forward, mixture_gaussian.py:340-365): the scorer fills time slices
-    of the log-probabilities on a side stream (hmm355_gmm_diag_logprob_slice_f32) while the
-    chain decodes the slices already scored (hmm355_viterbi_part_f32, one launch per part, each
-    waiting only for its own slice), so the scorer runs beside the chain instead of before it.
-    Bit-identical to the two calls in sequence.  Needs a host-known dense plan, N <= 128 and
-    C in {1, 2, 4}; otherwise it is the two calls in sequence.
-
-    OFF by default (HMM355_GMM_VIT_PARTS=1 turns it on): measured at config 3 it is slower than
-    the two calls in sequence (0.98 vs 0.84 ms per step, profiles/r5n_c3, r5o_c3).  The chain
-    launches of the parts need whole CUs (all of a CU's LDS) and are dispatched only as the
-    scorer's workgroups drain, and with the fp64 scorer busy on the rest of the chip the clock
-    drops: the chain steps ran at 0.33-0.49 us instead of 0.30.
-    Returns (log_probs (B,T,S), states (B,T), log_delta (B,T,S), final_score (B))."""
-    nat.require_gpu(x, means, log_vars, log_w, log_T, init)
-    x, means, log_vars, log_w = _f32c(x), _f32c(means), _f32c(log_vars), _f32c(log_w)
-    log_T, init = _f32c(log_T), _f32c(init)
-    B, T, D = x.shape
-    S, C, _ = means.shape
-    dev = x.device
-    parts = time_parts(T)
-    dense = plan is not None and getattr(plan, "_hmm355_banded", True) is False
-    if (not dense or len(parts) <= 2 or S > 128 or C not in (1, 2, 4) or B == 0
-            or os.environ.get("HMM355_GMM_VIT_PARTS", "0") != "1"):
-        lp = gmm_diag_logprob(x, means, log_vars, log_w, mix_lse)
-        states, delta, final = viterbi(lp, log_T, init, OBS_LOG, plan)
-        return lp, states, delta, final
-    L = nat.lib()
-    lp = torch.empty((B, T, S), device=dev)
-    states = torch.empty((B, T), dtype=torch.int64, device=dev)
-    delta = torch.empty((B, T, S), device=dev)
-    final = torch.empty(B, device=dev)
-    ws_g = _workspace(L.hmm355_gmm_workspace_bytes(B, T, D, S, C), dev)
-    ws_v = _workspace(L.hmm355_viterbi_workspace_bytes(B, T, S), dev)
-    main = torch.cuda.current_stream(dev)
-    side = _side_stream(dev)
-    side.wait_stream(main)
-    flags = VIT_PLAN_DENSE  # (parts need the host's dense word; the psi followers ride on it)
-    evs = []
-    with torch.cuda.device(dev):
-        with torch.cuda.stream(side):
-            sside = ctypes_stream(side)
-            for t0, t1 in zip(parts[:-1], parts[1:]):
-                nat.check(L.hmm355_gmm_diag_logprob_slice_f32(
-                    nat.ptr(x), nat.ptr(means), nat.ptr(log_vars), nat.ptr(log_w), B, T, D, S, C, mix_lse,
-                    t0, t1 - t0, nat.ptr(lp), nat.ptr(ws_g), ws_g.numel(), sside))
-                ev = torch.cuda.Event()
-                ev.record(side)
-                evs.append(ev)
-        smain = ctypes_stream(main)
-        for (t0, t1), ev in zip(zip(parts[:-1], parts[1:]), evs):
-            main.wait_event(ev)
-            nat.check(L.hmm355_viterbi_part_f32(
-                nat.ptr(lp), OBS_LOG, nat.ptr(log_T), nat.ptr(init), nat.ptr(plan), flags, B, T, S, t0, t1,
-                nat.ptr(states), nat.ptr(delta), nat.ptr(final), nat.ptr(ws_v), ws_v.numel(), smain))
-    # tensors the side stream used stay allocated until its work is done
-    for t_ in (x, means, log_vars, log_w, lp, ws_g):
-        t_.record_stream(side)
-    return lp, states, delta, final
-
-
-def ctypes_stream(s):
-    import ctypes
-    return ctypes.c_void_p(s.cuda_stream)
-
-
 # ------------------------------------------------------------------------------- HSMM
 @torch.library.custom_op("hmm355::hsmm_viterbi", mutates_args=())
-def hsmm_viterbi(lp: Tensor, dur_lp: Tensor, log_T: Tensor) -> Tuple[Tensor, Tensor]:
+def hsmm_viterbi(lp: Tensor, dur_lp: Tensor, log_T: Tensor, flags: int = 0) -> Tuple[Tensor, Tensor]:
+    """flags: kernel-form flags (FORM_GENERAL, FORM_SERIAL_WALK; identical results)."""
     nat.require_gpu(lp, dur_lp, log_T)
     lp, dur_lp, log_T = _f32c(lp), _f32c(dur_lp), _f32c(log_T)
     B, T, S = lp.shape
@@ -323,13 +238,14 @@ def hsmm_viterbi(lp: Tensor, dur_lp: Tensor, log_T: Tensor) -> Tuple[Tensor, Ten
     # The general form (S or Dmax beyond the register-slot kernels) keeps a (B,T,S,Dmax+1) fp32
     # table: checked against the device's free memory up front, and decoded in batch slices
     # that fit when the whole batch does not (sequences are independent).
-    Bc = _ws_batch(L.hmm355_hsmm_workspace_bytes, B, T, S, Dm, dev, "HSMM decode")
-    ws = _workspace(L.hmm355_hsmm_workspace_bytes(Bc, T, S, Dm), dev)
+    wsb = lambda b_, t_, s_, d_: L.hmm355_hsmm_workspace_bytes_ex(b_, t_, s_, d_, flags)
+    Bc = _ws_batch(wsb, B, T, S, Dm, dev, "HSMM decode")
+    ws = _workspace(wsb(Bc, T, S, Dm), dev)
     with torch.cuda.device(dev):
         for b0 in range(0, B, Bc):
             nb = min(Bc, B - b0)
-            nat.check(L.hmm355_hsmm_viterbi_f32(
-                nat.ptr(lp[b0:b0 + nb]), nat.ptr(dur_lp), nat.ptr(log_T), nb, T, S, Dm,
+            nat.check(L.hmm355_hsmm_viterbi_ex_f32(
+                nat.ptr(lp[b0:b0 + nb]), nat.ptr(dur_lp), nat.ptr(log_T), nb, T, S, Dm, flags,
                 nat.ptr(states[b0:b0 + nb]), nat.ptr(scores[b0:b0 + nb]), nat.ptr(ws), ws.numel(),
                 nat.stream_of(dev)))
     return states, scores
@@ -356,7 +272,7 @@ def _ws_batch(ws_bytes, B, T, S, Dm, dev, what):
 
 
 @hsmm_viterbi.register_fake
-def _(lp, dur_lp, log_T):
+def _(lp, dur_lp, log_T, flags=0):
     B, T, S = lp.shape
     return lp.new_empty((B, T), dtype=torch.int64), lp.new_empty(B)
 
@@ -417,47 +333,6 @@ def _(log_obs, log_A, log_p0, out_mask):
     B, T, N = log_obs.shape
     mk = lambda bit: log_obs.new_empty((B, T, N) if out_mask & bit else _EMPTY)
     return mk(FB_POSTERIOR), mk(FB_FORWARD), mk(FB_BACKWARD), log_obs.new_empty(B), log_obs.new_empty(B)
-
-
-@torch.library.custom_op("hmm355::tv_fb_viterbi", mutates_args=())
-def tv_fb_viterbi(log_obs: Tensor, log_A: Tensor, log_p0: Tensor, init: Tensor,
-                  out_mask: int) -> Tuple[Tensor, Tensor, Tensor, Tensor, Tensor, Tensor, Tensor]:
-    """tv_forward_backward and tv_viterbi of the same model in one call
-    (hmm355_tv_fb_viterbi_f32): the alpha and Viterbi recursions share one stream of log_A.
-    Returns (posterior, forward, backward, loglik, lik_ref, states, log_delta)."""
-    nat.require_gpu(log_obs, log_A, log_p0, init)
-    log_obs, log_p0, init = _f32c(log_obs), _f32c(log_p0), _f32c(init)
-    B, T, N = log_obs.shape
-    dev = log_obs.device
-    L = nat.lib()
-    post = torch.empty((B, T, N) if out_mask & FB_POSTERIOR else _EMPTY, device=dev)
-    fwd = torch.empty((B, T, N) if out_mask & FB_FORWARD else _EMPTY, device=dev)
-    bwd = torch.empty((B, T, N) if out_mask & FB_BACKWARD else _EMPTY, device=dev)
-    loglik = torch.empty(B, device=dev)
-    lik_ref = torch.empty(B, device=dev)
-    states = torch.empty((B, T), dtype=torch.int64, device=dev)
-    delta = torch.empty((B, T, N), device=dev)
-    if B == 0:
-        return post, fwd, bwd, loglik, lik_ref, states, delta
-    A, sb, st = _tv_matrix(log_A, B, T, N)
-    ws = _workspace(L.hmm355_tv_fb_viterbi_workspace_bytes(B, T, N), dev)
-    with torch.cuda.device(dev):
-        nat.check(L.hmm355_tv_fb_viterbi_f32(
-            nat.ptr(log_obs), nat.ptr(A), sb, st, nat.ptr(log_p0), nat.ptr(init), B, T, N, out_mask,
-            nat.ptr(post) if out_mask & FB_POSTERIOR else None,
-            nat.ptr(fwd) if out_mask & FB_FORWARD else None,
-            nat.ptr(bwd) if out_mask & FB_BACKWARD else None,
-            nat.ptr(loglik), nat.ptr(lik_ref), nat.ptr(states), nat.ptr(delta), nat.ptr(ws), ws.numel(),
-            nat.stream_of(dev)))
-    return post, fwd, bwd, loglik, lik_ref, states, delta
-
-
-@tv_fb_viterbi.register_fake
-def _(log_obs, log_A, log_p0, init, out_mask):
-    B, T, N = log_obs.shape
-    mk = lambda bit: log_obs.new_empty((B, T, N) if out_mask & bit else _EMPTY)
-    return (mk(FB_POSTERIOR), mk(FB_FORWARD), mk(FB_BACKWARD), log_obs.new_empty(B), log_obs.new_empty(B),
-            log_obs.new_empty((B, T), dtype=torch.int64), log_obs.new_empty((B, T, N)))
 
 
 @torch.library.custom_op("hmm355::tv_viterbi", mutates_args=())
@@ -525,9 +400,9 @@ def _smk_args(quad, seg_const, log_init, log_T, dur_lp):
 
 @torch.library.custom_op("hmm355::semimarkov_viterbi", mutates_args=())
 def semimarkov_viterbi(quad: Tensor, seg_const: Optional[Tensor], log_init: Tensor, log_T: Tensor,
-                       dur_lp: Tensor) -> Tuple[Tensor, Tensor, Tensor, Tensor]:
+                       dur_lp: Tensor, flags: int = 0) -> Tuple[Tensor, Tensor, Tensor, Tensor]:
     """-> seg_states (B,T) int64, seg_durs (B,T) int64 (right-aligned), seg_count (B) int32,
-    scores (B)."""
+    scores (B).  flags: FORM_GENERAL forces the general form (identical results)."""
     quad, seg_const, log_init, log_T, dur_lp, B, T, S, Dm = _smk_args(quad, seg_const, log_init, log_T, dur_lp)
     dev = quad.device
     seg_s = torch.empty((B, T), dtype=torch.int64, device=dev)
@@ -537,20 +412,21 @@ def semimarkov_viterbi(quad: Tensor, seg_const: Optional[Tensor], log_init: Tens
     if B == 0:
         return seg_s, seg_d, cnt, scores
     L = nat.lib()
-    Bc = _ws_batch(L.hmm355_semimarkov_workspace_bytes, B, T, S, Dm, dev, "semi-Markov decode")
-    ws = _workspace(L.hmm355_semimarkov_workspace_bytes(Bc, T, S, Dm), dev)
+    wsb = lambda b_, t_, s_, d_: L.hmm355_semimarkov_workspace_bytes_ex(b_, t_, s_, d_, flags)
+    Bc = _ws_batch(wsb, B, T, S, Dm, dev, "semi-Markov decode")
+    ws = _workspace(wsb(Bc, T, S, Dm), dev)
     with torch.cuda.device(dev):
         for b0 in range(0, B, Bc):
             nb = min(Bc, B - b0)
-            nat.check(L.hmm355_semimarkov_viterbi_f32(
+            nat.check(L.hmm355_semimarkov_viterbi_ex_f32(
                 nat.ptr(quad[b0:b0 + nb]), nat.ptr(seg_const), nat.ptr(log_init), nat.ptr(log_T), nat.ptr(dur_lp),
-                nb, T, S, Dm, nat.ptr(seg_s[b0:b0 + nb]), nat.ptr(seg_d[b0:b0 + nb]), nat.ptr(cnt[b0:b0 + nb]),
+                nb, T, S, Dm, flags, nat.ptr(seg_s[b0:b0 + nb]), nat.ptr(seg_d[b0:b0 + nb]), nat.ptr(cnt[b0:b0 + nb]),
                 nat.ptr(scores[b0:b0 + nb]), nat.ptr(ws), ws.numel(), nat.stream_of(dev)))
     return seg_s, seg_d, cnt, scores
 
 
 @semimarkov_viterbi.register_fake
-def _(quad, seg_const, log_init, log_T, dur_lp):
+def _(quad, seg_const, log_init, log_T, dur_lp, flags=0):
     B, T, _ = quad.shape
     return (quad.new_empty((B, T), dtype=torch.int64), quad.new_empty((B, T), dtype=torch.int64),
             quad.new_empty(B, dtype=torch.int32), quad.new_empty(B))
@@ -558,7 +434,7 @@ def _(quad, seg_const, log_init, log_T, dur_lp):
 
 @torch.library.custom_op("hmm355::semimarkov_forward", mutates_args=())
 def semimarkov_forward(quad: Tensor, seg_const: Optional[Tensor], log_init: Tensor, log_T: Tensor,
-                       dur_lp: Tensor, want_alpha: bool) -> Tuple[Tensor, Tensor]:
+                       dur_lp: Tensor, want_alpha: bool, flags: int = 0) -> Tuple[Tensor, Tensor]:
     """-> log_prob (B), log_alpha (B,T,S,Dmax) (empty (0,) unless want_alpha)."""
     quad, seg_const, log_init, log_T, dur_lp, B, T, S, Dm = _smk_args(quad, seg_const, log_init, log_T, dur_lp)
     dev = quad.device
@@ -567,20 +443,21 @@ def semimarkov_forward(quad: Tensor, seg_const: Optional[Tensor], log_init: Tens
     if B == 0:
         return lp, alpha
     L = nat.lib()
-    Bc = _ws_batch(L.hmm355_semimarkov_workspace_bytes, B, T, S, Dm, dev, "semi-Markov forward")
-    ws = _workspace(L.hmm355_semimarkov_workspace_bytes(Bc, T, S, Dm), dev)
+    wsb = lambda b_, t_, s_, d_: L.hmm355_semimarkov_workspace_bytes_ex(b_, t_, s_, d_, flags)
+    Bc = _ws_batch(wsb, B, T, S, Dm, dev, "semi-Markov forward")
+    ws = _workspace(wsb(Bc, T, S, Dm), dev)
     with torch.cuda.device(dev):
         for b0 in range(0, B, Bc):
             nb = min(Bc, B - b0)
-            nat.check(L.hmm355_semimarkov_forward_f32(
+            nat.check(L.hmm355_semimarkov_forward_ex_f32(
                 nat.ptr(quad[b0:b0 + nb]), nat.ptr(seg_const), nat.ptr(log_init), nat.ptr(log_T), nat.ptr(dur_lp),
-                nb, T, S, Dm, nat.ptr(alpha[b0:b0 + nb]) if want_alpha else None, nat.ptr(lp[b0:b0 + nb]),
+                nb, T, S, Dm, flags, nat.ptr(alpha[b0:b0 + nb]) if want_alpha else None, nat.ptr(lp[b0:b0 + nb]),
                 nat.ptr(ws), ws.numel(), nat.stream_of(dev)))
     return lp, alpha
 
 
 @semimarkov_forward.register_fake
-def _(quad, seg_const, log_init, log_T, dur_lp, want_alpha):
+def _(quad, seg_const, log_init, log_T, dur_lp, want_alpha, flags=0):
     B, T, S = quad.shape
     return quad.new_empty(B), quad.new_empty((B, T, S, dur_lp.shape[1]) if want_alpha else (0,))
 

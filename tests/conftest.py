@@ -25,6 +25,14 @@ def gold():
     return golden
 
 
+def force_dense_plans(monkeypatch):
+    """Every transition plan made from here on selects the dense chains (HMM355_PLAN_DENSE):
+    the layers and HMMPyTorch build their plans through ops.make_plan."""
+    from pytorch_hmm_amd import ops
+    orig = ops.make_plan
+    monkeypatch.setattr(ops, "make_plan", lambda log_P, read_banded=True, dense=False: orig(log_P, read_banded, True))
+
+
 # -- host numerics fingerprint ------------------------------------------------------------
 # The fixtures under tests/golden/ were produced by the reference on torch-CPU in the build
 # container. torch-CPU's vector exp/log/softmax and its GEMMs pick kernels by host ISA, so the

@@ -68,9 +68,7 @@ def test_loglik_gradients(kind, B, T, N, mat):
 
 
 @pytest.mark.parametrize("dense", [False, True])
-def test_gradients_dense_and_banded_agree(dense, monkeypatch):
-    if dense:
-        monkeypatch.setenv("HMM355_DENSE", "1")
+def test_gradients_dense_and_banded_agree(dense):
     rng = np.random.default_rng(3)
     B, T, N = 2, 50, 64
     lP, lp0 = O.hmm_params(O.left_to_right_matrix(N, 0.7))
@@ -81,7 +79,8 @@ def test_gradients_dense_and_banded_agree(dense, monkeypatch):
     p0 = lp0.to(DEV).requires_grad_(True)
     from pytorch_hmm_amd.autograd import SequenceLogLik
     from pytorch_hmm_amd import ops
-    (SequenceLogLik.apply(o, P_, p0, ops.OBS_PROB, "exact") * w.float().to(DEV)).sum().backward()
+    plan = ops.make_plan(P_.detach(), dense=dense)   # dense: HMM355_PLAN_DENSE on a banded matrix
+    (SequenceLogLik.apply(o, P_, p0, ops.OBS_PROB, "exact", plan) * w.float().to(DEV)).sum().backward()
     close(o.grad.cpu(), g_obs)
     close(P_.grad.cpu(), g_lP)
 

@@ -3,7 +3,7 @@ oracle and against the dense chains on the same inputs.
 
 Contracts: Viterbi states and trellis bit-identical to the C oracle (the decomposition is an
 exact reorganisation of the max); forward-backward within the dense path's tolerances.
-HMM355_DENSE=1 forces the dense chains (read per call by the C ABI)."""
+A plan made with HMM355_PLAN_DENSE (ops.make_plan(..., dense=True)) forces the dense chains."""
 import os
 
 import numpy as np
@@ -25,11 +25,9 @@ def ops():
     return o
 
 
-def dense(flag):
-    if flag:
-        os.environ["HMM355_DENSE"] = "1"
-    else:
-        os.environ.pop("HMM355_DENSE", None)
+def dense_plan(lP, flag):
+    """None (the chains detect the structure per call) or a plan that forces the dense chains"""
+    return ops().make_plan(lP, dense=True) if flag else None
 
 
 def banded_matrix(N, kind, rng):
@@ -45,12 +43,6 @@ def banded_matrix(N, kind, rng):
     return P
 
 
-@pytest.fixture(autouse=True)
-def _restore_env():
-    yield
-    os.environ.pop("HMM355_DENSE", None)
-
-
 @pytest.mark.parametrize("kind", ["l2r", "left_to_right_skip", "circular", "ergodic", "band5"])
 @pytest.mark.parametrize("B,T,N", [(2, 300, 128), (3, 77, 40), (1, 50, 256), (2, 129, 64)])
 def test_banded_viterbi_bitexact(kind, B, T, N):
@@ -61,8 +53,7 @@ def test_banded_viterbi_bitexact(kind, B, T, N):
     cs, cd, _ = O.c_viterbi(lo, lP.numpy(), lp0.numpy())
     o = ops()
     for d in (False, True):
-        dense(d)
-        states, delta, final = o.viterbi(t(lo), t(lP), t(lp0), o.OBS_LOG)
+        states, delta, final = o.viterbi(t(lo), t(lP), t(lp0), o.OBS_LOG, dense_plan(t(lP), d))
         assert np.array_equal(states.cpu().numpy(), cs), f"dense={d}"
         assert np.array_equal(delta.cpu().numpy(), cd), f"dense={d}"
 
@@ -114,9 +105,9 @@ def test_banded_fb_vs_fp64(kind, B, T, N):
     o = ops()
     outs = {}
     for d in (False, True):
-        dense(d)
         post, fwd, bwd, loglik, lik_ref = o.forward_backward(t(obs), t(lP), t(lp0), o.OBS_PROB,
-                                                             o.FB_POSTERIOR | o.FB_FORWARD | o.FB_BACKWARD)
+                                                             o.FB_POSTERIOR | o.FB_FORWARD | o.FB_BACKWARD,
+                                                             dense_plan(t(lP), d))
         np.testing.assert_allclose(post.cpu().numpy(), post64, atol=2e-5)
         np.testing.assert_allclose(loglik.cpu().numpy(), ll64, rtol=2e-6)
         outs[d] = (fwd.cpu().numpy(), bwd.cpu().numpy(), lik_ref.cpu().numpy())
@@ -127,7 +118,7 @@ def test_banded_fb_vs_fp64(kind, B, T, N):
 
 def test_dense_matrix_stays_dense_and_exact():
     """A random dense matrix has no band: the decomposition must not engage (results
-    identical with and without HMM355_DENSE).  (The factory's 'ergodic' matrix IS banded in
+    identical with and without a dense plan).  (The factory's 'ergodic' matrix IS banded in
     this sense — a constant off-diagonal floor plus the diagonal, W = 1.)"""
     rng = np.random.default_rng(3)
     N, B, T = 128, 2, 100
@@ -136,6 +127,5 @@ def test_dense_matrix_stays_dense_and_exact():
     o = ops()
     r = {}
     for d in (False, True):
-        dense(d)
-        r[d] = o.viterbi(t(lo), t(lP), t(lp0), o.OBS_LOG)[1].cpu().numpy()
+        r[d] = o.viterbi(t(lo), t(lP), t(lp0), o.OBS_LOG, dense_plan(t(lP), d))[1].cpu().numpy()
     assert np.array_equal(r[False], r[True])

@@ -1,5 +1,5 @@
 """GPU: forward-backward with both chains of a sequence in one workgroup (csrc/fbpair.h,
-HMM355_FB_PAIR) against the two-kernel path (fb_recur + fb_posterior) on the same inputs.
+HMM355_FB_PAIR, forced with pair=True) against the two-kernel path (fb_recur + fb_posterior) on the same inputs.
 
 Both paths run the same chain code, so the scaled rows and log-scales are the same bits; the
 pair kernel forms forward / backward / loglik / lik_ref from them with the same formulas
@@ -18,11 +18,6 @@ from oracle import hmm_oracle as O
 
 pytestmark = pytest.mark.gpu
 DEV = "cuda"
-
-
-@pytest.fixture(autouse=True)
-def _pair_on(monkeypatch):
-    monkeypatch.setenv("HMM355_PAIR", "1")  # the pair kernel is opt-in (ops.forward_backward)
 
 
 def ops():
@@ -48,7 +43,7 @@ def run_both(obs, lP, lp0, mode, mask):
     o = ops()
     plan = o.make_plan(lP)
     plain = plan.clone()  # no banded attribute: the two-kernel path
-    a = o.forward_backward(obs, lP, lp0, mode, mask, plan)
+    a = o.forward_backward(obs, lP, lp0, mode, mask, plan, pair=True)
     b = o.forward_backward(obs, lP, lp0, mode, mask, plain)
     return plan, a, b
 
@@ -122,6 +117,6 @@ def test_pair_wrong_hint_falls_back_to_dense():
     assert not plan._hmm355_banded
     wrong = plan.clone()
     wrong._hmm355_banded = True  # the C ABI then runs the pair kernel, which finds dense chains
-    a = o.forward_backward(obs, lP.to(DEV), lp0.to(DEV), o.OBS_PROB, 7, wrong)
+    a = o.forward_backward(obs, lP.to(DEV), lp0.to(DEV), o.OBS_PROB, 7, wrong, pair=True)
     b = o.forward_backward(obs, lP.to(DEV), lp0.to(DEV), o.OBS_PROB, 7, plan)
     check(a, b, 7)

@@ -6,7 +6,7 @@ forward-backward, :162-178 Viterbi) on machine-independent PCG64 inputs that are
 here bit-for-bit (input_sha256 checked).  tests/golden/fullsize_mixture.npz does the same for
 BASELINE config 3 (MixtureGaussianHMMLayer(128, 80, num_components=4), mixture_gaussian.py:157-214,
 290-338).  Both ops run through the bench's path (HMMPyTorch -> transition plan -> ops), once on
-the banded chains and once with HMM355_DENSE=1 (the dense chains).
+the banded chains and once with dense plans (HMM355_PLAN_DENSE: the dense chains).
 
 Tolerances (north_star: "within 1e-4 on log-likelihoods, bit-exact on Viterbi state paths"):
   * Viterbi states and the final trellis row: bit-exact vs the reference.
@@ -23,17 +23,11 @@ import numpy as np
 import pytest
 import torch
 
-from conftest import golden
+from conftest import force_dense_plans, golden
 from oracle import hmm_oracle as O
 
 pytestmark = pytest.mark.gpu
 DEV = "cuda"
-
-
-@pytest.fixture(autouse=True)
-def _restore_env():
-    yield
-    os.environ.pop("HMM355_DENSE", None)
 
 
 @pytest.fixture(scope="module")
@@ -51,11 +45,11 @@ def ns():
 
 @pytest.mark.parametrize("dense", [False, True], ids=["banded", "dense"])
 @torch.no_grad()
-def test_north_star_shape_vs_reference(ns, dense):
+def test_north_star_shape_vs_reference(ns, dense, monkeypatch):
     import pytorch_hmm_amd as ph
     g, obs, lo_cr, post64, ll64, cs, cd = ns
     if dense:
-        os.environ["HMM355_DENSE"] = "1"
+        force_dense_plans(monkeypatch)
     N = obs.shape[-1]
     hmm = ph.HMMPyTorch(ph.create_left_to_right_matrix(N, 0.7))
     # parameter bits are the reference's (hmm.py:39-55)
@@ -90,14 +84,14 @@ def test_north_star_shape_vs_reference(ns, dense):
 
 @pytest.mark.parametrize("dense", [False, True], ids=["banded", "dense"])
 @torch.no_grad()
-def test_north_star_ops_with_plan(ns, dense):
+def test_north_star_ops_with_plan(ns, dense, monkeypatch):
     """The exact calls bench.py times: ops.forward_backward / ops.viterbi with the cached plan
     (OBS_PROB, all three FB outputs)."""
     import pytorch_hmm_amd as ph
     from pytorch_hmm_amd import ops
     g, obs, lo_cr, post64, ll64, cs, cd = ns
     if dense:
-        os.environ["HMM355_DENSE"] = "1"
+        force_dense_plans(monkeypatch)
     hmm = ph.HMMPyTorch(ph.create_left_to_right_matrix(obs.shape[-1], 0.7))
     lP, lp0, plan = hmm._device_params(torch.device(DEV, 0))
     x = torch.from_numpy(obs).to(DEV)
@@ -121,13 +115,13 @@ def mix():
 
 
 @pytest.mark.parametrize("dense", [False, True], ids=["auto", "dense"])
-def test_config3_mixture_vs_reference(mix, dense):
+def test_config3_mixture_vs_reference(mix, dense, monkeypatch):
     """BASELINE config 3 at full size: GMM emission (rtol 2e-6 of the reference's rows), then the
     Viterbi states and final scores; the random learned matrix takes the dense chain either way."""
     import pytorch_hmm_amd as ph
     g, x = mix
     if dense:
-        os.environ["HMM355_DENSE"] = "1"
+        force_dense_plans(monkeypatch)
     B, T, D, S, C = (int(v) for v in g["shape"])
     m = ph.MixtureGaussianHMMLayer(S, D, num_components=C)
     with torch.no_grad():

@@ -145,8 +145,6 @@ def test_hsmm_layer_beyond_register_kernels_vs_c_oracle():
 def test_pair_kernel_b256_fullsize(monkeypatch):
     import pytorch_hmm_amd as ph
     from pytorch_hmm_amd import ops
-    monkeypatch.delenv("HMM355_PAIR", raising=False)
-    monkeypatch.delenv("HMM355_DENSE", raising=False)
     B, T, N = 256, 2000, 128
     hmm = ph.HMMPyTorch(ph.create_left_to_right_matrix(N, 0.7))
     dev = torch.device(DEV, 0)
@@ -175,6 +173,5 @@ def test_pair_kernel_b256_fullsize(monkeypatch):
     rs = post.sum(-1)
     assert float((rs - 1).abs().max()) < 1e-4 and bool(torch.isfinite(loglik).all())
     # and the two-kernel path gives the same posteriors on the whole batch
-    monkeypatch.setenv("HMM355_PAIR", "0")
-    p2 = ops.forward_backward(obs, lP, lp0, ops.OBS_PROB, 1, plan)[0]
+    p2 = ops.forward_backward(obs, lP, lp0, ops.OBS_PROB, 1, plan, pair=False)[0]
     assert float((p2 - post).abs().max()) < 1e-5

@@ -204,14 +204,11 @@ def test_hsmm_ties_vs_c_oracle(seed, T, S, Dm):
     assert np.array_equal(scores.cpu().numpy(), csc)
 
 
-# every kernel geometry (csrc/hsmm.hip hsmm_cfg): (8,16,64) Dmax <= 127, (4,16,128)
-# S <= 128 / Dmax <= 63; for S <= 64 / Dmax <= 63 the default 4-lane (4,16,64) form and
-# HMM355_HSMM_SUB=8 / =16's (8,8,64) and (16,4,64) ones
-@pytest.mark.parametrize("sub", ["4", "8", "16"])
+# every kernel geometry (csrc/hsmm.hip hsmm_cfg): (4,16,64) S <= 64 / Dmax <= 63, (8,16,64)
+# Dmax <= 71, (4,16,128) S <= 128 / Dmax <= 63, and the general form beyond
 @pytest.mark.parametrize("B,T,S,Dm", [(2, 150, 16, 12), (1, 300, 64, 40), (3, 70, 7, 63), (2, 260, 40, 100),
                                       (1, 200, 100, 50), (2, 180, 128, 63), (1, 90, 65, 63), (2, 130, 3, 127)])
-def test_hsmm_vs_c_oracle(B, T, S, Dm, sub, monkeypatch):
-    monkeypatch.setenv("HMM355_HSMM_SUB", sub)
+def test_hsmm_vs_c_oracle(B, T, S, Dm):
     rng = np.random.default_rng(T + S + Dm)
     lp = (-(rng.random((B, T, S), dtype=np.float32) * 40 + 80)).astype(np.float32)
     dur = np.log(rng.random((S, Dm), dtype=np.float32) + np.float32(1e-8)).astype(np.float32)
@@ -224,14 +221,13 @@ def test_hsmm_vs_c_oracle(B, T, S, Dm, sub, monkeypatch):
 
 
 # the general form (csrc/hsmm_wide.hip): sizes beyond the register-slot geometries, and
-# (HMM355_HSMM_WIDE=1) sizes those also cover, against the C oracle; uniform and coarse
+# (HMM355_FORM_GENERAL) sizes those also cover, against the C oracle; uniform and coarse
 # tie-heavy tables
-@pytest.mark.parametrize("B,T,S,Dm,force,coarse", [(2, 120, 200, 12, "0", False), (1, 150, 70, 80, "0", False),
-                                                   (2, 90, 8, 150, "0", False), (2, 100, 140, 10, "0", True),
-                                                   (2, 200, 16, 12, "1", False), (1, 300, 64, 40, "1", False),
-                                                   (2, 150, 12, 33, "1", True)])
-def test_hsmm_wide_vs_c_oracle(B, T, S, Dm, force, coarse, monkeypatch):
-    monkeypatch.setenv("HMM355_HSMM_WIDE", force)
+@pytest.mark.parametrize("B,T,S,Dm,force,coarse", [(2, 120, 200, 12, 0, False), (1, 150, 70, 80, 0, False),
+                                                   (2, 90, 8, 150, 0, False), (2, 100, 140, 10, 0, True),
+                                                   (2, 200, 16, 12, 1, False), (1, 300, 64, 40, 1, False),
+                                                   (2, 150, 12, 33, 1, True)])
+def test_hsmm_wide_vs_c_oracle(B, T, S, Dm, force, coarse):
     rng = np.random.default_rng(T + S + Dm)
     if coarse:
         lp = np.round(-(rng.random((B, T, S)) * 8 + 4), 1).astype(np.float32)
@@ -243,13 +239,13 @@ def test_hsmm_wide_vs_c_oracle(B, T, S, Dm, force, coarse, monkeypatch):
         logT = np.log(rng.random((S, S), dtype=np.float32) + np.float32(1e-8)).astype(np.float32)
     cs, csc = O.c_hsmm(lp, dur, logT)
     o = ops()
-    states, scores = o.hsmm_viterbi(t(lp), t(dur), t(logT))
+    states, scores = o.hsmm_viterbi(t(lp), t(dur), t(logT), o.FORM_GENERAL if force else 0)
     assert np.array_equal(states.cpu().numpy(), cs)
     assert np.array_equal(scores.cpu().numpy(), csc)
 
 
 @pytest.mark.parametrize("case", ["random", "peaked", "ties", "longdur", "s128"])
-def test_hsmm_chunked_backtrace_equals_serial(case, monkeypatch):
+def test_hsmm_chunked_backtrace_equals_serial(case):
     """The chunked backtrace (parallel chunk walks from guessed segments, stitched top-down,
     csrc/hsmm.hip) against the serial walk and the C oracle: uniform random tables (short
     segments), peaked emissions (long segments), coarse tie-heavy values, Dmax > the 64-frame
@@ -269,20 +265,16 @@ def test_hsmm_chunked_backtrace_equals_serial(case, monkeypatch):
         dur, logT = np.round(dur).astype(np.float32), np.round(logT).astype(np.float32)
     cs, csc = O.c_hsmm(lp, dur, logT)
     o = ops()
-    monkeypatch.setenv("HMM355_HSMM_SERIAL", "1")
-    s1, sc1 = o.hsmm_viterbi(t(lp), t(dur), t(logT))
-    monkeypatch.setenv("HMM355_HSMM_SERIAL", "0")
+    s1, sc1 = o.hsmm_viterbi(t(lp), t(dur), t(logT), o.FORM_SERIAL_WALK)
     s2, sc2 = o.hsmm_viterbi(t(lp), t(dur), t(logT))
     assert np.array_equal(s1.cpu().numpy(), cs) and np.array_equal(sc1.cpu().numpy(), csc)
     assert np.array_equal(s2.cpu().numpy(), cs) and np.array_equal(sc2.cpu().numpy(), csc)
 
 
-@pytest.mark.parametrize("sub", ["4", "8", "16"])
-def test_hsmm_impossible_transitions_and_durations(sub, monkeypatch):
+def test_hsmm_impossible_transitions_and_durations():
     """-inf in the tables (a left-to-right transition matrix, durations below a minimum, a state
     no segment may take): the kernel's folded conditions (M = -inf for slots not started, -inf
     duration rows) against the C oracle."""
-    monkeypatch.setenv("HMM355_HSMM_SUB", sub)
     rng = np.random.default_rng(5)
     B, T, S, Dm = 3, 140, 12, 20
     lp = (-(rng.random((B, T, S), dtype=np.float32) * 30 + 10)).astype(np.float32)
@@ -317,13 +309,12 @@ def test_hsmm_single_state_contiguous_sum(T, Dm):
         assert scores[b].cpu().numpy().tobytes() == np.float32(want).tobytes()
 
 
-@pytest.mark.parametrize("S,Dm,wide", [(4, 20, "0"), (40, 100, "0"), (6, 30, "1")])
-def test_hsmm_no_path_leaves_reference_zeros(S, Dm, wide, monkeypatch):
+@pytest.mark.parametrize("S,Dm,wide", [(4, 20, 0), (40, 100, 0), (6, 30, 1)])
+def test_hsmm_no_path_leaves_reference_zeros(S, Dm, wide):
     """A left-to-right chain of S states with durations <= Dm cannot cover T > S * Dm frames:
     every final score is -inf, the walk has no predecessor after its first segment, and the
     frames it never reaches keep the reference's torch.zeros value (hsmm.py:332; the reference's
     own walk would not terminate here).  Both the register-slot and the general form."""
-    monkeypatch.setenv("HMM355_HSMM_WIDE", wide)
     rng = np.random.default_rng(S)
     T = S * Dm + 10
     lp = (-(rng.random((2, T, S), dtype=np.float32) * 10 + 5)).astype(np.float32)
@@ -333,7 +324,7 @@ def test_hsmm_no_path_leaves_reference_zeros(S, Dm, wide, monkeypatch):
         logT[i, i + 1] = 0.0
     o = ops()
     for _ in range(2):  # the second call reuses a dirty output buffer from the caching allocator
-        states, scores = o.hsmm_viterbi(t(lp), t(dur), t(logT))
+        states, scores = o.hsmm_viterbi(t(lp), t(dur), t(logT), o.FORM_GENERAL if wide else 0)
         assert np.all(np.isneginf(scores.cpu().numpy()))
         assert np.array_equal(states.cpu().numpy(), np.zeros((2, T), np.int64))
 

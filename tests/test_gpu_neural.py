@@ -105,24 +105,6 @@ def test_tv_forward_backward_vs_fp64_oracle(B, T, N, static):
     np.testing.assert_allclose(np.log(b_[ok]), lb[ok], atol=2e-4 * max(1.0, np.abs(lb[ok]).max() / 100))
 
 
-@pytest.mark.parametrize("B,T,N,static", SHAPES)
-def test_tv_fb_viterbi_one_call_equals_two(B, T, N, static):
-    """hmm355_tv_fb_viterbi_f32 (alpha and Viterbi in one workgroup, one stream of log_A): every
-    output bit-identical to the separate calls (the same arithmetic in the same order), and the
-    Viterbi path still bit-exact against the C oracle."""
-    lo, lA, init = _random_case(B, T, N, B * 100 + T * 10 + N + 2, static)
-    o = ops()
-    mask = o.FB_POSTERIOR | o.FB_FORWARD | o.FB_BACKWARD
-    p0 = init - 0.25   # a different initial vector for the forward-backward
-    one = o.tv_fb_viterbi(t(lo), t(lA), t(p0), t(init), mask)
-    fb = o.tv_forward_backward(t(lo), t(lA), t(p0), mask)
-    vit = o.tv_viterbi(t(lo), t(lA), t(init))
-    for a, b in zip(one, (*fb, *vit)):
-        assert torch.equal(a, b)
-    cs, cd = O.c_tv_viterbi(lo, lA, init)
-    assert np.array_equal(one[5].cpu().numpy(), cs) and np.array_equal(one[6].cpu().numpy(), cd)
-
-
 def test_tv_expanded_view_is_not_materialised():
     """A static matrix expand()ed over (B,T) is read through zero strides (neural.py:385)."""
     lo, lA, init = _random_case(3, 40, 64, 5, static=True)

@@ -44,8 +44,8 @@ def random_tables(rng, B, T, S, Dm, gaussian=True, ties=False):
     return q, cs, li, lT, du
 
 
-def gpu_viterbi(q, cs, li, lT, du):
-    ss, sd, cnt, sc = ops.semimarkov_viterbi(t(q), None if cs is None else t(cs), t(li), t(lT), t(du))
+def gpu_viterbi(q, cs, li, lT, du, flags=0):
+    ss, sd, cnt, sc = ops.semimarkov_viterbi(t(q), None if cs is None else t(cs), t(li), t(lT), t(du), flags)
     T = q.shape[1]
     ss, sd, cnt, sc = ss.cpu().numpy(), sd.cpu().numpy(), cnt.cpu().numpy(), sc.cpu().numpy()
     return [(ss[b, T - cnt[b]:], sd[b, T - cnt[b]:], sc[b]) for b in range(q.shape[0])]
@@ -186,18 +186,16 @@ def test_wide_viterbi_bitexact_vs_literal(seed, B, T, S, Dm, gaussian, ties):
         assert np.float32(gsc) == np.float32(sc) or (np.isinf(gsc) and np.isinf(sc)), (gsc, sc)
 
 
-def test_wide_forced_equals_register_form(monkeypatch):
-    """HMM355_SMK_WIDE=1 forces the general form on a size the register form holds: the same
+def test_wide_forced_equals_register_form():
+    """HMM355_FORM_GENERAL forces the general form on a size the register form holds: the same
     segments and scores bit for bit, the forward within float64 tolerance of both."""
     rng = np.random.default_rng(30)
     for gaussian, ties in ((True, False), (False, True)):
         q, cs, li, lT, du = random_tables(rng, 3, 300, 20, 30, gaussian, ties)
-        monkeypatch.setenv("HMM355_SMK_WIDE", "0")
         a = gpu_viterbi(q, cs, li, lT, du)
         fa = ops.semimarkov_forward(t(q), None if cs is None else t(cs), t(li), t(lT), t(du), True)
-        monkeypatch.setenv("HMM355_SMK_WIDE", "1")
-        b = gpu_viterbi(q, cs, li, lT, du)
-        fb = ops.semimarkov_forward(t(q), None if cs is None else t(cs), t(li), t(lT), t(du), True)
+        b = gpu_viterbi(q, cs, li, lT, du, ops.FORM_GENERAL)
+        fb = ops.semimarkov_forward(t(q), None if cs is None else t(cs), t(li), t(lT), t(du), True, ops.FORM_GENERAL)
         for (s1, d1, c1), (s2, d2, c2) in zip(a, b):
             assert np.array_equal(s1, s2) and np.array_equal(d1, d2) and np.float32(c1) == np.float32(c2)
         np.testing.assert_allclose(fb[0].cpu().numpy(), fa[0].cpu().numpy(), rtol=2e-6)

@@ -22,9 +22,8 @@ def _dense(N, seed):
 
 def _run(lo, lP, lp0, plan, follow, monkeypatch, mode=None):
     from pytorch_hmm_amd import ops
-    monkeypatch.setenv("HMM355_VIT_FOLLOW", "1" if follow else "0")
     x = torch.from_numpy(lo).to(DEV)
-    s, d, f = ops.viterbi(x, lP.to(DEV), lp0.to(DEV), ops.OBS_LOG if mode is None else mode, plan)
+    s, d, f = ops.viterbi(x, lP.to(DEV), lp0.to(DEV), ops.OBS_LOG if mode is None else mode, plan, follow=follow)
     torch.cuda.synchronize()
     return s.cpu().numpy(), d.cpu().numpy(), f.cpu().numpy()
 
@@ -40,7 +39,7 @@ def test_followers_vs_c_oracle(N, T, monkeypatch):
     B = 5
     lo = np.log(rng.random((B, T, N), dtype=np.float32) + np.float32(1e-3)).astype(np.float32)
     cs, cd, _ = O.c_viterbi(lo, lP.numpy(), lp0.numpy())
-    for follow in (True, False):  # (HMM355_VIT_FOLLOW overrides the default either way)
+    for follow in (True, False):
         s, d, f = _run(lo, lP, lp0, plan, follow, monkeypatch)
         assert np.array_equal(d, cd), follow
         assert np.array_equal(s, cs), follow
@@ -162,9 +161,8 @@ def test_followers_no_cliff_beside_busy_stream(monkeypatch):
     vs = torch.cuda.Stream()
 
     def run(follow):
-        monkeypatch.setenv("HMM355_VIT_FOLLOW", "1" if follow else "0")
         with torch.cuda.stream(vs):
-            ops.viterbi(lo, lPd, lp0d, ops.OBS_LOG, plan)   # warm
+            ops.viterbi(lo, lPd, lp0d, ops.OBS_LOG, plan, follow=follow)   # warm
         torch.cuda.synchronize()
         times = []
         for _ in range(3):
@@ -174,7 +172,7 @@ def test_followers_no_cliff_beside_busy_stream(monkeypatch):
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             with torch.cuda.stream(vs):
                 e0.record()
-                out = ops.viterbi(lo, lPd, lp0d, ops.OBS_LOG, plan)
+                out = ops.viterbi(lo, lPd, lp0d, ops.OBS_LOG, plan, follow=follow)
                 e1.record()
             torch.cuda.synchronize()
             times.append(e0.elapsed_time(e1))

@@ -51,6 +51,10 @@ def test_constants_match_header():
     assert (d["HMM355_FB_POSTERIOR"], d["HMM355_FB_FORWARD"], d["HMM355_FB_BACKWARD"]) == \
         (nat.FB_POSTERIOR, nat.FB_FORWARD, nat.FB_BACKWARD)
     assert d["HMM355_FB_PAIR"] == nat.FB_PAIR == 0x100
+    assert d["HMM355_FB_PLAN_BANDED"] == nat.FB_PLAN_BANDED
+    assert (d["HMM355_VIT_PLAN_BANDED"], d["HMM355_VIT_PLAN_DENSE"]) == (nat.VIT_PLAN_BANDED, nat.VIT_PLAN_DENSE)
+    assert d["HMM355_PLAN_DENSE"] == nat.PLAN_DENSE
+    assert (d["HMM355_FORM_GENERAL"], d["HMM355_FORM_SERIAL_WALK"]) == (nat.FORM_GENERAL, nat.FORM_SERIAL_WALK)
     assert d["HMM355_OK"] == 0
 
 
@@ -74,15 +78,36 @@ def test_workspace_sizes(L):
 
 def test_fb_workspace_layout_matches_header(L):
     """include/hmm355.h's forward-backward workspace layout (U | V | LA | LB | BandDesc | (B,NP) |
-    (B) | (B,T) | CA | CB, 256-B aligned) is what hmm355_fb_workspace_bytes sizes, so the adjoint's
-    views of CA / CB (autograd._run_fb) end exactly at the workspace's end."""
+    (B) | (B,T) | CA | CB | the followers' counts, 256-B aligned) is what hmm355_fb_workspace_bytes
+    sizes and what hmm355_fb_workspace_layout reports -- the offsets the adjoint reads U / V / LA /
+    LB / CA / CB at (autograd.fb_layout), for every padded state count (N 200: NP 256)."""
+    from pytorch_hmm_amd.autograd import FB_PIECES, fb_layout
     al = lambda n: ((n + 255) // 256) * 256
-    for B, T, N in ((32, 2000, 128), (3, 17, 5), (2, 1, 200), (7, 129, 64)):
+    for B, T, N in ((32, 2000, 128), (3, 17, 5), (2, 1, 200), (7, 129, 64), (4, 300, 200)):
         NP = 64 if N <= 64 else (128 if N <= 128 else 256)
         rows = B * T
-        want = (al(2 * rows * NP * 4) + al(2 * rows * 4) + al(L.hmm355_plan_bytes(N)) + al(B * NP * 4) + al(B * 4)
-                + al(rows * 4) + al(2 * rows * 4))
-        assert L.hmm355_fb_workspace_bytes(B, T, N) == want, (B, T, N)
+        sizes = [rows * NP * 4, rows * NP * 4, rows * 4, rows * 4, L.hmm355_plan_bytes(N), B * NP * 4, B * 4,
+                 rows * 4, rows * 4, rows * 4]
+        off = fb_layout(B, T, N)
+        # U | V and LA | LB and CA | CB are contiguous pairs, each pair 256-B aligned
+        want, pos, pair = {}, 0, 0
+        for name, nbytes in zip(FB_PIECES, sizes):
+            want[name] = pos + pair
+            if name in ("U", "LA", "CA"):
+                pair = nbytes
+            else:
+                pos, pair = pos + al(pair + nbytes), 0
+        assert off == want, (B, T, N, off, want)
+        assert L.hmm355_fb_workspace_bytes(B, T, N) == pos + al(((2 * B * 4 + 15) // 16) * 16), (B, T, N)
+
+
+def test_release_build_reads_no_environment():
+    """the library's behaviour does not depend on the process environment --
+    a release build imports no getenv (the diagnostic switches exist only in HMM355_DIAG builds)."""
+    from pytorch_hmm_amd import _native as nat
+    out = subprocess.run(["nm", "-D", "--undefined-only", nat.LIB_PATH], capture_output=True, text=True,
+                         check=True).stdout
+    assert not re.search(r"\b(secure_)?getenv\b", out), "libhmm355.so imports getenv"
 
 
 def test_argument_rejection_before_launch(L):

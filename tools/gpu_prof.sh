@@ -8,12 +8,12 @@ cd $GRAFT_REPO_ROOT
 TAG=${1:-r1}; shift
 ARGS="$@"
 export TMPDIR=/tmp
-export HMM355_BENCH_NO_KPROF=1   # no torch.profiler inside the rocprofv3 passes
+# (--no-kernel-profile: no torch.profiler inside the rocprofv3 passes)
 D=gpurun_out/prof_$TAG
 mkdir -p $D
-timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $D/trace -o run -- python3 bench.py --steps 20 --warmup 3 --cpu-seconds 0 $ARGS > $D/bench_trace.log 2>&1 &&
-timeout -k 10 600 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $D/fetch -o run -- python3 bench.py --steps 5 --warmup 1 --cpu-seconds 0 $ARGS > $D/bench_fetch.log 2>&1 &&
-timeout -k 10 600 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $D/write -o run -- python3 bench.py --steps 5 --warmup 1 --cpu-seconds 0 $ARGS > $D/bench_write.log 2>&1
+timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $D/trace -o run -- python3 bench.py --steps 20 --warmup 3 --cpu-seconds 0 --no-kernel-profile $ARGS > $D/bench_trace.log 2>&1 &&
+timeout -k 10 600 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $D/fetch -o run -- python3 bench.py --steps 5 --warmup 1 --cpu-seconds 0 --no-kernel-profile $ARGS > $D/bench_fetch.log 2>&1 &&
+timeout -k 10 600 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $D/write -o run -- python3 bench.py --steps 5 --warmup 1 --cpu-seconds 0 --no-kernel-profile $ARGS > $D/bench_write.log 2>&1
 rc=$?
 echo "rocprof rc=$rc"
 find $D -name "*.csv" | sort

@@ -1,5 +1,5 @@
 cd $GRAFT_REPO_ROOT
-export TMPDIR=/tmp HMM355_BENCH_NO_KPROF=1
+export TMPDIR=/tmp
 D=gpurun_out/pmc_gmm
 mkdir -p $D
 timeout -s KILL 120 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_INSTS_LDS SQ_WAIT_INST_LDS SQ_WAIT_ANY --output-format csv -d $D/p1 -o run -- python3 bench.py --workload c3 --steps 2 --warmup 1 --cpu-seconds 0 > $D/b1.log 2>&1
