@@ -18,6 +18,13 @@
 #define HMM355_STAMP 0
 #endif
 
+// Ablation knobs of the work beside the chains (csrc/follow.h), diagnostic builds only: 1 no
+// per-block publishing (completion only), 2 followers return at once (timing only), 4 plain
+// instead of write-through row / psi stores (timing only), 8 no log leaders.
+#ifndef HMM355_FABL
+#define HMM355_FABL 0
+#endif
+
 namespace hmm355 {
 
 constexpr int kWave = 64;
@@ -35,6 +42,7 @@ __device__ __forceinline__ unsigned long long stamp() {
 template <typename T>
 __device__ __forceinline__ void keep(T& v) { asm volatile("" : "+v"(v)); }
 constexpr int kAbl = HMM355_ABL;
+constexpr int kFAbl = HMM355_FABL;
 
 // compile-time loop: f(integral_constant<int, J>) for J in [B, E)
 template <int J, int E, typename F>
@@ -220,6 +228,9 @@ constexpr int kAuxSc1 = 16;  // buffer instruction cache-policy bits: sc1
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* p, size_t bytes) {
   return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, (int)bytes, 0x00020000);
 }
+// published counts sit one per 128-B line (no two counters share a line: a chain's store and
+// another chain's follower polls never meet on one)
+constexpr int kPubStride = 32;
 __device__ __forceinline__ int poll_count(const int* p) {
   return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }

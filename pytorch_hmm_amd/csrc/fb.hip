@@ -58,7 +58,7 @@ __global__ void __launch_bounds__(256) row_max_kernel(const float* __restrict__ 
 struct FbWs {
   float *U, *V, *LA, *LB, *binit, *bscale, *rmax, *CA, *CB;
   BandDesc* band;
-  int* pub;  // (2B) the chains' published block counts (posterior followers, follow.h)
+  int* pub;  // (2B x kPubStride) the chains' published block counts (posterior followers, follow.h)
 };
 static size_t fb_ws_layout(int B, int T, int N, char* base, FbWs* w) {
   const size_t NP = pad_states(N);
@@ -72,7 +72,7 @@ static size_t fb_ws_layout(int B, int T, int N, char* base, FbWs* w) {
   const size_t oS = take((size_t)B * sizeof(float));
   const size_t oM = take(rows * sizeof(float));
   const size_t oC = take(2 * rows * sizeof(float));
-  const size_t oP = take(align_up((size_t)2 * B * sizeof(int), 16));
+  const size_t oP = take((size_t)2 * B * kPubStride * sizeof(int));
   if (w && base) {
     w->U = reinterpret_cast<float*>(base + oU);
     w->V = w->U + rows * NP;

@@ -45,7 +45,7 @@ __device__ __forceinline__ void follow_poll(const int* p, int need, int* slot) {
   int have = poll_count(p), last = have;
   long long t0 = __builtin_amdgcn_s_memrealtime();
   while (have < need) {
-    __builtin_amdgcn_s_sleep(8);
+    __builtin_amdgcn_s_sleep(20);
     have = poll_count(p);
     const long long now = __builtin_amdgcn_s_memrealtime();
     if (have != last) {
@@ -66,12 +66,12 @@ __device__ __forceinline__ void follow_poll(const int* p, int need, int* slot) {
 template <int NP>
 __device__ __forceinline__ void vit_lead(const RecArgs& a, int b) {
   const int T = a.T, N = a.N, nblocks = (T + 15) / 16;
-  if (!a.lobuf || nblocks <= 4) return;
+  if (!a.lobuf || nblocks <= 4 || (kFAbl & (2 | 8))) return;
   const int tid = threadIdx.x, nt = blockDim.x;
   const size_t off = (size_t)b * T * N;
   const float* src = a.obs + off;
   float* dst = const_cast<float*>(a.lobuf) + off;
-  int* cnt = const_cast<int*>(a.lready) + b;
+  int* cnt = const_cast<int*>(a.lready) + b * kPubStride;
   const __amdgpu_buffer_rsrc_t rs = make_rsrc(dst, (size_t)T * N * 4);
   const bool vec = (N & 3) == 0 && ((reinterpret_cast<uintptr_t>(src) | reinterpret_cast<uintptr_t>(dst)) & 15) == 0;
   constexpr int kRound = 8;  // blocks per round
@@ -131,11 +131,12 @@ __device__ __forceinline__ void vit_decode_follow(const RecArgs& a, int b, float
     for (int t = tid; t < T; t += blockDim.x) sb[t] = -1;
     if (tid == 0 && a.final_score) a.final_score[b] = __builtin_bit_cast(float, 0x7fc00000u);
   };
+  if (kFAbl & 2) return;
   if (rec_band_code<kVit, NP>(a) == 0) {
     invalid();
     return;
   }
-  const int* pubp = a.pub + b;
+  const int* pubp = a.pub + b * kPubStride;
   const __amdgpu_buffer_rsrc_t psi_rs = make_rsrc(a.psi + (size_t)b * T * NP, (size_t)T * NP);
   constexpr int G = follow_g(NP);
   int have = 0;   // psi blocks published (nblocks + 1: everything)
@@ -287,11 +288,13 @@ __device__ __forceinline__ void fb_post_follow(const RecArgs& fa, const RecArgs&
     for (size_t i = tid; i < (size_t)T * N; i += blockDim.x) pbase[i] = __builtin_bit_cast(float, 0x7fc00000u);
     if (tid == 0 && fa.lik_ref) fa.lik_ref[b] = __builtin_bit_cast(float, 0x7fc00000u);
   };
+  if (kFAbl & 2) return;
   if (rec_band_code<kFbAlpha, NP>(fa) == 0 || rec_band_code<kFbBeta, NP>(fb) == 0) {
     invalid();  // (the dense chains publish nothing: a plan passed as banded that is not)
     return;
   }
-  const int* pa = fa.pub + 2 * b;
+  const int* pa = fa.pub + 2 * b * kPubStride;
+  const int* pb_ = pa + kPubStride;
   const __amdgpu_buffer_rsrc_t rU = make_rsrc(fa.rows + (size_t)b * T * NP, (size_t)T * NP * 4);
   const __amdgpu_buffer_rsrc_t rV = make_rsrc(fb.rows + (size_t)b * T * NP, (size_t)T * NP * 4);
   const bool vec = N == NP && (reinterpret_cast<uintptr_t>(posterior) % (4 * K)) == 0;
@@ -344,13 +347,13 @@ __device__ __forceinline__ void fb_post_follow(const RecArgs& fa, const RecArgs&
       int ok = 1;
       long long t0 = __builtin_amdgcn_s_memrealtime();
       for (;;) {
-        const int na = poll_count(pa), nb = poll_count(pa + 1);
+        const int na = poll_count(pa), nb = poll_count(pb_);
         const int lo = T - rows_of(nb), hi = rows_of(na);
         const bool more = lo < hi && (plo < 0 || lo < plo || hi > phi);
         if (more) { ca = na; cb = nb; break; }
         if (na != ca || nb != cb) { ca = na; cb = nb; t0 = __builtin_amdgcn_s_memrealtime(); }
         else if (__builtin_amdgcn_s_memrealtime() - t0 > kFollowGiveUp) { ok = 0; break; }
-        __builtin_amdgcn_s_sleep(8);
+        __builtin_amdgcn_s_sleep(20);
       }
       ctl[0] = ok; ctl[1] = ca; ctl[2] = cb;
     }

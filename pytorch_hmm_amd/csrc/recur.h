@@ -469,7 +469,7 @@ __device__ __forceinline__ void rec_flush(const RecArgs& a, const float* lds, in
     const float4 v = *reinterpret_cast<const float4*>(lds + C::OFF_RING + (q & (C::RING - 1)) * NP + c4);
     const size_t tr = (size_t)b * a.T + rec_tau<KIND>(q, a.T);
     if (q < a.T) {
-      if (a.pub) {
+      if (a.pub && !(kFAbl & 4)) {
         // followers read these rows in this launch: write-through (sc1) 16-B stores (follow.h)
         const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
             a.rows + (size_t)b * a.T * NP, (short)0, (int)((size_t)a.T * NP * 4), 0x00020000);
@@ -504,7 +504,7 @@ __device__ __forceinline__ void rec_flush(const RecArgs& a, const float* lds, in
       float* dst = a.rows + ((size_t)b * a.T + rec_tau<KIND>(q, a.T)) * a.row_stride + col;
       const float v = lds[C::OFF_RING + (q & (C::RING - 1)) * NP + col];
       if (q < a.T) {
-        if (a.pub) __hip_atomic_store(dst, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // (sc1)
+        if (a.pub && !(kFAbl & 4)) __hip_atomic_store(dst, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // (sc1)
         else *dst = v;
       }
     }
@@ -1634,14 +1634,16 @@ __device__ __forceinline__ void rec_band(const RecArgs& a, float* lds, int b, co
       }
     };
     // Publishing (a.pub, follow.h): the flushes of the rows (FB: U / V, Viterbi: delta) and the
-    // copies of the psi rows are write-through stores issued BEFORE the block's global loads, and
-    // a wave's vector-memory counter retires in issue order, so the compiler's wait for the loads
-    // of block k + 1 (at their staging in block_work(k)) also retires every store issued before
-    // them: the flush of block k - 4 and the psi copy of block k - 5.  After the barrier that ends
-    // block_work(k) those are complete in every helper, and in block_work(k + 1) one lane
-    // publishes the count -- no fence, no explicit drain of the prefetches.
+    // copies of the psi rows are write-through stores, and a wave's vector-memory counter retires
+    // in issue order, so the compiler's wait for a register set's loads at its staging also
+    // retires every store issued before those loads.  The loads of block k + 4 are issued in
+    // block_work(k + 1), after block_work(k)'s flush of block k - 2 and psi copy of block k - 3, and
+    // they are staged (waited for) in block_work(k + 3): after the barrier that ends it those
+    // stores are complete in every helper, and in block_work(k + 4) one lane publishes the count.
+    // (The stores are never waited for sooner: a write-through store retires late, and a helper
+    // stalled on it stalls the chain at the next barrier.)
     const bool pubon = a.pub != nullptr;
-    int* const pubp = pubon ? a.pub + (FB ? 2 * b + (KIND == kFbBeta) : b) : nullptr;
+    int* const pubp = pubon ? a.pub + (FB ? 2 * b + (KIND == kFbBeta) : b) * kPubStride : nullptr;
     [[maybe_unused]] const __amdgpu_buffer_rsrc_t psi_rs =
         FUSE ? make_rsrc(a.psi + (size_t)b * T * NP, (size_t)T * NP) : make_rsrc(a.obs, 0);
     // copy the 16 psi rows of block bk from the LDS ring to HBM, one 16-B sc1 store per lane
@@ -1655,48 +1657,44 @@ __device__ __forceinline__ void rec_band(const RecArgs& a, float* lds, int b, co
         const u32x4_t v = *reinterpret_cast<const u32x4_t*>(reinterpret_cast<const uint8_t*>(lds + C::OFF_PSR) +
                                                             (t & (C::PSR - 1)) * NP + 16 * pc);
         if (bk >= 0 && hidx < 16 * PER && t < T)
-          __builtin_amdgcn_raw_buffer_store_b128(v, psi_rs, t * NP + 16 * pc, 0, kAuxSc1);
+          __builtin_amdgcn_raw_buffer_store_b128(v, psi_rs, t * NP + 16 * pc, 0, (kFAbl & 4) ? 0 : kAuxSc1);
       }
     };
     // Straight-line block work (no branch around the staging or the loads: the tail stages
     // a block past the end as padding and re-loads the last block), so the waitcnt pass
     // keeps exact counts and never drains the in-flight prefetches or the flush stores.
-    // Order: publish, log-scales, staging of block kb+1 (waits for its loads), flush of block
-    // kb-2 and psi copy of block kb-3 (stores), the leaders' poll, the loads of block kb+3.
-    // Viterbi with log leaders: the poll issued here is read two blocks later (`pold`), where the
-    // staging's wait has already retired it, so the poll never stalls the helper.
-    auto block_work = [&](int kb, float(&ernext)[HV][5], float(&erfree)[HV][5], int& pnew, int pold, auto FULLC) {
+    // Viterbi with log leaders: `lp` holds the leaders' count as polled three blocks ago (read
+    // here, where the staging's wait has already retired that poll, so it never stalls the
+    // helper), and takes this block's poll.
+    auto block_work = [&](int kb, float(&ernext)[HV][5], float(&erfree)[HV][5], int& lp, auto FULLC) {
+      asm volatile("" ::: "memory");  // (block_work(kb - 1)'s stores stay ahead of this block's loads)
       const int kload = kb + 3 < nblocks ? kb + 3 : nblocks - 1;
-      if (pubon && hi == 0 && l == 0) {
-        const int cnt = FB ? kb - 4 : kb - 5;
-        if (cnt > 0) publish_count(pubp, cnt);
-      }
       // the block's log-scales once per helper (its own base); helper 1 writes LA / LB
       float lsv = 0.f;
       if (!(kAbl & 32) && kb >= 2) lsv = rec_ls_scan<NP, KIND>(a, lds, b, kb - 2, base, w == 1);
-#pragma unroll
-      for (int h = 0; h < HV; ++h) {
-        const int vw = vw_of(h);
-        if (vw < C::NW && !(kAbl & 32768) && !(kAbl & 64)) rec_stage<NP, KIND, FUSE>(a, lds, kb + 1, vw, l, ernext[h]);
-      }
-#pragma unroll
-      for (int h = 0; h < HV; ++h) {
-        const int vw = vw_of(h);
-        if (vw < C::NW && !(kAbl & 32768) && !(kAbl & 32) && kb >= 2) rec_flush<NP, KIND>(a, lds, b, kb - 2, l + 64 * vw, lsv);
-      }
-      psi_copy(kb - 3);
-      asm volatile("" ::: "memory");  // (the stores stay ahead of the loads below)
-      if (KIND == kVit && a.lready) pnew = poll_count(a.lready + b);
       // Viterbi: the block's source -- the leaders' log rows when they are ready, else the raw
       // emissions (the staging takes the log)
-      const bool fromlog = KIND == kVit && a.lobuf && kload >= 4 && pold >= kload + 1;
+      const bool fromlog = KIND == kVit && a.lobuf && kload >= 4 && lp >= kload + 1;
       const float* src = fromlog ? a.lobuf : a.obs;
       const float vmode = (fromlog || a.obs_mode == HMM355_OBS_LOG) ? 1.f : 0.f;
 #pragma unroll
       for (int h = 0; h < HV; ++h) {
         const int vw = vw_of(h);
-        if (vw < C::NW && !(kAbl & 32768) && !(kAbl & 64))
-          rec_load<NP, KIND, decltype(FULLC)::value, FUSE>(a, b, kload, vw, l, erfree[h], src, vmode);
+        if (vw < C::NW && !(kAbl & 32768)) {
+          if (!(kAbl & 64)) {
+            rec_stage<NP, KIND, FUSE>(a, lds, kb + 1, vw, l, ernext[h]);
+            rec_load<NP, KIND, decltype(FULLC)::value, FUSE>(a, b, kload, vw, l, erfree[h], src, vmode);
+          }
+          if (!(kAbl & 32) && kb >= 2) rec_flush<NP, KIND>(a, lds, b, kb - 2, l + 64 * vw, lsv);
+        }
+      }
+      psi_copy(kb - 3);
+      if (KIND == kVit && a.lready) lp = poll_count(a.lready + b * kPubStride);
+      // every fourth block (Viterbi: whole 64-step chunks of psi rows), after this block's loads
+      // (so the stores it signals are never waited for sooner than three blocks on)
+      if (pubon && !(kFAbl & 1) && hi == 0 && l == 0) {
+        const int cnt = FB ? kb - 5 : kb - 6;
+        if (cnt > 0 && (cnt & 3) == 0) publish_count(pubp, cnt);
       }
       if (!(kAbl & 16384)) lds_barrier();
     };
@@ -1713,12 +1711,12 @@ __device__ __forceinline__ void rec_band(const RecArgs& a, float* lds, int b, co
         return;
       }
     }
-    int lp0 = 0, lp1 = 0, lp2 = 0;  // the leaders' poll ring (block kb's poll is read at kb + 2)
+    int lp0 = 0, lp1 = 0, lp2 = 0;  // the leaders' polls (block kb's is read at kb + 3)
     auto helper_loop = [&](auto FULLC) {
       for (int kb = 0; kb < nblocks; kb += 3) {
-        block_work(kb, er1, er0, lp0, lp1, FULLC);
-        if (kb + 1 < nblocks) block_work(kb + 1, er2, er1, lp1, lp2, FULLC);
-        if (kb + 2 < nblocks) block_work(kb + 2, er0, er2, lp2, lp0, FULLC);
+        block_work(kb, er1, er0, lp0, FULLC);
+        if (kb + 1 < nblocks) block_work(kb + 1, er2, er1, lp1, FULLC);
+        if (kb + 2 < nblocks) block_work(kb + 2, er0, er2, lp2, FULLC);
       }
     };
     if (a.N == NP && (reinterpret_cast<uintptr_t>(a.obs) & 15) == 0 &&

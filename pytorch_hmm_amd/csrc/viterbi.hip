@@ -72,7 +72,7 @@ HMM355_API size_t hmm355_viterbi_workspace_bytes(int B, int T, int N) {
   // psi followers' progress and done words (last)
   return align_up((size_t)B * T * NP, 256) + align_up((size_t)B * nc * NP, 256) + align_up(sizeof(BandDesc), 256) +
          align_up((size_t)B * T * N * sizeof(float), 256) + align_up((size_t)B * kProgSlots * sizeof(int), 256) +
-         align_up((size_t)B * nc, 256);
+         align_up((size_t)B * nc, 256) + (size_t)2 * B * kPubStride * sizeof(int);
 }
 
 // CUs of the current device, queried once per device (a relaxed atomic per slot: concurrent
@@ -123,6 +123,7 @@ static int viterbi_run(const float* obs, int obs_mode, const float* log_P, const
   float* lobuf = reinterpret_cast<float*>(bandp + align_up(sizeof(BandDesc), 256));
   int* prog = reinterpret_cast<int*>(reinterpret_cast<uint8_t*>(lobuf) + align_up((size_t)B * T * N * sizeof(float), 256));
   uint8_t* done = reinterpret_cast<uint8_t*>(prog) + align_up((size_t)B * kProgSlots * sizeof(int), 256);
+  int* counts = reinterpret_cast<int*>(done + align_up((size_t)B * nc, 256));  // (2B x kPubStride) follow.h
   BandDesc* band = plan ? static_cast<BandDesc*>(const_cast<void*>(plan)) : reinterpret_cast<BandDesc*>(bandp);
   VitArgs va{obs, log_P, init, log_delta, final_score, states, psi, G, B, T, N, obs_mode, nc, band};
   hipStream_t sm = static_cast<hipStream_t>(stream);
@@ -130,13 +131,13 @@ static int viterbi_run(const float* obs, int obs_mode, const float* log_P, const
   if (vit_follow_ok(flags, plan, B, T, N)) {
     // one launch: the chains, and per sequence a workgroup that first forms log(x + 1e-8) of
     // the sequence's emissions ahead of its chain (OBS_PROB) and then composes the chunk maps and
-    // backtraces the path (follow.h).  The counts live in prog: [0, B) published psi blocks, [B, 2B)
-    // the leaders' blocks, zeroed first (a 16-B multiple inside prog's block).
-    if ((e = hipMemsetAsync(prog, 0, align_up((size_t)2 * B * sizeof(int), 16), sm)) != hipSuccess) return (int)e;
-    va.pub = prog;
+    // backtraces the path (follow.h).  The counts, one per 128-B line, zeroed first: [0, B) the
+    // published psi blocks, [B, 2B) the leaders' blocks.
+    if ((e = hipMemsetAsync(counts, 0, (size_t)2 * B * kPubStride * sizeof(int), sm)) != hipSuccess) return (int)e;
+    va.pub = counts;
     if (obs_mode == HMM355_OBS_PROB) {
       va.lobuf = lobuf;
-      va.lready = prog + B;
+      va.lready = counts + (size_t)B * kPubStride;
     }
     va.nfollow = B;
     switch (NP) {

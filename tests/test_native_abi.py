@@ -98,7 +98,7 @@ def test_fb_workspace_layout_matches_header(L):
             else:
                 pos, pair = pos + al(pair + nbytes), 0
         assert off == want, (B, T, N, off, want)
-        assert L.hmm355_fb_workspace_bytes(B, T, N) == pos + al(((2 * B * 4 + 15) // 16) * 16), (B, T, N)
+        assert L.hmm355_fb_workspace_bytes(B, T, N) == pos + al(2 * B * 128), (B, T, N)
 
 
 def test_release_build_reads_no_environment():
