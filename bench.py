@@ -69,8 +69,18 @@ def parse():
                    help="layer workloads: skip the torch.profiler pass that finds the dominant kernel")
     p.add_argument("--no-follow", action="store_true",
                    help="ns workload, diagnostic: run the passes after the chains instead of the work "
-                        "beside them in the chains' launches (csrc/follow.h)")
+                        "beside them in the chains' launches (csrc/follow.h); = --follow none")
+    p.add_argument("--follow", choices=["default", "none", "fb", "vit", "all"], default="default",
+                   help="ns workload, diagnostic: which op runs its work beside the chains (default: "
+                        "the ops' own choice)")
     return p.parse_args()
+
+
+def ns_follow(args):
+    """(fb, vit) follow arguments of the ns step's two ops (None = the op's default)"""
+    mode = "none" if args.no_follow else args.follow
+    return {"default": (None, None), "none": (False, False), "fb": (True, False),
+            "vit": (False, True), "all": (True, True)}[mode]
 
 
 def spawn_ranks(args):
@@ -746,9 +756,9 @@ def main():
     # the batch (+ the gather when world > 1).  The two ops are independent, so each runs on
     # its own stream, replayed from a HIP graph; consecutive steps pipeline across the streams
     # (no per-step join: a cross-stream join costs two cross-queue signal hops, ~35 us).
-    follow = False if args.no_follow else None
-    step = NsStep({"fb": lambda: ops.forward_backward(obs, lP, lp0, ops.OBS_PROB, 7, plan, follow=follow),
-                   "vit": lambda: ops.viterbi(obs, lP, lp0, ops.OBS_PROB, plan, follow=follow)},
+    fb_fl, vit_fl = ns_follow(args)
+    step = NsStep({"fb": lambda: ops.forward_backward(obs, lP, lp0, ops.OBS_PROB, 7, plan, follow=fb_fl),
+                   "vit": lambda: ops.viterbi(obs, lP, lp0, ops.OBS_PROB, plan, follow=vit_fl)},
                   dev, gatherer, use_graph=not args.no_graph, serial=args.serial)
 
     for _ in range(args.warmup):
@@ -799,8 +809,9 @@ def main():
     pair = banded and ops._use_pair(B, dev)
     cus = torch.cuda.get_device_properties(dev).multi_processor_count
     # (the C ABI's conditions for the work beside the chains: fb.hip, viterbi.hip vit_follow_ok)
-    fb_follow = banded and not pair and not args.no_follow and 3 * B <= cus
-    vit_follow = banded and not args.no_follow and N > 64 and 4 * B <= cus
+    fb_fl, vit_fl = ns_follow(args)
+    fb_follow = banded and not pair and fb_fl is not False and ops.fb_follow_default(fb_fl) and 3 * B <= cus
+    vit_follow = banded and vit_fl is not False and N > 64 and 4 * B <= cus
     if fb_ms >= vit_ms:
         dom, dur_ms, bytes_per_launch = "forward_backward", fb_ms, 16 * N * B * T
         kernels = ("fb_pair_kernel" if pair else

@@ -52,10 +52,10 @@ extern "C" {
  * hint still gives correct results (slower).  N <= 128; ignored otherwise. */
 #define HMM355_FB_PAIR 0x100u
 /* Hint (forward_backward with a plan): the caller read hmm355_plan_banded(plan) == 1.  The chains
- * then publish their rows as they go and one extra workgroup per sequence forms the posterior
- * (and the chain forms lik_ref) inside the chains' own launch, instead of a pass after them
- * (csrc/follow.h).  Needs HMM355_FB_POSTERIOR; ignored when the 3B workgroups would not fit the
- * device at once.  Passing it with a plan that is not banded is a caller error: posterior and
+ * then publish their rows as they go and extra workgroups (two per sequence while 4B workgroups
+ * fit the device, else one) form the posterior (and the chain forms lik_ref) inside the chains'
+ * own launch, instead of a pass after them (csrc/follow.h).  Needs HMM355_FB_POSTERIOR; ignored
+ * when the 3B workgroups would not fit the device at once.  Passing it with a plan that is not banded is a caller error: posterior and
  * lik_ref come back NaN. */
 #define HMM355_FB_PLAN_BANDED 0x200u
 

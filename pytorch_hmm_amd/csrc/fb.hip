@@ -32,7 +32,7 @@ namespace hmm355 {
 
 // per-NP launchers (fb_kern.h, instantiated in fb_np64/128/256.hip)
 template <int NP>
-hipError_t launch_fb(const RecArgs& fa, const RecArgs& fb, const PostArgs& pa, bool prep, hipStream_t st);
+hipError_t launch_fb(const RecArgs& fa, const RecArgs& fb, const PostArgs& pa, bool prep, hipStream_t st, int nfollow);
 template <int NP>
 hipError_t launch_fb_pair(const PairArgs& pa, int B, hipStream_t st);
 // OBS_LOG: the row maxima M_t = max_j lo_t[j] (one wave per (b,t) row, grid-stride); the
@@ -206,20 +206,23 @@ HMM355_API int hmm355_forward_backward_plan_f32(const float* obs, int obs_mode, 
   fa.out_exp = (out_mask & HMM355_FB_FORWARD) ? forward : nullptr;
   fb.out_exp = (out_mask & HMM355_FB_BACKWARD) ? backward : nullptr;
   // HMM355_FB_PLAN_BANDED (the caller read hmm355_plan_banded(plan) == 1): the posterior and the
-  // reference's likelihood are formed inside the chains' launch (follow.h) -- one follower
-  // workgroup per sequence beside the 2B chains, while all 3B fit the chip at once
+  // reference's likelihood are formed inside the chains' launch (follow.h) -- F follower
+  // workgroups per sequence beside the 2B chains (two while 4B fit the chip, else one while 3B
+  // do: a follower CU's write-through reads bound its rate)
+  int nfollow = 0;
   if ((out_mask & HMM355_FB_PLAN_BANDED) && plan && (out_mask & HMM355_FB_POSTERIOR) && 3 * B <= fb_device_cus() &&
       (size_t)T * NP * 4 < ((size_t)1 << 31)) {
     fa.pub = fb.pub = w.pub;
     fa.lik_ref = lik_ref;
+    nfollow = HMM355_FBF > 0 ? HMM355_FBF : (4 * B <= fb_device_cus() ? 2 : 1);
   }
   PostArgs pa{w.U, w.V, w.LA, w.LB, posterior, forward, backward, lik_ref, B, T, N,
               out_mask & (HMM355_FB_POSTERIOR)};
   hipError_t e;
   switch (NP) {
-    case 64: e = launch_fb<64>(fa, fb, pa, plan == nullptr, st); break;
-    case 128: e = launch_fb<128>(fa, fb, pa, plan == nullptr, st); break;
-    default: e = launch_fb<256>(fa, fb, pa, plan == nullptr, st); break;
+    case 64: e = launch_fb<64>(fa, fb, pa, plan == nullptr, st, nfollow); break;
+    case 128: e = launch_fb<128>(fa, fb, pa, plan == nullptr, st, nfollow); break;
+    default: e = launch_fb<256>(fa, fb, pa, plan == nullptr, st, nfollow); break;
   }
   return e == hipSuccess ? HMM355_OK : (int)e;
 }

@@ -27,7 +27,7 @@ __global__ void __launch_bounds__(kFbNT<NP>) fb_recur_kernel(RecArgs fa, RecArgs
 }
 
 template <int NP>
-hipError_t launch_fb(const RecArgs& fa, const RecArgs& fb, const PostArgs& pa, bool prep, hipStream_t st) {
+hipError_t launch_fb(const RecArgs& fa, const RecArgs& fb, const PostArgs& pa, bool prep, hipStream_t st, int nfollow) {
   hipError_t e = allow_lds(fb_recur_kernel<NP>, kExclusiveLds);  // own the CU (recur.h)
   if (e != hipSuccess) return e;
   if (fa.band && prep) {
@@ -35,10 +35,12 @@ hipError_t launch_fb(const RecArgs& fa, const RecArgs& fb, const PostArgs& pa, b
     if (e != hipSuccess) return e;
   }
   if (fa.pub) {
-    // posterior followers beside the banded chains (follow.h): 2B chains + B followers, no pass after
+    // posterior followers beside the banded chains (follow.h): 2B chains + F*B followers (F from
+    // the host: fb.hip), no pass after
     e = hipMemsetAsync(fa.pub, 0, (size_t)2 * fa.B * kPubStride * sizeof(int), st);
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(fb_recur_kernel<NP>, dim3(3 * fa.B), dim3(kFbNT<NP>), kExclusiveLds, st, fa, fb, pa.posterior);
+    hipLaunchKernelGGL(fb_recur_kernel<NP>, dim3((2 + nfollow) * fa.B), dim3(kFbNT<NP>), kExclusiveLds, st, fa, fb,
+                       pa.posterior);
     return hipGetLastError();
   }
   hipLaunchKernelGGL(fb_recur_kernel<NP>, dim3(2 * fa.B), dim3(kFbNT<NP>), kExclusiveLds, st, fa, fb, pa.posterior);

@@ -3,7 +3,7 @@
 
 namespace hmm355 {
 template hipError_t launch_fb<128>(const RecArgs& fa, const RecArgs& fb, const PostArgs& pa, bool prep,
-                                   hipStream_t st);
+                                   hipStream_t st, int nfollow);
 template hipError_t launch_fb_pair<128>(const PairArgs& pa, int B, hipStream_t st);
 }  // namespace hmm355
 

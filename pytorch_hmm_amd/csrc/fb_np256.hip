@@ -3,5 +3,5 @@
 
 namespace hmm355 {
 template hipError_t launch_fb<256>(const RecArgs& fa, const RecArgs& fb, const PostArgs& pa, bool prep,
-                                   hipStream_t st);
+                                   hipStream_t st, int nfollow);
 }  // namespace hmm355

@@ -39,6 +39,12 @@ namespace hmm355 {
 
 constexpr long long kFollowGiveUp = 20000000;  // 0.2 s of the 100 MHz real-time counter
 
+// (diagnostic builds: real-time stamp k of this workgroup, tools/band_stamps.py)
+__device__ __forceinline__ void fstamp(int k) {
+  if (kStamp && threadIdx.x == 0)
+    g_rec_stamps[((size_t)blockIdx.x * 16 % kStampWaves) * 8 + k] = __builtin_amdgcn_s_memrealtime();
+}
+
 // One lane polls *p until it reaches `need` or the count stops moving for kFollowGiveUp;
 // the value seen goes to *slot (LDS), -1 on give-up.  The caller's workgroup barrier follows.
 __device__ __forceinline__ void follow_poll(const int* p, int need, int* slot) {
@@ -131,6 +137,7 @@ __device__ __forceinline__ void vit_decode_follow(const RecArgs& a, int b, float
     for (int t = tid; t < T; t += blockDim.x) sb[t] = -1;
     if (tid == 0 && a.final_score) a.final_score[b] = __builtin_bit_cast(float, 0x7fc00000u);
   };
+  fstamp(0);
   if (kFAbl & 2) return;
   if (rec_band_code<kVit, NP>(a) == 0) {
     invalid();
@@ -194,6 +201,7 @@ __device__ __forceinline__ void vit_decode_follow(const RecArgs& a, int b, float
     invalid();
     return;
   }
+  fstamp(1);
   // s_{T-1} = first argmax of delta_{T-1} (hmm.py:174); the maps from the last chunk down
   if (w == 0) {
     const float* dl = a.rows + ((size_t)b * T + T - 1) * a.row_stride;
@@ -215,6 +223,7 @@ __device__ __forceinline__ void vit_decode_follow(const RecArgs& a, int b, float
     }
   }
   __syncthreads();
+  fstamp(2);
   // every chunk's walk: wave w takes chunks w, w + nw, ...; a chunk is two groups of GR = 32
   // rows walked from the top, the rows held in registers (RPV rows per VGPR) and read by
   // v_readlane at the current state, the next group's rows loaded while this one is walked
@@ -262,13 +271,26 @@ __device__ __forceinline__ void vit_decode_follow(const RecArgs& a, int b, float
     });
     if (l < GR && glo + l <= ghi) sb[glo + l] = stv;
   };
-  unsigned pa[NV], pq[NV];
-  load(0, pa);
-  for (int i = 0; i < nitems; i += 2) {
-    load(i + 1, pq);
-    walk(i, pa);
-    load(i + 2, pa);
-    walk(i + 1, pq);
+  // four groups' loads in flight (a wave's whole share at the north-star T): one exposed round
+  // trip to the write-through rows instead of one per group
+  unsigned p0[NV], p1[NV], p2[NV], p3[NV];
+  load(0, p0);
+  load(1, p1);
+  load(2, p2);
+  load(3, p3);
+  for (int i = 0; i < nitems; i += 4) {
+    walk(i, p0);
+    load(i + 4, p0);
+    walk(i + 1, p1);
+    load(i + 5, p1);
+    walk(i + 2, p2);
+    load(i + 6, p2);
+    walk(i + 3, p3);
+    load(i + 7, p3);
+  }
+  if (kStamp) {
+    __syncthreads();
+    fstamp(3);
   }
 }
 
@@ -276,18 +298,25 @@ __device__ __forceinline__ void vit_decode_follow(const RecArgs& a, int b, float
 // Row t's posterior needs alpha row t (published by the alpha chain after step t) and beta row
 // t (by the beta chain after step T-1-t): the ready rows are [T - rows_beta, rows_alpha).  The
 // done rows are always one interval [plo, phi); each round takes the new rows at both ends,
-// one wave per row, with fb_posterior_kernel's arithmetic (post.h) bit for bit.
+// R rows per wave, with fb_posterior_kernel's arithmetic (post.h) bit for bit.
 template <int NP>
 __device__ __forceinline__ void fb_post_follow(const RecArgs& fa, const RecArgs& fb, float* posterior, int b, float* ldsf) {
+  // (b: the follower's index among the F * B followers, split below)
   const int T = fa.T, N = fa.N, nblocks = (T + 15) / 16;
   const int tid = threadIdx.x, w = tid >> 6, l = tid & 63, nw = blockDim.x >> 6;
   int* ctl = reinterpret_cast<int*>(ldsf);
   constexpr int K = NP / 64;
+  // F followers per sequence (the launch's grid: 2B chains + F*B followers); follower f forms
+  // the rows t with t % F == f (a follower's CU moves ~50 GB/s of write-through rows: DESIGN §5)
+  const int F = ((int)gridDim.x - 2 * fa.B) / fa.B, f = b / fa.B;
+  b -= f * fa.B;
+  auto first_own = [&](int x) { return x + ((f - x % F) % F + F) % F; };
   float* pbase = posterior + (size_t)b * T * N;
   auto invalid = [&]() {
     for (size_t i = tid; i < (size_t)T * N; i += blockDim.x) pbase[i] = __builtin_bit_cast(float, 0x7fc00000u);
     if (tid == 0 && fa.lik_ref) fa.lik_ref[b] = __builtin_bit_cast(float, 0x7fc00000u);
   };
+  fstamp(0);
   if (kFAbl & 2) return;
   if (rec_band_code<kFbAlpha, NP>(fa) == 0 || rec_band_code<kFbBeta, NP>(fb) == 0) {
     invalid();  // (the dense chains publish nothing: a plan passed as banded that is not)
@@ -299,44 +328,59 @@ __device__ __forceinline__ void fb_post_follow(const RecArgs& fa, const RecArgs&
   const __amdgpu_buffer_rsrc_t rV = make_rsrc(fb.rows + (size_t)b * T * NP, (size_t)T * NP * 4);
   const bool vec = N == NP && (reinterpret_cast<uintptr_t>(posterior) % (4 * K)) == 0;
   auto rows_of = [&](int c) { return c > nblocks ? T : (16 * c < T ? 16 * c : T); };
-  auto row = [&](int t) {
-    float u[K], v[K];
-    if constexpr (K == 1) {
-      u[0] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rU, (t * NP + l) * 4, 0, kAuxSc1));
-      v[0] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rV, (t * NP + l) * 4, 0, kAuxSc1));
-    } else if constexpr (K == 2) {
-      const float2 x = __builtin_bit_cast(float2, __builtin_amdgcn_raw_buffer_load_b64(rU, (t * NP + 2 * l) * 4, 0, kAuxSc1));
-      const float2 y = __builtin_bit_cast(float2, __builtin_amdgcn_raw_buffer_load_b64(rV, (t * NP + 2 * l) * 4, 0, kAuxSc1));
-      u[0] = x.x; u[1] = x.y; v[0] = y.x; v[1] = y.y;
-    } else {
-      const float4 x = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rU, (t * NP + 4 * l) * 4, 0, kAuxSc1));
-      const float4 y = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rV, (t * NP + 4 * l) * 4, 0, kAuxSc1));
-      u[0] = x.x; u[1] = x.y; u[2] = x.z; u[3] = x.w; v[0] = y.x; v[1] = y.y; v[2] = y.z; v[3] = y.w;
+  // up to R rows per wave per pass, all 2R loads issued before the first row's arithmetic: the
+  // second half of the chains hands over two rows per step (a 4-block publish: 128 rows), and
+  // a row's write-through source is a far cache's round trip away -- one exposed round trip per
+  // pass, not per row
+  constexpr int R = 4;
+  auto rows = [&](const int (&t)[R], int nv) {
+    float u[R][K], v[R][K];
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      const int tr = r < nv ? t[r] : t[0];
+      if constexpr (K == 1) {
+        u[r][0] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rU, (tr * NP + l) * 4, 0, kAuxSc1));
+        v[r][0] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rV, (tr * NP + l) * 4, 0, kAuxSc1));
+      } else if constexpr (K == 2) {
+        const float2 x = __builtin_bit_cast(float2, __builtin_amdgcn_raw_buffer_load_b64(rU, (tr * NP + 2 * l) * 4, 0, kAuxSc1));
+        const float2 y = __builtin_bit_cast(float2, __builtin_amdgcn_raw_buffer_load_b64(rV, (tr * NP + 2 * l) * 4, 0, kAuxSc1));
+        u[r][0] = x.x; u[r][1] = x.y; v[r][0] = y.x; v[r][1] = y.y;
+      } else {
+        const float4 x = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rU, (tr * NP + 4 * l) * 4, 0, kAuxSc1));
+        const float4 y = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rV, (tr * NP + 4 * l) * 4, 0, kAuxSc1));
+        u[r][0] = x.x; u[r][1] = x.y; u[r][2] = x.z; u[r][3] = x.w;
+        v[r][0] = y.x; v[r][1] = y.y; v[r][2] = y.z; v[r][3] = y.w;
+      }
     }
-    // post.h fb_posterior_kernel: max-normalised product, normalised by its sum
-    float mu = 0.f, mv = 0.f;
 #pragma unroll
-    for (int k = 0; k < K; ++k) { mu = fmaxf(mu, u[k]); mv = fmaxf(mv, v[k]); }
-    mu = wave_max_dpp2(mu);
-    mv = wave_max_dpp2(mv);
-    const float iu = mu > 0.f ? 1.f / mu : 0.f, iv = mv > 0.f ? 1.f / mv : 0.f;
-    float p[K], sum = 0.f;
+    for (int r = 0; r < R; ++r) {
+      if (r >= nv) break;
+      const int t_ = t[r];
+      // post.h fb_posterior_kernel: max-normalised product, normalised by its sum
+      float mu = 0.f, mv = 0.f;
 #pragma unroll
-    for (int k = 0; k < K; ++k) { p[k] = (u[k] * iu) * (v[k] * iv); sum += p[k]; }
-    sum = wave_sum_dpp(sum);
-    const float is = sum > 0.f ? 1.f / sum : 0.f;
+      for (int k = 0; k < K; ++k) { mu = fmaxf(mu, u[r][k]); mv = fmaxf(mv, v[r][k]); }
+      mu = wave_max_dpp2(mu);
+      mv = wave_max_dpp2(mv);
+      const float iu = mu > 0.f ? 1.f / mu : 0.f, iv = mv > 0.f ? 1.f / mv : 0.f;
+      float p[K], sum = 0.f;
 #pragma unroll
-    for (int k = 0; k < K; ++k) p[k] *= is;
-    if (vec) {
-      float* dst = pbase + (size_t)t * N + K * l;
-      if constexpr (K == 1) dst[0] = p[0];
-      else if constexpr (K == 2) *reinterpret_cast<float2*>(dst) = make_float2(p[0], p[1]);
-      else *reinterpret_cast<float4*>(dst) = make_float4(p[0], p[1], p[2], p[3]);
-    } else {
-      // (not vec: lane l holds states K*l .. K*l + K - 1 all the same)
+      for (int k = 0; k < K; ++k) { p[k] = (u[r][k] * iu) * (v[r][k] * iv); sum += p[k]; }
+      sum = wave_sum_dpp(sum);
+      const float is = sum > 0.f ? 1.f / sum : 0.f;
 #pragma unroll
-      for (int k = 0; k < K; ++k)
-        if (K * l + k < N) pbase[(size_t)t * N + K * l + k] = p[k];
+      for (int k = 0; k < K; ++k) p[k] *= is;
+      if (vec) {
+        float* dst = pbase + (size_t)t_ * N + K * l;
+        if constexpr (K == 1) dst[0] = p[0];
+        else if constexpr (K == 2) *reinterpret_cast<float2*>(dst) = make_float2(p[0], p[1]);
+        else *reinterpret_cast<float4*>(dst) = make_float4(p[0], p[1], p[2], p[3]);
+      } else {
+        // (not vec: lane l holds states K*l .. K*l + K - 1 all the same)
+#pragma unroll
+        for (int k = 0; k < K; ++k)
+          if (K * l + k < N) pbase[(size_t)t_ * N + K * l + k] = p[k];
+      }
     }
   };
   int plo = -1, phi = -1;  // done rows [plo, phi); empty while plo < 0
@@ -366,14 +410,27 @@ __device__ __forceinline__ void fb_post_follow(const RecArgs& fa, const RecArgs&
       invalid();
       return;
     }
+    if (kStamp && ca > nblocks && cb > nblocks) fstamp(1);
     const int lo = T - rows_of(cb), hi = rows_of(ca);
-    // new rows: [lo, plo) and [phi, hi) (all of [lo, hi) the first time)
-    const int a0 = lo, a1 = plo < 0 ? hi : plo;
-    const int b0 = plo < 0 ? hi : phi, b1 = hi;
-    const int na = a1 - a0, nn = na + (b1 - b0);
-    for (int i = w; i < nn; i += nw) row(i < na ? a0 + i : b0 + (i - na));
+    // new rows: [lo, plo) and [phi, hi) (all of [lo, hi) the first time); this follower's are
+    // those with t % F == f
+    const int a0 = first_own(lo), a1 = plo < 0 ? hi : plo;
+    const int b0 = first_own(plo < 0 ? hi : phi), b1 = hi;
+    const int na = a1 > a0 ? (a1 - a0 + F - 1) / F : 0;
+    const int nn = na + (b1 > b0 ? (b1 - b0 + F - 1) / F : 0);
+    // R consecutive (own) rows per wave
+    for (int i0 = w * R; i0 < nn; i0 += nw * R) {
+      int t[R];
+#pragma unroll
+      for (int r = 0; r < R; ++r) t[r] = i0 + r < na ? a0 + F * (i0 + r) : b0 + F * (i0 + r - na);
+      rows(t, nn - i0 < R ? nn - i0 : R);
+    }
     plo = lo;
     phi = hi;
+  }
+  if (kStamp) {
+    __syncthreads();
+    fstamp(2);
   }
 }
 

@@ -1411,6 +1411,10 @@ __device__ __forceinline__ void band_chain(const RecArgs& a, float* lds, int b, 
     }
   };
 
+  // (diagnostic builds: cycles at the block barriers, the whole chain, and its real time)
+  unsigned long long st_bar = 0, st_t0 = 0;
+  long long rt0 = 0;
+  if (kStamp) { st_t0 = stamp(); rt0 = __builtin_amdgcn_s_memrealtime(); }
   auto run_blocks = [&](auto UA) {
     for (int kb = 0; kb < nblocks; ++kb) {
       const int q0 = kb * 16 < 1 ? 1 : kb * 16;
@@ -1443,7 +1447,10 @@ __device__ __forceinline__ void band_chain(const RecArgs& a, float* lds, int b, 
                [sc](float&, float v) { *sc = v; });
         }
       }
+      unsigned long long sb = 0;
+      if (kStamp) sb = stamp();
       if (!(kAbl & 16384)) lds_barrier();  // B_{kb+1}: block kb+1 staged by the helpers, rows of block kb-1 written
+      if (kStamp) st_bar += stamp() - sb;
     }
   };
   if constexpr (KIND == kFbAlpha) {
@@ -1451,6 +1458,13 @@ __device__ __forceinline__ void band_chain(const RecArgs& a, float* lds, int b, 
     else run_blocks(std::false_type{});
   } else {
     run_blocks(std::false_type{});
+  }
+  if (kStamp && l == 0) {
+    const unsigned long long t1 = stamp();
+    const long long rt1 = __builtin_amdgcn_s_memrealtime();
+    unsigned long long* o8 = g_rec_stamps + ((size_t)blockIdx.x * 16 % kStampWaves) * 8;
+    o8[0] = (unsigned long long)rt0; o8[1] = (unsigned long long)rt1; o8[3] = st_bar;
+    o8[4] = T; o8[5] = t1 - st_t0; o8[6] = t1 - st_t0; o8[7] = (unsigned long long)(rt1 - rt0);
   }
   float* row = lds + C::OFF_RING + ((T - 1) & (C::RING - 1)) * NP;
   st(row + NB * l, y);
@@ -1491,17 +1505,25 @@ __device__ __forceinline__ void rec_band(const RecArgs& a, float* lds, int b, co
   // 195, neither 189; tools/ablate.py, profiles/r3g_ablate.log), so SIMDs 1..3 each carry
   // TWO staging helpers (waves 1,2,3 and 9,10,11) and TWO psi waves (5,6,7 and 13,14,15), and
   // nothing shares the chain's SIMD: waves 4, 8, 12 (w = 0 mod 4, the chain's SIMD) exit.
+  // Round 6, forward-backward (FBW): every wave of the launch off the chain's SIMD stages
+  // (waves 1,2,3, 5,6,7, 9,10,11 of kFbNT<128>: one virtual staging wave each).  With three
+  // helpers of three virtual waves, helper 1's block work took ~3.4 k cycles, the chain's 16
+  // steps ~3.2 k, and the chains waited 18 (beta) / 28 (alpha) cycles a step at the block
+  // barrier (tools/band_stamps.py).
   constexpr bool FUSE = KIND == kVit && kVitFused<NP>;
   constexpr bool WIDE = FUSE;
-  constexpr int NH = WIDE ? 6 : ((KIND == kVit && C::NW >= 8) ? 4 : 3);  // (NP = 64: a 4-wave workgroup)
+  constexpr bool FBW = KIND != kVit;
+  constexpr int NWB = kFbNT<NP> / kWave;  // (FBW) the launch's waves
+  constexpr int NH = WIDE ? 6 : FBW ? (NWB / 4) * 3 + (NWB % 4 > 1 ? NWB % 4 - 1 : 0)
+                                    : ((KIND == kVit && C::NW >= 8) ? 4 : 3);  // (NP = 64: a 4-wave workgroup)
   constexpr int HV = (C::NW + NH - 1) / NH;  // virtual staging waves per helper
   const int tid = threadIdx.x;
   const int w = tid >> 6, l = tid & 63;
   // role of wave w: staging helper index hi (0 .. NH-1), psi wave index, or neither (exit)
   const int grp = (w >> 3) * 3 + (w & 3) - 1;  // WIDE: waves 1,2,3 / 5,6,7 -> 0,1,2; 9,.. / 13,.. -> 3,4,5
-  const bool stager = WIDE ? ((w & 4) == 0 && (w & 3) != 0) : (w > 0 && w <= NH);
+  const bool stager = WIDE ? ((w & 4) == 0 && (w & 3) != 0) : FBW ? (w & 3) != 0 : (w > 0 && w <= NH);
   const bool psiw = WIDE && (w & 4) != 0 && (w & 3) != 0;
-  const int hi = WIDE ? grp : w - 1;
+  const int hi = WIDE ? grp : FBW ? (w >> 2) * 3 + (w & 3) - 1 : w - 1;
   auto vw_of = [&](int h) -> int { return hi + h * NH; };  // virtual staging wave h of this helper
   constexpr bool FB = KIND != kVit;
   if (w != 0 && !stager && !psiw) return;  // ended waves take no part in s_barrier
@@ -1666,8 +1688,12 @@ __device__ __forceinline__ void rec_band(const RecArgs& a, float* lds, int b, co
     // Viterbi with log leaders: `lp` holds the leaders' count as polled three blocks ago (read
     // here, where the staging's wait has already retired that poll, so it never stalls the
     // helper), and takes this block's poll.
+    // (diagnostic builds: a helper's cycles of block work and at the barrier)
+    unsigned long long hs_work = 0, hs_wait = 0;
     auto block_work = [&](int kb, float(&ernext)[HV][5], float(&erfree)[HV][5], int& lp, auto FULLC) {
       asm volatile("" ::: "memory");  // (block_work(kb - 1)'s stores stay ahead of this block's loads)
+      unsigned long long hs0 = 0;
+      if (kStamp) hs0 = stamp();
       const int kload = kb + 3 < nblocks ? kb + 3 : nblocks - 1;
       // the block's log-scales once per helper (its own base); helper 1 writes LA / LB
       float lsv = 0.f;
@@ -1696,7 +1722,10 @@ __device__ __forceinline__ void rec_band(const RecArgs& a, float* lds, int b, co
         const int cnt = FB ? kb - 5 : kb - 6;
         if (cnt > 0 && (cnt & 3) == 0) publish_count(pubp, cnt);
       }
+      unsigned long long hs1 = 0;
+      if (kStamp) { hs1 = stamp(); hs_work += hs1 - hs0; }
       if (!(kAbl & 16384)) lds_barrier();
+      if (kStamp) hs_wait += stamp() - hs1;
     };
     if constexpr (FUSE) {
       if (psiw) {  // psi-only waves: one compact loop, same barrier count as the helpers
@@ -1724,6 +1753,10 @@ __device__ __forceinline__ void rec_band(const RecArgs& a, float* lds, int b, co
       helper_loop(std::true_type{});
     else
       helper_loop(std::false_type{});
+    if (kStamp && l == 0 && stager) {
+      unsigned long long* o8 = g_rec_stamps + (((size_t)blockIdx.x * 16 + w) % kStampWaves) * 8;
+      o8[0] = hs_work; o8[1] = hs_wait; o8[4] = (unsigned long long)nblocks;
+    }
     lds_barrier();  // the chain's last row and c_{T-1}
     const float lsv2 = nblocks >= 2 ? rec_ls_scan<NP, KIND>(a, lds, b, nblocks - 2, base, w == 1) : 0.f;
     const float lsv1 = rec_ls_scan<NP, KIND>(a, lds, b, nblocks - 1, base, w == 1);
@@ -1770,6 +1803,7 @@ __device__ __forceinline__ void rec_band(const RecArgs& a, float* lds, int b, co
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();  // (the chain and psi waves have ended: the helpers alone)
       if (hi == 0 && l == 0) publish_count(pubp, nblocks + 1);
+      if (kStamp && hi == 0 && l == 0) g_rec_stamps[((size_t)blockIdx.x * 16 % kStampWaves) * 8 + 2] = __builtin_amdgcn_s_memrealtime();
     }
 }
 
@@ -1799,7 +1833,7 @@ template <int NP, int KIND>
 __device__ __forceinline__ void rec_dispatch(const RecArgs& a, float* lds, int b) {
   const int code = rec_band_code<KIND, NP>(a);
   // the banded chains are written for RC<NP>::NT threads (the fused Viterbi form for 1024)
-  constexpr int kBandNT = (KIND == kVit && kVitFused<NP>) ? 1024 : RC<NP>::NT;
+  constexpr int kBandNT = (KIND == kVit && kVitFused<NP>) ? 1024 : (KIND != kVit ? kFbNT<NP> : RC<NP>::NT);
   if (code != 0 && threadIdx.x >= kBandNT) return;
   switch (code) {
     case 2: rec_band<NP, KIND, 2>(a, lds, b, a.band); break;

@@ -99,6 +99,15 @@ def plan_info(plan: Optional[Tensor]) -> dict:
 _CUS = {}
 
 
+# forward_backward's posterior beside the chains (follow=None): measured per round on MI355X
+# (DESIGN.md §5); a caller's True / False wins
+FB_FOLLOW_DEFAULT = True
+
+
+def fb_follow_default(follow: Optional[bool]) -> bool:
+    return FB_FOLLOW_DEFAULT if follow is None else bool(follow)
+
+
 def _use_pair(B: int, dev) -> bool:
     """Both chains of a sequence in one workgroup (csrc/fbpair.h, HMM355_FB_PAIR) when the
     batch is larger than half the CUs: the two-kernel path then needs more CU-owning
@@ -136,7 +145,7 @@ def forward_backward(obs: Tensor, log_P: Tensor, log_p0: Tensor, obs_mode: int,
     use_pair = banded and (_use_pair(B, dev) if pair is None else pair)
     if use_pair:
         out_mask |= FB_PAIR
-    elif banded and (out_mask & FB_POSTERIOR) and follow is not False:
+    elif banded and (out_mask & FB_POSTERIOR) and fb_follow_default(follow):
         out_mask |= FB_PLAN_BANDED
     with torch.cuda.device(dev):
         nat.check(L.hmm355_forward_backward_plan_f32(

@@ -86,15 +86,16 @@ def both(fb, vit):
     cur.wait_stream(s_vit)
 
 
-specs = sys.argv[1:]
-runs = {s: make(s) for s in specs}
-res = {s: {"fb": [], "vit": [], "both": []} for s in specs}
-for rnd in range(3):
-    for s, (fb, vit) in runs.items():
-        cur = torch.cuda.current_stream(dev)
-        res[s]["fb"].append(timed(lambda: fb(cur)))
-        res[s]["vit"].append(timed(lambda: vit(cur)))
-        res[s]["both"].append(timed(lambda: both(fb, vit)))
-for s in specs:
-    r = res[s]
-    print(f"{s:60s} fb {min(r['fb']):7.1f}  vit {min(r['vit']):7.1f}  both {min(r['both']):7.1f} us", flush=True)
+if __name__ == "__main__":
+    specs = sys.argv[1:]
+    runs = {s: make(s) for s in specs}
+    res = {s: {"fb": [], "vit": [], "both": []} for s in specs}
+    for rnd in range(3):
+        for s, (fb, vit) in runs.items():
+            cur = torch.cuda.current_stream(dev)
+            res[s]["fb"].append(timed(lambda: fb(cur)))
+            res[s]["vit"].append(timed(lambda: vit(cur)))
+            res[s]["both"].append(timed(lambda: both(fb, vit)))
+    for s in specs:
+        r = res[s]
+        print(f"{s:60s} fb {min(r['fb']):7.1f}  vit {min(r['vit']):7.1f}  both {min(r['both']):7.1f} us", flush=True)
