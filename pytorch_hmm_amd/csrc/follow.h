@@ -126,7 +126,7 @@ inline size_t vit_follow_lds_bytes(int T, int NP) {
 template <int NP>
 __device__ __forceinline__ void vit_decode_follow(const RecArgs& a, int b, float* ldsf) {
   const int T = a.T, N = a.N, nblocks = (T + 15) / 16, nc = (T + kChunk - 1) / kChunk;
-  const int tid = threadIdx.x, w = tid >> 6, l = tid & 63, nw = blockDim.x >> 6;
+  const int tid = threadIdx.x, w = __builtin_amdgcn_readfirstlane(tid >> 6), l = tid & 63, nw = blockDim.x >> 6;
   uint8_t* lds = reinterpret_cast<uint8_t*>(ldsf);
   uint8_t* gm = lds;                                             // [nc][NP]
   uint8_t* stg = gm + align_up((size_t)nc * NP, 16);             // [G][64][NP]
@@ -231,7 +231,6 @@ __device__ __forceinline__ void vit_decode_follow(const RecArgs& a, int b, float
   constexpr int LPR = NP / 4;
   constexpr int GR = 32;
   constexpr int NV = GR / RPV;
-  const uint8_t* pb = a.psi + (size_t)b * T * NP;
   const int nitems = w < nc ? 2 * ((nc - w + nw - 1) / nw) : 0;
   auto group = [&](int i, int& c, int& ghi, int& glo) {
     c = w + nw * (i >> 1);
@@ -240,53 +239,52 @@ __device__ __forceinline__ void vit_decode_follow(const RecArgs& a, int b, float
     ghi = t_hi - GR * (i & 1);
     glo = ghi - GR + 1 > t_lo ? ghi - GR + 1 : t_lo;
   };
+  // (everything but the lane's column is wave-uniform and kept scalar: a per-lane condition
+  // around a step becomes an exec-mask branch whose join waits for every load in flight)
   auto load = [&](int i, unsigned(&pv)[NV]) {
     int c = 0, ghi = -1, glo = 0;
     if (i < nitems) group(i, c, ghi, glo);
 #pragma unroll
     for (int v = 0; v < NV; ++v) {
       const int t = glo + v * RPV + l / LPR;
-      pv[v] = (i < nitems && t <= ghi)
-                  ? __hip_atomic_load(reinterpret_cast<const unsigned*>(pb + (size_t)t * NP) + (l % LPR),
-                                      __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
-                  : 0u;
+      // rows past the group read as 0: an offset beyond the buffer (no branch)
+      const int off = t <= ghi ? t * NP + 4 * (l % LPR) : 0x7ffffff0;
+      pv[v] = __builtin_amdgcn_raw_buffer_load_b32(psi_rs, off, 0, kAuxSc1);
     }
   };
-  int s = 0;
+  int s = 0;  // (uniform)
   auto walk = [&](int i, const unsigned(&pv)[NV]) {
     if (i >= nitems) return;
     int c, ghi, glo;
     group(i, c, ghi, glo);
-    if ((i & 1) == 0) s = send[c];
-    if (ghi < glo) return;  // (the lower group of a short last chunk)
+    if ((i & 1) == 0) s = __builtin_amdgcn_readfirstlane(send[c]);
+    const int nk = ghi - glo + 1;  // rows of the group (< 1: the lower group of a short last chunk)
     int stv = 0;
+    int su = s;
     static_for<0, GR>([&](auto KK) {
       constexpr int k = GR - 1 - decltype(KK)::value;
-      if (glo + k <= ghi) {
-        const int su = __builtin_amdgcn_readfirstlane(s);  // (uniform: keeps it in an SGPR)
-        asm("v_writelane_b32 %0, %1, %2" : "+v"(stv) : "s"(su), "i"(k));
-        const unsigned word = __builtin_amdgcn_readlane(pv[k / RPV], (k % RPV) * LPR + (su >> 2));
-        s = (int)((word >> ((su & 3) * 8)) & 0xffu);
-      }
+      // branch-free (a branch's join makes the waitcnt pass drain every load in flight): rows
+      // past a short chunk's end keep the state (scalar select) and are not stored
+      asm("v_writelane_b32 %0, %1, %2" : "+v"(stv) : "s"(su), "i"(k));
+      const unsigned word = __builtin_amdgcn_readlane(pv[k / RPV], (k % RPV) * LPR + (su >> 2));
+      const int nxt = (int)((word >> ((su & 3) * 8)) & 0xffu);
+      su = k < nk ? nxt : su;
     });
-    if (l < GR && glo + l <= ghi) sb[glo + l] = stv;
+    s = su;
+    if (l < GR && l < nk) sb[glo + l] = stv;
   };
-  // four groups' loads in flight (a wave's whole share at the north-star T): one exposed round
-  // trip to the write-through rows instead of one per group
+  // four groups' loads at once (a wave's whole share at the north-star T), then their walks:
+  // one exposed round trip to the write-through rows per four groups
   unsigned p0[NV], p1[NV], p2[NV], p3[NV];
-  load(0, p0);
-  load(1, p1);
-  load(2, p2);
-  load(3, p3);
   for (int i = 0; i < nitems; i += 4) {
+    load(i, p0);
+    load(i + 1, p1);
+    load(i + 2, p2);
+    load(i + 3, p3);
     walk(i, p0);
-    load(i + 4, p0);
     walk(i + 1, p1);
-    load(i + 5, p1);
     walk(i + 2, p2);
-    load(i + 6, p2);
     walk(i + 3, p3);
-    load(i + 7, p3);
   }
   if (kStamp) {
     __syncthreads();
