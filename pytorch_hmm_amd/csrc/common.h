@@ -241,6 +241,19 @@ __device__ __forceinline__ void publish_count(int* p, int v) {
   __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+// Zeroes n 4-byte words (the followers' counters) as a kernel node: a hipMemsetAsync captured
+// into a HIP graph was measured not to order against the chain launch that follows it in
+// replay (the followers then saw the previous replay's final counts; tools/diag_graph.py)
+static __global__ void zero_words_kernel(unsigned* p, int n) {
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) p[i] = 0u;
+}
+inline hipError_t zero_words(void* p, size_t bytes, hipStream_t st) {
+  const int n = (int)((bytes + 3) / 4);
+  const int blocks = n < 256 * 64 ? (n + 255) / 256 : 64;
+  hipLaunchKernelGGL(zero_words_kernel, dim3(blocks > 0 ? blocks : 1), dim3(256), 0, st, static_cast<unsigned*>(p), n);
+  return hipGetLastError();
+}
+
 inline int pad_states(int N) { return N <= 64 ? 64 : (N <= 128 ? 128 : 256); }
 
 __host__ __device__ inline size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }

@@ -37,7 +37,7 @@ hipError_t launch_fb(const RecArgs& fa, const RecArgs& fb, const PostArgs& pa, b
   if (fa.pub) {
     // posterior followers beside the banded chains (follow.h): 2B chains + F*B followers (F from
     // the host: fb.hip), no pass after
-    e = hipMemsetAsync(fa.pub, 0, (size_t)2 * fa.B * kPubStride * sizeof(int), st);
+    e = zero_words(fa.pub, (size_t)2 * fa.B * kPubStride * sizeof(int), st);
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(fb_recur_kernel<NP>, dim3((2 + nfollow) * fa.B), dim3(kFbNT<NP>), kExclusiveLds, st, fa, fb,
                        pa.posterior);

@@ -350,8 +350,8 @@ hipError_t launch_vit(const VitArgs& va, bool prep, hipStream_t sm) {
   // psi followers beside a dense chain (NP <= 128: the chain with block-work helpers publishes)
   const int nfollow = (NP <= 128 && va.prog && va.done) ? va.nfollow : 0;
   if (nfollow > 0) {
-    e = hipMemsetAsync(va.prog, 0, (size_t)va.B * kProgSlots * sizeof(int), sm);
-    if (e == hipSuccess) e = hipMemsetAsync(va.done, 0, (size_t)va.B * va.nchunks, sm);
+    e = zero_words(va.prog, (size_t)va.B * kProgSlots * sizeof(int), sm);
+    if (e == hipSuccess) e = zero_words(va.done, (size_t)va.B * va.nchunks, sm);
     if (e != hipSuccess) return e;
     ra.prog = va.prog;
     ra.done = va.done;

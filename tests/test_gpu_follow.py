@@ -206,3 +206,48 @@ def test_wrong_banded_hint_marks_outputs_invalid():
     assert rc == 0
     torch.cuda.synchronize()
     assert bool(torch.isnan(post).all()) and bool(torch.isnan(lr).all())
+
+
+def test_followers_in_graph_replays():
+    """Both ops with their followers captured into two HIP graphs each (own workspaces and
+    outputs) and replayed alternately on changing inputs: every replay resets the counts (a
+    kernel node: a captured hipMemsetAsync did not order against the chain launch in replay and
+    the followers read the previous replay's rows), so each replay's outputs are its own."""
+    o = ops()
+    B, T, N = 8, 600, 128
+    lP, lp0 = O.hmm_params(banded(N))
+    lPd, lp0d = lP.to(DEV), lp0.to(DEV)
+    plan = o.make_plan(lPd)
+    g = torch.Generator(device=DEV).manual_seed(5)
+    base = torch.softmax(torch.randn(B, T, N, device=DEV, generator=g), -1)
+    obs = base.clone()
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        for _ in range(2):
+            o.forward_backward(obs, lPd, lp0d, o.OBS_PROB, 7, plan)
+            o.viterbi(obs, lPd, lp0d, o.OBS_PROB, plan)
+    torch.cuda.synchronize()
+    graphs, outs = [], []
+    for _ in range(2):
+        gr = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(gr, stream=s):
+            f = o.forward_backward(obs, lPd, lp0d, o.OBS_PROB, 7, plan)
+            v = o.viterbi(obs, lPd, lp0d, o.OBS_PROB, plan)
+        graphs.append(gr)
+        outs.append((f, v))
+    torch.cuda.synchronize()
+    for k in range(6):
+        x = base.clone()
+        x[:, :, (7 * k) % N] += 0.5 + 0.1 * k
+        obs.copy_(x)
+        torch.cuda.synchronize()
+        graphs[k % 2].replay()
+        torch.cuda.synchronize()
+        f, v = outs[k % 2]
+        rf = o.forward_backward(obs, lPd, lp0d, o.OBS_PROB, 7, plan, follow=False)
+        rv = o.viterbi(obs, lPd, lp0d, o.OBS_PROB, plan, follow=False)
+        for a, b_ in zip(f, rf):
+            assert torch.equal(a, b_), k
+        for a, b_ in zip(v, rv):
+            assert torch.equal(a, b_), k

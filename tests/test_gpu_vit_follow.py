@@ -123,7 +123,8 @@ def _abi_viterbi(lo_dev, lPd, lp0d, plan, flags, stream=None):
 
 def test_followers_complete_chunks():
     """The followers really do the work: after a dense decode the workspace's done words
-    (viterbi.hip layout: the last B*nchunks bytes, 256-aligned) mark the chunks they finished.
+    (viterbi.hip layout: B*nchunks bytes, 256-aligned, before the banded followers' 2B counts of
+    128 bytes each at the end) mark the chunks they finished.
     With two followers per sequence keeping pace with the chain nearly every chunk is theirs."""
     import pytorch_hmm_amd._native as nat
     from pytorch_hmm_amd import ops
@@ -137,7 +138,8 @@ def test_followers_complete_chunks():
     torch.cuda.synchronize()
     nc = (T + 63) // 64
     span = (B * nc + 255) // 256 * 256
-    done = ws[ws.numel() - span: ws.numel() - span + B * nc].cpu().numpy()
+    end = ws.numel() - 2 * B * 128
+    done = ws[end - span: end - span + B * nc].cpu().numpy()
     frac = float((done == 1).mean())
     print(f"followers finished {int((done == 1).sum())} of {B * nc} chunks")
     assert frac > 0.5, frac
