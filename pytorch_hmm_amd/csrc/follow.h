@@ -184,49 +184,9 @@ __device__ __forceinline__ void vit_decode_follow(const RecArgs& a, int b, float
       __syncthreads();
     }
   };
-  // while the chain runs: every chunk whose four psi blocks are published
-  while (next < nc) {
-    const int need = 4 * (next + 1) < nblocks ? 4 * (next + 1) : nblocks;
-    if (have < need && !wait_for(need)) {
-      invalid();
-      return;
-    }
-    int c_end = have > nblocks ? nc : have / 4;  // chunks with all rows published
-    if (c_end > nc) c_end = nc;
-    if (c_end <= next) c_end = next + 1;  // (the last, short chunk once have == nblocks)
-    compose(c_end);
-  }
-  // the whole trellis and every psi row stored
-  if (have <= nblocks && !wait_for(nblocks + 1)) {
-    invalid();
-    return;
-  }
-  fstamp(1);
-  // s_{T-1} = first argmax of delta_{T-1} (hmm.py:174); the maps from the last chunk down
-  if (w == 0) {
-    const float* dl = a.rows + ((size_t)b * T + T - 1) * a.row_stride;
-    float bv = -INFINITY;
-    int bi = 0x7fffffff;
-#pragma unroll
-    for (int k = 0; k < NP / 64; ++k) {
-      const int j = l + 64 * k;
-      const float v = __hip_atomic_load(dl + (j < N ? j : 0), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      if (j < N) argmax_combine(bv, bi, v, j);
-    }
-    wave_argmax_dpp(bv, bi);
-    if (l == 0 && a.final_score) a.final_score[b] = bv;
-    int s = bi < N ? bi : 0;
-    if (l == 0) send[nc - 1] = s;
-    for (int c = nc - 1; c >= 1; --c) {
-      s = gm[(size_t)c * NP + s];
-      if (l == 0) send[c - 1] = s;
-    }
-  }
-  __syncthreads();
-  fstamp(2);
-  // every chunk's walk: wave w takes chunks w, w + nw, ...; a chunk is two groups of GR = 32
-  // rows walked from the top, the rows held in registers (RPV rows per VGPR) and read by
-  // v_readlane at the current state, the next group's rows loaded while this one is walked
+  // the backtrace's groups (below), defined here: each wave's first chunk (two groups; its psi
+  // rows published long before the end) is loaded while the last chunks are still being waited
+  // for, and walked while the second chunk's loads are in flight
   constexpr int RPV = 256 / NP;  // psi rows per VGPR (a row = NP bytes = NP/4 lanes)
   constexpr int LPR = NP / 4;
   constexpr int GR = 32;
@@ -273,12 +233,69 @@ __device__ __forceinline__ void vit_decode_follow(const RecArgs& a, int b, float
     s = su;
     if (l < GR && l < nk) sb[glo + l] = stv;
   };
-  // four groups' loads at once (a wave's whole share at the north-star T), then their walks:
-  // one exposed round trip to the write-through rows per four groups
   unsigned p0[NV], p1[NV], p2[NV], p3[NV];
+  bool ld0 = false, ld1 = false;  // (uniform)
+  auto preload = [&]() {
+    auto pre = [&](int i, unsigned(&pv)[NV], bool& f) {
+      if (f || i >= nitems) return;
+      int c, ghi, glo;
+      group(i, c, ghi, glo);
+      if (ghi < 16 * have) {
+        load(i, pv);
+        f = true;
+      }
+    };
+    pre(0, p0, ld0);
+    pre(1, p1, ld1);
+  };
+  // while the chain runs: every chunk whose four psi blocks are published
+  while (next < nc) {
+    const int need = 4 * (next + 1) < nblocks ? 4 * (next + 1) : nblocks;
+    if (have < need && !wait_for(need)) {
+      invalid();
+      return;
+    }
+    int c_end = have > nblocks ? nc : have / 4;  // chunks with all rows published
+    if (c_end > nc) c_end = nc;
+    if (c_end <= next) c_end = next + 1;  // (the last, short chunk once have == nblocks)
+    compose(c_end);
+    if (next + 4 >= nc) preload();  // (near the end: most rows are published)
+  }
+  // the whole trellis and every psi row stored
+  if (have <= nblocks && !wait_for(nblocks + 1)) {
+    invalid();
+    return;
+  }
+  fstamp(1);
+  // s_{T-1} = first argmax of delta_{T-1} (hmm.py:174); the maps from the last chunk down
+  if (w == 0) {
+    const float* dl = a.rows + ((size_t)b * T + T - 1) * a.row_stride;
+    float bv = -INFINITY;
+    int bi = 0x7fffffff;
+#pragma unroll
+    for (int k = 0; k < NP / 64; ++k) {
+      const int j = l + 64 * k;
+      const float v = __hip_atomic_load(dl + (j < N ? j : 0), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (j < N) argmax_combine(bv, bi, v, j);
+    }
+    wave_argmax_dpp(bv, bi);
+    if (l == 0 && a.final_score) a.final_score[b] = bv;
+    int s = bi < N ? bi : 0;
+    if (l == 0) send[nc - 1] = s;
+    for (int c = nc - 1; c >= 1; --c) {
+      s = gm[(size_t)c * NP + s];
+      if (l == 0) send[c - 1] = s;
+    }
+  }
+  __syncthreads();
+  fstamp(2);
+  // every chunk's walk: wave w takes chunks w, w + nw, ...; a chunk is two groups of GR = 32
+  // rows walked from the top, the rows held in registers (RPV rows per VGPR) and read by
+  // v_readlane at the current state.  Four groups' loads at once (a wave's whole share at the
+  // north-star T; the first two loaded already by preload), then their walks
   for (int i = 0; i < nitems; i += 4) {
-    load(i, p0);
-    load(i + 1, p1);
+    if (i > 0 || !ld0) load(i, p0);
+    if (i > 0 || !ld1) load(i + 1, p1);
     load(i + 2, p2);
     load(i + 3, p3);
     walk(i, p0);
