@@ -21,6 +21,9 @@
 // Ablation knobs of the work beside the chains (csrc/follow.h), diagnostic builds only: 1 no
 // per-block publishing (completion only), 2 followers return at once (timing only), 4 plain
 // instead of write-through row / psi stores (timing only), 8 no log leaders.
+#ifndef HMM355_FBR
+#define HMM355_FBR 4  // posterior rows per follower wave per pass (follow.h)
+#endif
 #ifndef HMM355_FBF
 #define HMM355_FBF 0  // diagnostic builds: posterior followers per sequence (0: the host's choice)
 #endif

@@ -13,10 +13,11 @@
 //                      block themselves otherwise, so the chain never waits for the leader.
 //   vit_decode_follow  (Viterbi) composes the 64-step chunk maps G_c[j] = state at the chunk's
 //                      first step - 1 given state j at its last (post.h compose_chunk_map's
-//                      map) from the psi rows the chain's helpers publish, then, once the
-//                      chain is complete, the backtrace: the first argmax of the last trellis
-//                      row (hmm.py:174), the walk over the maps, and every chunk's walk over its
-//                      psi rows (hmm.py:177-178), all in this workgroup.
+//                      map) from the psi rows the chain's helpers publish, storing each chunk's
+//                      path for every end state on the way; once the chain is complete, the
+//                      backtrace (hmm.py:174-178) is the first argmax of the last trellis row,
+//                      the walk over the maps, and a gather of every chunk's path at its end
+//                      state, all in this workgroup.
 //   fb_post_follow     (forward-backward) the posterior (hmm.py:119-126) of every row t as soon
 //                      as both chains have published it: rows from the middle outwards, two per
 //                      chain step in the second half.
@@ -147,7 +148,7 @@ __device__ __forceinline__ void vit_decode_follow(const RecArgs& a, int b, float
   const __amdgpu_buffer_rsrc_t psi_rs = make_rsrc(a.psi + (size_t)b * T * NP, (size_t)T * NP);
   constexpr int G = follow_g(NP);
   int have = 0;   // psi blocks published (nblocks + 1: everything)
-  int next = 1;   // the next chunk to compose (chunk 0 needs no map)
+  int next = 0;   // the next chunk to compose (chunk 0 for its paths; its map is unused)
   auto wait_for = [&](int need) -> bool {
     if (tid == 0) follow_poll(pubp, need, ctl);
     __syncthreads();
@@ -157,7 +158,12 @@ __device__ __forceinline__ void vit_decode_follow(const RecArgs& a, int b, float
     have = v;
     return true;
   };
-  // compose chunks [next, c_end) in groups of G: group member g (NP lanes) takes chunk next + g
+  // compose chunks [next, c_end) in groups of G: group member g (NP lanes) takes chunk next + g.
+  // Lane j walks the chunk's psi rows down from state j at its last step: the state it reaches
+  // at each step is byte k of the chunk's path for end state j (the state at t_lo + k), stored
+  // (64 bytes) to the workspace, and the state before the chunk is the map entry G_c[j].  The
+  // backtrace is then one map walk and a gather of each chunk's path at its end state.
+  uint8_t* const pbase = a.path + (size_t)b * nc * NP * kChunk;
   auto compose = [&](int c_end) {
     while (next < c_end) {
       const int cnt = c_end - next < G ? c_end - next : G;
@@ -175,78 +181,30 @@ __device__ __forceinline__ void vit_decode_follow(const RecArgs& a, int b, float
       if (g < cnt) {
         const int c = next + g;
         const int t_lo = c * kChunk, t_hi = (t_lo + kChunk < T ? t_lo + kChunk : T) - 1;
+        const int len = t_hi - t_lo;  // the chunk's last step, relative (< 63: the short last chunk)
         const uint8_t* pr = stg + (size_t)g * kChunk * NP;
-        int s = j < N ? j : 0;
-        for (int t = t_hi; t > t_lo; --t) s = pr[(t - t_lo) * NP + s];
-        gm[(size_t)c * NP + j] = pr[s];
+        int st = j < N ? j : 0;
+        unsigned acc[kChunk / 4];
+        static_for<0, kChunk>([&](auto KK) {
+          constexpr int k = kChunk - 1 - decltype(KK)::value;
+          // st = the state at t_lo + min(k, len); beyond len: the end state (never read)
+          if constexpr ((k & 3) == 3) acc[k >> 2] = (unsigned)st << 24;
+          else acc[k >> 2] |= (unsigned)st << (8 * (k & 3));
+          if constexpr (k >= 1) {
+            const int nx = pr[k * NP + st];  // (unconditional read, inside the staged chunk)
+            st = k <= len ? nx : st;
+          }
+        });
+        gm[(size_t)c * NP + j] = pr[st];
+        uint8_t* dst = pbase + ((size_t)c * NP + j) * kChunk;
+#pragma unroll
+        for (int q = 0; q < kChunk / 16; ++q)
+          *reinterpret_cast<u32x4_t*>(dst + 16 * q) = u32x4_t{acc[4 * q], acc[4 * q + 1], acc[4 * q + 2], acc[4 * q + 3]};
       }
       next += cnt;
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (the paths stored before the barrier)
       __syncthreads();
     }
-  };
-  // the backtrace's groups (below), defined here: each wave's first chunk (two groups; its psi
-  // rows published long before the end) is loaded while the last chunks are still being waited
-  // for, and walked while the second chunk's loads are in flight
-  constexpr int RPV = 256 / NP;  // psi rows per VGPR (a row = NP bytes = NP/4 lanes)
-  constexpr int LPR = NP / 4;
-  constexpr int GR = 32;
-  constexpr int NV = GR / RPV;
-  const int nitems = w < nc ? 2 * ((nc - w + nw - 1) / nw) : 0;
-  auto group = [&](int i, int& c, int& ghi, int& glo) {
-    c = w + nw * (i >> 1);
-    const int t_lo = c * kChunk;
-    const int t_hi = (t_lo + kChunk < T ? t_lo + kChunk : T) - 1;
-    ghi = t_hi - GR * (i & 1);
-    glo = ghi - GR + 1 > t_lo ? ghi - GR + 1 : t_lo;
-  };
-  // (everything but the lane's column is wave-uniform and kept scalar: a per-lane condition
-  // around a step becomes an exec-mask branch whose join waits for every load in flight)
-  auto load = [&](int i, unsigned(&pv)[NV]) {
-    int c = 0, ghi = -1, glo = 0;
-    if (i < nitems) group(i, c, ghi, glo);
-#pragma unroll
-    for (int v = 0; v < NV; ++v) {
-      const int t = glo + v * RPV + l / LPR;
-      // rows past the group read as 0: an offset beyond the buffer (no branch)
-      const int off = t <= ghi ? t * NP + 4 * (l % LPR) : 0x7ffffff0;
-      pv[v] = __builtin_amdgcn_raw_buffer_load_b32(psi_rs, off, 0, kAuxSc1);
-    }
-  };
-  int s = 0;  // (uniform)
-  auto walk = [&](int i, const unsigned(&pv)[NV]) {
-    if (i >= nitems) return;
-    int c, ghi, glo;
-    group(i, c, ghi, glo);
-    if ((i & 1) == 0) s = __builtin_amdgcn_readfirstlane(send[c]);
-    const int nk = ghi - glo + 1;  // rows of the group (< 1: the lower group of a short last chunk)
-    int stv = 0;
-    int su = s;
-    static_for<0, GR>([&](auto KK) {
-      constexpr int k = GR - 1 - decltype(KK)::value;
-      // branch-free (a branch's join makes the waitcnt pass drain every load in flight): rows
-      // past a short chunk's end keep the state (scalar select) and are not stored
-      asm("v_writelane_b32 %0, %1, %2" : "+v"(stv) : "s"(su), "i"(k));
-      const unsigned word = __builtin_amdgcn_readlane(pv[k / RPV], (k % RPV) * LPR + (su >> 2));
-      const int nxt = (int)((word >> ((su & 3) * 8)) & 0xffu);
-      su = k < nk ? nxt : su;
-    });
-    s = su;
-    if (l < GR && l < nk) sb[glo + l] = stv;
-  };
-  unsigned p0[NV], p1[NV], p2[NV], p3[NV];
-  bool ld0 = false, ld1 = false;  // (uniform)
-  auto preload = [&]() {
-    auto pre = [&](int i, unsigned(&pv)[NV], bool& f) {
-      if (f || i >= nitems) return;
-      int c, ghi, glo;
-      group(i, c, ghi, glo);
-      if (ghi < 16 * have) {
-        load(i, pv);
-        f = true;
-      }
-    };
-    pre(0, p0, ld0);
-    pre(1, p1, ld1);
   };
   // while the chain runs: every chunk whose four psi blocks are published
   while (next < nc) {
@@ -259,7 +217,6 @@ __device__ __forceinline__ void vit_decode_follow(const RecArgs& a, int b, float
     if (c_end > nc) c_end = nc;
     if (c_end <= next) c_end = next + 1;  // (the last, short chunk once have == nblocks)
     compose(c_end);
-    if (next + 4 >= nc) preload();  // (near the end: most rows are published)
   }
   // the whole trellis and every psi row stored
   if (have <= nblocks && !wait_for(nblocks + 1)) {
@@ -289,19 +246,17 @@ __device__ __forceinline__ void vit_decode_follow(const RecArgs& a, int b, float
   }
   __syncthreads();
   fstamp(2);
-  // every chunk's walk: wave w takes chunks w, w + nw, ...; a chunk is two groups of GR = 32
-  // rows walked from the top, the rows held in registers (RPV rows per VGPR) and read by
-  // v_readlane at the current state.  Four groups' loads at once (a wave's whole share at the
-  // north-star T; the first two loaded already by preload), then their walks
-  for (int i = 0; i < nitems; i += 4) {
-    if (i > 0 || !ld0) load(i, p0);
-    if (i > 0 || !ld1) load(i + 1, p1);
-    load(i + 2, p2);
-    load(i + 3, p3);
-    walk(i, p0);
-    walk(i + 1, p1);
-    walk(i + 2, p2);
-    walk(i + 3, p3);
+  // every state: chunk c's path at its end state send[c], one dword (4 steps) per thread
+  const __amdgpu_buffer_rsrc_t path_rs = make_rsrc(pbase, (size_t)nc * NP * kChunk);
+  for (int idx = tid; idx < nc * (kChunk / 4); idx += blockDim.x) {
+    const int c = idx / (kChunk / 4), q = idx % (kChunk / 4);
+    const int t0 = c * kChunk + 4 * q;
+    if (t0 < T) {
+      const unsigned word = __builtin_amdgcn_raw_buffer_load_b32(path_rs, (c * NP + send[c]) * kChunk + 4 * q, 0, kAuxSc1);
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+        if (t0 + i < T) sb[t0 + i] = (int64_t)((word >> (8 * i)) & 0xffu);
+    }
   }
   if (kStamp) {
     __syncthreads();
@@ -347,7 +302,7 @@ __device__ __forceinline__ void fb_post_follow(const RecArgs& fa, const RecArgs&
   // second half of the chains hands over two rows per step (a 4-block publish: 128 rows), and
   // a row's write-through source is a far cache's round trip away -- one exposed round trip per
   // pass, not per row
-  constexpr int R = 4;
+  constexpr int R = HMM355_FBR;
   auto rows = [&](const int (&t)[R], int nv) {
     float u[R][K], v[R][K];
 #pragma unroll

@@ -177,6 +177,7 @@ struct VitArgs {
   int* pub;
   const float* lobuf;
   const int* lready;
+  uint8_t* path;  // (B, nchunks, NP, 64) the decode follower's chunk paths (follow.h)
 };
 
 // chunk map: G[j] = state at t_lo - 1 given state j at t_hi (psi rows of the chunk in LDS)

@@ -294,6 +294,7 @@ struct RecArgs {
   const float* lobuf;
   const int* lready;
   float* lik_ref;        // FB alpha with publishing: (B) the reference's compute_likelihood value
+  uint8_t* path;         // Viterbi decode follower: (B, nchunks, NP, 64) chunk paths (follow.h)
 };
 constexpr int kProgSlots = 8;  // >= kRbHelpers<NP>::NH
 

@@ -69,9 +69,11 @@ HMM355_API size_t hmm355_viterbi_workspace_bytes(int B, int T, int N) {
   const size_t NP = pad_states(N);
   const size_t nc = (T + kChunk - 1) / kChunk;
   // psi rows, chunk maps, the plan-less band descriptor, the log-emissions of a dense plan, the
-  // psi followers' progress and done words (last)
+  // decode follower's chunk paths (follow.h), the psi followers' progress and done words, the
+  // banded followers' counts (last)
   return align_up((size_t)B * T * NP, 256) + align_up((size_t)B * nc * NP, 256) + align_up(sizeof(BandDesc), 256) +
-         align_up((size_t)B * T * N * sizeof(float), 256) + align_up((size_t)B * kProgSlots * sizeof(int), 256) +
+         align_up((size_t)B * T * N * sizeof(float), 256) + align_up((size_t)B * nc * kChunk * NP, 256) +
+         align_up((size_t)B * kProgSlots * sizeof(int), 256) +
          align_up((size_t)B * nc, 256) + (size_t)2 * B * kPubStride * sizeof(int);
 }
 
@@ -121,7 +123,8 @@ static int viterbi_run(const float* obs, int obs_mode, const float* log_P, const
   uint8_t* G = psi + align_up((size_t)B * T * NP, 256);
   uint8_t* bandp = G + align_up((size_t)B * nc * NP, 256);
   float* lobuf = reinterpret_cast<float*>(bandp + align_up(sizeof(BandDesc), 256));
-  int* prog = reinterpret_cast<int*>(reinterpret_cast<uint8_t*>(lobuf) + align_up((size_t)B * T * N * sizeof(float), 256));
+  uint8_t* path = reinterpret_cast<uint8_t*>(lobuf) + align_up((size_t)B * T * N * sizeof(float), 256);
+  int* prog = reinterpret_cast<int*>(path + align_up((size_t)B * nc * kChunk * NP, 256));
   uint8_t* done = reinterpret_cast<uint8_t*>(prog) + align_up((size_t)B * kProgSlots * sizeof(int), 256);
   int* counts = reinterpret_cast<int*>(done + align_up((size_t)B * nc, 256));  // (2B x kPubStride) follow.h
   BandDesc* band = plan ? static_cast<BandDesc*>(const_cast<void*>(plan)) : reinterpret_cast<BandDesc*>(bandp);
@@ -135,6 +138,7 @@ static int viterbi_run(const float* obs, int obs_mode, const float* log_P, const
     // published psi blocks, [B, 2B) the leaders' blocks.
     if ((e = zero_words(counts, (size_t)2 * B * kPubStride * sizeof(int), sm)) != hipSuccess) return (int)e;
     va.pub = counts;
+    va.path = path;
     if (obs_mode == HMM355_OBS_PROB) {
       va.lobuf = lobuf;
       va.lready = counts + (size_t)B * kPubStride;

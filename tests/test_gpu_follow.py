@@ -251,3 +251,44 @@ def test_followers_in_graph_replays():
             assert torch.equal(a, b_), k
         for a, b_ in zip(v, rv):
             assert torch.equal(a, b_), k
+
+
+def test_leaders_and_followers_did_the_work():
+    """After a banded call the workspace's published counts (the last 2B x 128 bytes of each
+    workspace) show the hand-offs ran in the launch: every chain published completion
+    (nblocks + 1), and the Viterbi log leaders converted every block they own (count = nblocks)."""
+    from pytorch_hmm_amd import _native as nat
+    o = ops()
+    B, T, N = 4, 2000, 128
+    nblocks = (T + 15) // 16
+    lP, lp0 = O.hmm_params(banded(N))
+    lPd, lp0d = lP.to(DEV), lp0.to(DEV)
+    plan = o.make_plan(lPd)
+    g = torch.Generator(device=DEV).manual_seed(2)
+    x = torch.softmax(torch.randn(B, T, N, device=DEV, generator=g), -1)
+    L, p, st = nat.lib(), nat.ptr, nat.stream_of(torch.device(DEV))
+    states = torch.empty(B, T, dtype=torch.int64, device=DEV)
+    delta = torch.empty(B, T, N, device=DEV)
+    final = torch.empty(B, device=DEV)
+    ws = torch.zeros(L.hmm355_viterbi_workspace_bytes(B, T, N), dtype=torch.uint8, device=DEV)
+    assert L.hmm355_viterbi_plan_ex_f32(p(x), o.OBS_PROB, p(lPd), p(lp0d), p(plan), nat.VIT_PLAN_BANDED, B, T, N,
+                                        p(states), p(delta), p(final), p(ws), ws.numel(), st) == 0
+    torch.cuda.synchronize()
+    cnt = ws[ws.numel() - 2 * B * 128:].view(torch.int32).view(2 * B, 32)[:, 0].cpu().tolist()
+    assert cnt[:B] == [nblocks + 1] * B, cnt     # the chains: psi rows and trellis complete
+    assert cnt[B:] == [nblocks] * B, cnt         # the leaders: every block's log rows
+    cs, _, _ = O.c_viterbi(lo_cr(x.cpu().numpy()), lP.numpy(), lp0.numpy())
+    assert np.array_equal(states.cpu().numpy(), cs)
+    post = torch.empty(B, T, N, device=DEV)
+    ll, lr = torch.empty(B, device=DEV), torch.empty(B, device=DEV)
+    nbytes = L.hmm355_fb_workspace_bytes(B, T, N)
+    wsf = torch.zeros(nbytes, dtype=torch.uint8, device=DEV)
+    assert L.hmm355_forward_backward_plan_f32(p(x), o.OBS_PROB, p(lPd), p(lp0d), p(plan), None, B, T, N,
+                                              o.FB_POSTERIOR | nat.FB_PLAN_BANDED, p(post), None, None, p(ll),
+                                              p(lr), p(wsf), nbytes, st) == 0
+    torch.cuda.synchronize()
+    span = (2 * B * 128 + 255) // 256 * 256
+    cf = wsf[nbytes - span: nbytes - span + 2 * B * 128].view(torch.int32).view(2 * B, 32)[:, 0].cpu().tolist()
+    assert cf == [nblocks + 1] * (2 * B), cf      # both chains of every sequence published completion
+    ref = o.forward_backward(x, lPd, lp0d, o.OBS_PROB, o.FB_POSTERIOR, plan, follow=False)
+    assert torch.equal(post, ref[0])

@@ -8,7 +8,7 @@ import os
 import sys
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB = os.path.join(HERE, "ablate_libs", "libhmm355_stamp.so")
+LIB = os.environ.get("STAMP_LIB", os.path.join(HERE, "ablate_libs", "libhmm355_stamp.so"))
 if sys.argv[1:] == ["build"]:
     sys.path.insert(0, os.path.dirname(HERE))
     from pytorch_hmm_amd import build_native as bn
