@@ -1759,6 +1759,13 @@ __device__ __forceinline__ void rec_band(const RecArgs& a, float* lds, int b, co
       o8[0] = hs_work; o8[1] = hs_wait; o8[4] = (unsigned long long)nblocks;
     }
     lds_barrier();  // the chain's last row and c_{T-1}
+    if (FB && pubon && nblocks > 6) {
+      // the loop's flushes (blocks < nblocks - 2) retired: published now, so the followers form
+      // those rows while the last two blocks are flushed (the final count comes after them)
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();  // (the chain wave has ended: the helpers alone)
+      if (hi == 0 && l == 0) publish_count(pubp, nblocks - 2);
+    }
     const float lsv2 = nblocks >= 2 ? rec_ls_scan<NP, KIND>(a, lds, b, nblocks - 2, base, w == 1) : 0.f;
     const float lsv1 = rec_ls_scan<NP, KIND>(a, lds, b, nblocks - 1, base, w == 1);
 #pragma unroll
