@@ -52,8 +52,10 @@ def parse():
                    help="layer workloads c2/c3/c5: consecutive steps on two alternating streams (step "
                         "k+1's emission beside step k's recursion; two batches in flight)")
     p.add_argument("--cpu-seconds", type=float, default=12.0, help="bounded CPU-baseline budget (0 = skip)")
-    p.add_argument("--no-graph", action="store_true",
-                   help="launch every step eagerly instead of replaying one captured HIP graph")
+    p.add_argument("--graph", action="store_true",
+                   help="ns workload: replay each op from a captured HIP graph instead of launching it "
+                        "eagerly (round 6: each op is one launch, eager is faster -- DESIGN.md §5)")
+    p.add_argument("--no-graph", action="store_true", help=argparse.SUPPRESS)  # (the default since round 6)
     p.add_argument("--transition", default="left_to_right", choices=["left_to_right", "ergodic", "random", "trained"],
                    help="transition matrix of the workload (BASELINE: left_to_right 0.7; SURVEY §8(d) also "
                         "names create_transition_matrix(N,'ergodic'); 'random' = a dense learned-style "
@@ -754,12 +756,14 @@ def main():
 
     # A step is one forward_backward (posterior, forward, backward) and one viterbi_decode of
     # the batch (+ the gather when world > 1).  The two ops are independent, so each runs on
-    # its own stream, replayed from a HIP graph; consecutive steps pipeline across the streams
-    # (no per-step join: a cross-stream join costs two cross-queue signal hops, ~35 us).
+    # its own stream; consecutive steps pipeline across the streams (no per-step join: a
+    # cross-stream join costs two cross-queue signal hops, ~35 us).  Each op is one launch
+    # (the work beside the chains runs inside it), launched eagerly: a HIP graph replay put
+    # ~19 us between consecutive replays on a stream, eager launches ~11 (--graph replays).
     fb_fl, vit_fl = ns_follow(args)
     step = NsStep({"fb": lambda: ops.forward_backward(obs, lP, lp0, ops.OBS_PROB, 7, plan, follow=fb_fl),
                    "vit": lambda: ops.viterbi(obs, lP, lp0, ops.OBS_PROB, plan, follow=vit_fl)},
-                  dev, gatherer, use_graph=not args.no_graph, serial=args.serial)
+                  dev, gatherer, use_graph=args.graph and not args.no_graph, serial=args.serial)
 
     for _ in range(args.warmup):
         step()

@@ -1,5 +1,6 @@
 // hmm355 — shared device helpers for the gfx950 (CDNA4) kernels.
 #pragma once
+#include <atomic>
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -237,16 +238,40 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* p, size_
 // published counts sit one per 128-B line (no two counters share a line: a chain's store and
 // another chain's follower polls never meet on one)
 constexpr int kPubStride = 32;
-__device__ __forceinline__ int poll_count(const int* p) {
-  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+// A count is one 8-byte word {call token, count ^ mix(token)}, stored and polled whole (8-B
+// granules are untorn).  An eager call takes a fresh nonzero token (count_token()), so the
+// words a previous call or any other use of the workspace left behind read as 0 -- no reset
+// launch before the chains; a stale word passes only if its high half equals the token AND its
+// low half decodes to a count <= cap.  Token 0 (calls captured into a HIP graph, whose replays
+// share one token) keeps the reset kernel below before every launch.
+__device__ __host__ __forceinline__ unsigned count_mix(unsigned token) { return token * 2654435761u; }
+__device__ __forceinline__ int poll_count(const int* p, unsigned token, int cap) {
+  const unsigned long long v =
+      __hip_atomic_load(reinterpret_cast<const unsigned long long*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const unsigned c = (unsigned)v ^ count_mix(token);
+  return ((unsigned)(v >> 32) == token && c <= (unsigned)cap) ? (int)c : 0;
 }
-__device__ __forceinline__ void publish_count(int* p, int v) {
-  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+__device__ __forceinline__ void publish_count(int* p, int v, unsigned token) {
+  const unsigned long long w = ((unsigned long long)token << 32) | ((unsigned)v ^ count_mix(token));
+  __hip_atomic_store(reinterpret_cast<unsigned long long*>(p), w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// a fresh nonzero token per eager call (process-wide, wraps past 0)
+inline unsigned next_count_token() {
+  static std::atomic<unsigned> g_token{0x5bd1e995u};
+  unsigned t;
+  do t = g_token.fetch_add(0x9e3779b9u, std::memory_order_relaxed) + 0x9e3779b9u; while (t == 0u);
+  return t;
+}
+// true while `st` is being captured into a graph (its replays would share one token)
+inline bool stream_capturing(hipStream_t st) {
+  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+  return hipStreamIsCapturing(st, &cs) == hipSuccess && cs != hipStreamCaptureStatusNone;
 }
 
-// Zeroes n 4-byte words (the followers' counters) as a kernel node: a hipMemsetAsync captured
-// into a HIP graph was measured not to order against the chain launch that follows it in
-// replay (the followers then saw the previous replay's final counts; tools/diag_graph.py)
+// Zeroes n 4-byte words (the followers' counters under token 0) as a kernel node: a
+// hipMemsetAsync captured into a HIP graph was measured not to order against the chain launch
+// that follows it in replay (the followers then saw the previous replay's final counts;
+// tools/diag_graph.py)
 static __global__ void zero_words_kernel(unsigned* p, int n) {
   for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) p[i] = 0u;
 }
@@ -255,6 +280,16 @@ inline hipError_t zero_words(void* p, size_t bytes, hipStream_t st) {
   const int blocks = n < 256 * 64 ? (n + 255) / 256 : 64;
   hipLaunchKernelGGL(zero_words_kernel, dim3(blocks > 0 ? blocks : 1), dim3(256), 0, st, static_cast<unsigned*>(p), n);
   return hipGetLastError();
+}
+// the counts before a publishing launch: a fresh token for an eager call, else token 0 and
+// the reset kernel
+inline hipError_t prepare_counts(void* p, size_t bytes, hipStream_t st, unsigned* token) {
+  if (!stream_capturing(st)) {
+    *token = next_count_token();
+    return hipSuccess;
+  }
+  *token = 0u;
+  return zero_words(p, bytes, st);
 }
 
 inline int pad_states(int N) { return N <= 64 ? 64 : (N <= 128 ? 128 : 256); }

@@ -37,9 +37,12 @@ hipError_t launch_fb(const RecArgs& fa, const RecArgs& fb, const PostArgs& pa, b
   if (fa.pub) {
     // posterior followers beside the banded chains (follow.h): 2B chains + F*B followers (F from
     // the host: fb.hip), no pass after
-    e = zero_words(fa.pub, (size_t)2 * fa.B * kPubStride * sizeof(int), st);
+    unsigned token = 0;
+    e = prepare_counts(fa.pub, (size_t)2 * fa.B * kPubStride * sizeof(int), st, &token);
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(fb_recur_kernel<NP>, dim3((2 + nfollow) * fa.B), dim3(kFbNT<NP>), kExclusiveLds, st, fa, fb,
+    RecArgs ta = fa, tb = fb;
+    ta.token = tb.token = token;
+    hipLaunchKernelGGL(fb_recur_kernel<NP>, dim3((2 + nfollow) * fa.B), dim3(kFbNT<NP>), kExclusiveLds, st, ta, tb,
                        pa.posterior);
     return hipGetLastError();
   }

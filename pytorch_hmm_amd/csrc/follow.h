@@ -48,12 +48,12 @@ __device__ __forceinline__ void fstamp(int k) {
 
 // One lane polls *p until it reaches `need` or the count stops moving for kFollowGiveUp;
 // the value seen goes to *slot (LDS), -1 on give-up.  The caller's workgroup barrier follows.
-__device__ __forceinline__ void follow_poll(const int* p, int need, int* slot) {
-  int have = poll_count(p), last = have;
+__device__ __forceinline__ void follow_poll(const int* p, int need, int* slot, unsigned token, int cap) {
+  int have = poll_count(p, token, cap), last = have;
   long long t0 = __builtin_amdgcn_s_memrealtime();
   while (have < need) {
     __builtin_amdgcn_s_sleep(20);
-    have = poll_count(p);
+    have = poll_count(p, token, cap);
     const long long now = __builtin_amdgcn_s_memrealtime();
     if (have != last) {
       last = have;
@@ -109,7 +109,7 @@ __device__ __forceinline__ void vit_lead(const RecArgs& a, int b) {
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-    if (tid == 0) publish_count(cnt, k1);
+    if (tid == 0) publish_count(cnt, k1, a.token);
   }
 }
 
@@ -150,7 +150,7 @@ __device__ __forceinline__ void vit_decode_follow(const RecArgs& a, int b, float
   int have = 0;   // psi blocks published (nblocks + 1: everything)
   int next = 0;   // the next chunk to compose (chunk 0 for its paths; its map is unused)
   auto wait_for = [&](int need) -> bool {
-    if (tid == 0) follow_poll(pubp, need, ctl);
+    if (tid == 0) follow_poll(pubp, need, ctl, a.token, nblocks + 1);
     __syncthreads();
     const int v = ctl[0];
     __syncthreads();
@@ -361,7 +361,7 @@ __device__ __forceinline__ void fb_post_follow(const RecArgs& fa, const RecArgs&
       int ok = 1;
       long long t0 = __builtin_amdgcn_s_memrealtime();
       for (;;) {
-        const int na = poll_count(pa), nb = poll_count(pb_);
+        const int na = poll_count(pa, fa.token, nblocks + 1), nb = poll_count(pb_, fa.token, nblocks + 1);
         const int lo = T - rows_of(nb), hi = rows_of(na);
         const bool more = lo < hi && (plo < 0 || lo < plo || hi > phi);
         if (more) { ca = na; cb = nb; break; }

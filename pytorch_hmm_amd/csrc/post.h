@@ -178,6 +178,7 @@ struct VitArgs {
   const float* lobuf;
   const int* lready;
   uint8_t* path;  // (B, nchunks, NP, 64) the decode follower's chunk paths (follow.h)
+  unsigned token;  // the counts' call token (common.h)
 };
 
 // chunk map: G[j] = state at t_lo - 1 given state j at t_hi (psi rows of the chunk in LDS)

@@ -295,6 +295,7 @@ struct RecArgs {
   const int* lready;
   float* lik_ref;        // FB alpha with publishing: (B) the reference's compute_likelihood value
   uint8_t* path;         // Viterbi decode follower: (B, nchunks, NP, 64) chunk paths (follow.h)
+  unsigned token;        // the published counts' call token (common.h poll_count / publish_count)
 };
 constexpr int kProgSlots = 8;  // >= kRbHelpers<NP>::NH
 
@@ -1716,12 +1717,12 @@ __device__ __forceinline__ void rec_band(const RecArgs& a, float* lds, int b, co
         }
       }
       psi_copy(kb - 3);
-      if (KIND == kVit && a.lready) lp = poll_count(a.lready + b * kPubStride);
+      if (KIND == kVit && a.lready) lp = poll_count(a.lready + b * kPubStride, a.token, nblocks);
       // every fourth block (Viterbi: whole 64-step chunks of psi rows), after this block's loads
       // (so the stores it signals are never waited for sooner than three blocks on)
       if (pubon && !(kFAbl & 1) && hi == 0 && l == 0) {
         const int cnt = FB ? kb - 5 : kb - 6;
-        if (cnt > 0 && (cnt & 3) == 0) publish_count(pubp, cnt);
+        if (cnt > 0 && (cnt & 3) == 0) publish_count(pubp, cnt, a.token);
       }
       unsigned long long hs1 = 0;
       if (kStamp) { hs1 = stamp(); hs_work += hs1 - hs0; }
@@ -1764,7 +1765,7 @@ __device__ __forceinline__ void rec_band(const RecArgs& a, float* lds, int b, co
       // those rows while the last two blocks are flushed (the final count comes after them)
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();  // (the chain wave has ended: the helpers alone)
-      if (hi == 0 && l == 0) publish_count(pubp, nblocks - 2);
+      if (hi == 0 && l == 0) publish_count(pubp, nblocks - 2, a.token);
     }
     const float lsv2 = nblocks >= 2 ? rec_ls_scan<NP, KIND>(a, lds, b, nblocks - 2, base, w == 1) : 0.f;
     const float lsv1 = rec_ls_scan<NP, KIND>(a, lds, b, nblocks - 1, base, w == 1);
@@ -1810,7 +1811,7 @@ __device__ __forceinline__ void rec_band(const RecArgs& a, float* lds, int b, co
       // everything stored: every helper's stores retired, then one lane publishes completion
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();  // (the chain and psi waves have ended: the helpers alone)
-      if (hi == 0 && l == 0) publish_count(pubp, nblocks + 1);
+      if (hi == 0 && l == 0) publish_count(pubp, nblocks + 1, a.token);
       if (kStamp && hi == 0 && l == 0) g_rec_stamps[((size_t)blockIdx.x * 16 % kStampWaves) * 8 + 2] = __builtin_amdgcn_s_memrealtime();
     }
 }

@@ -345,6 +345,7 @@ hipError_t launch_vit(const VitArgs& va, bool prep, hipStream_t sm) {
     ra.lobuf = va.lobuf;
     ra.lready = va.lready;
     ra.path = va.path;
+    ra.token = va.token;
     hipLaunchKernelGGL(vit_fwd_kernel<NP>, dim3(2 * va.B), dim3(kVitNT<NP>), kExclusiveLds, sm, ra);
     return hipGetLastError();
   }

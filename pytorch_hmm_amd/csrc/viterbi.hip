@@ -136,7 +136,7 @@ static int viterbi_run(const float* obs, int obs_mode, const float* log_P, const
     // the sequence's emissions ahead of its chain (OBS_PROB) and then composes the chunk maps and
     // backtraces the path (follow.h).  The counts, one per 128-B line, zeroed first: [0, B) the
     // published psi blocks, [B, 2B) the leaders' blocks.
-    if ((e = zero_words(counts, (size_t)2 * B * kPubStride * sizeof(int), sm)) != hipSuccess) return (int)e;
+    if ((e = prepare_counts(counts, (size_t)2 * B * kPubStride * sizeof(int), sm, &va.token)) != hipSuccess) return (int)e;
     va.pub = counts;
     va.path = path;
     if (obs_mode == HMM355_OBS_PROB) {

@@ -253,9 +253,20 @@ def test_followers_in_graph_replays():
             assert torch.equal(a, b_), k
 
 
+def _counts(region, n):
+    """the published counts of a workspace's count region (common.h: one 8-byte word per 128-B
+    line, {call token, count ^ (token * 2654435761)})"""
+    out = []
+    for v in region.view(torch.int64).view(n, 16)[:, 0].cpu().tolist():
+        v &= (1 << 64) - 1
+        hi, lo = v >> 32, v & 0xffffffff
+        out.append(lo ^ ((hi * 2654435761) & 0xffffffff))
+    return out
+
+
 def test_leaders_and_followers_did_the_work():
     """After a banded call the workspace's published counts (the last 2B x 128 bytes of each
-    workspace) show the hand-offs ran in the launch: every chain published completion
+    workspace, tokened words) show the hand-offs ran in the launch: every chain published completion
     (nblocks + 1), and the Viterbi log leaders converted every block they own (count = nblocks)."""
     from pytorch_hmm_amd import _native as nat
     o = ops()
@@ -274,7 +285,7 @@ def test_leaders_and_followers_did_the_work():
     assert L.hmm355_viterbi_plan_ex_f32(p(x), o.OBS_PROB, p(lPd), p(lp0d), p(plan), nat.VIT_PLAN_BANDED, B, T, N,
                                         p(states), p(delta), p(final), p(ws), ws.numel(), st) == 0
     torch.cuda.synchronize()
-    cnt = ws[ws.numel() - 2 * B * 128:].view(torch.int32).view(2 * B, 32)[:, 0].cpu().tolist()
+    cnt = _counts(ws[ws.numel() - 2 * B * 128:], 2 * B)
     assert cnt[:B] == [nblocks + 1] * B, cnt     # the chains: psi rows and trellis complete
     assert cnt[B:] == [nblocks] * B, cnt         # the leaders: every block's log rows
     cs, _, _ = O.c_viterbi(lo_cr(x.cpu().numpy()), lP.numpy(), lp0.numpy())
@@ -288,7 +299,54 @@ def test_leaders_and_followers_did_the_work():
                                               p(lr), p(wsf), nbytes, st) == 0
     torch.cuda.synchronize()
     span = (2 * B * 128 + 255) // 256 * 256
-    cf = wsf[nbytes - span: nbytes - span + 2 * B * 128].view(torch.int32).view(2 * B, 32)[:, 0].cpu().tolist()
+    cf = _counts(wsf[nbytes - span: nbytes - span + 2 * B * 128], 2 * B)
     assert cf == [nblocks + 1] * (2 * B), cf      # both chains of every sequence published completion
     ref = o.forward_backward(x, lPd, lp0d, o.OBS_PROB, o.FB_POSTERIOR, plan, follow=False)
     assert torch.equal(post, ref[0])
+
+
+@pytest.mark.parametrize("fill", ["ones_f32", "ff", "random", "stale_final"])
+def test_counts_ignore_workspace_garbage(fill):
+    """Eager calls reset no counts: each takes a fresh call token, so whatever the workspace
+    holds (float ones, 0xff bytes, random bytes, the final counts of an earlier call) reads as
+    no progress and the outputs are this call's own."""
+    from pytorch_hmm_amd import _native as nat
+    o = ops()
+    B, T, N = 3, 700, 128
+    lP, lp0 = O.hmm_params(banded(N))
+    lPd, lp0d = lP.to(DEV), lp0.to(DEV)
+    plan = o.make_plan(lPd)
+    g = torch.Generator(device=DEV).manual_seed(8)
+    x = torch.softmax(torch.randn(B, T, N, device=DEV, generator=g), -1)
+    L, p, st = nat.lib(), nat.ptr, nat.stream_of(torch.device(DEV))
+
+    def filled(nbytes):
+        if fill == "ones_f32":
+            return torch.ones((nbytes + 3) // 4, device=DEV).view(torch.uint8)[:nbytes]
+        if fill == "ff":
+            return torch.full((nbytes,), 255, dtype=torch.uint8, device=DEV)
+        if fill == "random":
+            return torch.randint(0, 256, (nbytes,), dtype=torch.uint8, device=DEV, generator=g)
+        return torch.zeros(nbytes, dtype=torch.uint8, device=DEV)
+
+    nv = L.hmm355_viterbi_workspace_bytes(B, T, N)
+    ws = filled(nv)
+    states = torch.empty(B, T, dtype=torch.int64, device=DEV)
+    delta = torch.empty(B, T, N, device=DEV)
+    final = torch.empty(B, device=DEV)
+    x_other = torch.softmax(torch.randn(B, T, N, device=DEV, generator=g), -1)
+    for inp in ([x_other, x] if fill == "stale_final" else [x]):
+        assert L.hmm355_viterbi_plan_ex_f32(p(inp), o.OBS_PROB, p(lPd), p(lp0d), p(plan), nat.VIT_PLAN_BANDED, B, T,
+                                            N, p(states), p(delta), p(final), p(ws), nv, st) == 0
+    ref = o.viterbi(x, lPd, lp0d, o.OBS_PROB, plan, follow=False)
+    assert torch.equal(states, ref[0]) and torch.equal(delta, ref[1])
+    nf = L.hmm355_fb_workspace_bytes(B, T, N)
+    wsf = filled(nf)
+    post = torch.empty(B, T, N, device=DEV)
+    ll, lr = torch.empty(B, device=DEV), torch.empty(B, device=DEV)
+    for inp in ([x_other, x] if fill == "stale_final" else [x]):
+        assert L.hmm355_forward_backward_plan_f32(p(inp), o.OBS_PROB, p(lPd), p(lp0d), p(plan), None, B, T, N,
+                                                  o.FB_POSTERIOR | nat.FB_PLAN_BANDED, p(post), None, None, p(ll),
+                                                  p(lr), p(wsf), nf, st) == 0
+    reff = o.forward_backward(x, lPd, lp0d, o.OBS_PROB, o.FB_POSTERIOR, plan, follow=False)
+    assert torch.equal(post, reff[0]) and torch.equal(lr, reff[4])
