@@ -42,6 +42,7 @@ EXPORTS = (
     "hmm355_plan_bytes", "hmm355_plan_f32", "hmm355_plan_ex_f32", "hmm355_plan_banded",
     "hmm355_forward_backward_plan_f32", "hmm355_viterbi_plan_f32", "hmm355_viterbi_plan_ex_f32",
     "hmm355_fb_adjoint_f32", "hmm355_tv_fb_adjoint_f32",
+    "hmm355_viterbi_ready_f32", "hmm355_count_token", "hmm355_count_publish", "hmm355_gmm_diag_logprob_ready_f32",
 )
 
 _lib = None
@@ -122,6 +123,12 @@ def lib():
     LL = ctypes.c_longlong
     L.hmm355_tv_fb_adjoint_f32.argtypes = [P, P, LL, LL, P, P, P, P, I, I, I, P, P, P]
     L.hmm355_tv_fb_adjoint_f32.restype = I
+    L.hmm355_viterbi_ready_f32.argtypes = [P, P, P, P, U, I, I, I, P, P, P, P, S, P, U, P]
+    L.hmm355_viterbi_ready_f32.restype = I
+    L.hmm355_count_token.argtypes, L.hmm355_count_token.restype = [], U
+    L.hmm355_count_publish.argtypes, L.hmm355_count_publish.restype = [P, I, U, P], I
+    L.hmm355_gmm_diag_logprob_ready_f32.argtypes = [P, P, P, P, I, I, I, I, I, I, P, P, S, I, I, P, U, P]
+    L.hmm355_gmm_diag_logprob_ready_f32.restype = I
     _lib = L
     return L
 

@@ -107,7 +107,8 @@ static bool vit_follow_ok(unsigned flags, const void* plan, int B, int T, int N)
 
 static int viterbi_run(const float* obs, int obs_mode, const float* log_P, const float* init, const void* plan,
                        unsigned flags, int B, int T, int N, int64_t* states, float* log_delta, float* final_score,
-                       void* workspace, size_t workspace_bytes, void* stream) {
+                       void* workspace, size_t workspace_bytes, void* stream, const int* ready = nullptr,
+                       unsigned ready_token = 0u) {
   if (B < 0 || N < 0) return HMM355_E_ARG;
   if (N < 1 || N > 256) return HMM355_E_STATES;
   if (T < 1) return HMM355_E_SHAPE;
@@ -116,6 +117,8 @@ static int viterbi_run(const float* obs, int obs_mode, const float* log_P, const
   if (!obs || !log_P || !init || !states || !log_delta || !workspace) return HMM355_E_ARG;
   if (obs_mode != HMM355_OBS_PROB && obs_mode != HMM355_OBS_LOG) return HMM355_E_ARG;
   if ((size_t)B * T > (size_t)1 << 40 || B > 65535) return HMM355_E_SHAPE;
+  if ((size_t)T * N * sizeof(float) >= ((size_t)1 << 31)) return HMM355_E_SHAPE;  // (per-sequence buffer loads)
+  if (ready && obs_mode != HMM355_OBS_LOG) return HMM355_E_ARG;
   if (workspace_bytes < hmm355_viterbi_workspace_bytes(B, T, N)) return HMM355_E_WORKSPACE;
   const int NP = pad_states(N);
   const int nc = (T + kChunk - 1) / kChunk;
@@ -129,6 +132,8 @@ static int viterbi_run(const float* obs, int obs_mode, const float* log_P, const
   int* counts = reinterpret_cast<int*>(done + align_up((size_t)B * nc, 256));  // (2B x kPubStride) follow.h
   BandDesc* band = plan ? static_cast<BandDesc*>(const_cast<void*>(plan)) : reinterpret_cast<BandDesc*>(bandp);
   VitArgs va{obs, log_P, init, log_delta, final_score, states, psi, G, B, T, N, obs_mode, nc, band};
+  va.ready = ready;
+  va.ready_token = ready_token;
   hipStream_t sm = static_cast<hipStream_t>(stream);
   hipError_t e;
   if (vit_follow_ok(flags, plan, B, T, N)) {
@@ -189,6 +194,24 @@ HMM355_API int hmm355_viterbi_plan_ex_f32(const float* obs, int obs_mode, const 
                                           size_t workspace_bytes, void* stream) {
   return viterbi_run(obs, obs_mode, log_P, init, plan, flags, B, T, N, states, log_delta, final_score, workspace,
                      workspace_bytes, stream);
+}
+
+HMM355_API int hmm355_viterbi_ready_f32(const float* obs, const float* log_P, const float* init, const void* plan,
+                                        unsigned flags, int B, int T, int N, int64_t* states, float* log_delta,
+                                        float* final_score, void* workspace, size_t workspace_bytes,
+                                        const int* ready, unsigned ready_token, void* stream) {
+  if (!ready) return HMM355_E_ARG;
+  return viterbi_run(obs, HMM355_OBS_LOG, log_P, init, plan, flags, B, T, N, states, log_delta, final_score, workspace,
+                     workspace_bytes, stream, ready, ready_token);
+}
+
+HMM355_API unsigned hmm355_count_token(void) { return next_count_token(); }
+
+HMM355_API int hmm355_count_publish(int* counter, int value, unsigned token, void* stream) {
+  if (!counter || value < 0) return HMM355_E_ARG;
+  hipLaunchKernelGGL(count_publish_kernel, dim3(1), dim3(64), 0, static_cast<hipStream_t>(stream), counter, value, token);
+  const hipError_t e = hipGetLastError();
+  return e == hipSuccess ? HMM355_OK : (int)e;
 }
 
 HMM355_API int hmm355_viterbi_plan_f32(const float* obs, int obs_mode, const float* log_P, const float* init,
