@@ -176,23 +176,6 @@ int hmm355_viterbi_plan_ex_f32(const float* obs, int obs_mode, const float* log_
                                const void* plan, unsigned flags, int B, int T, int N, int64_t* states,
                                float* log_delta, float* final_score, void* workspace,
                                size_t workspace_bytes, void* stream);
-/* Viterbi over log-emissions that another stream is still producing (round 6): as
- * hmm355_viterbi_plan_ex_f32 with HMM355_OBS_LOG, but the chains load 16-step block k of
- * `obs` only once *ready (a count of blocks written for every sequence, published under
- * `ready_token` by hmm355_count_publish or hmm355_gmm_diag_logprob_ready_f32) exceeds k.
- * The producer must publish every block (the chains give up after 0.2 s without progress and
- * read whatever is there: a caller error).  Launch this first, then the producer on another
- * stream (MixtureGaussianHMMLayer's inference: pytorch_hmm_amd.ops.gmm_viterbi).
- * Replaces mixture_gaussian.py:290-338 fed by :157-214. */
-int hmm355_viterbi_ready_f32(const float* obs, const float* log_P, const float* init, const void* plan,
-                             unsigned flags, int B, int T, int N, int64_t* states, float* log_delta,
-                             float* final_score, void* workspace, size_t workspace_bytes,
-                             const int* ready, unsigned ready_token, void* stream);
-/* A fresh nonzero token for one producer / consumer pair of counts (process-wide sequence). */
-unsigned hmm355_count_token(void);
-/* Stores `value` into the count word *counter (128 bytes, 8-aligned) under `token`, stream-
- * ordered after the stream's previous work (whose stores are then visible device-wide). */
-int hmm355_count_publish(int* counter, int value, unsigned token, void* stream);
 
 /* ---------------------------------------------------------------------------------
  * Viterbi.  Replaces HMMPyTorch.viterbi_decode (hmm.py:132-184) and
@@ -207,6 +190,9 @@ int hmm355_count_publish(int* counter, int value, unsigned token, void* stream);
  * reference's (every delta is one fp32 add of an exact max).
  * ------------------------------------------------------------------------------ */
 size_t hmm355_viterbi_workspace_bytes(int B, int T, int N);
+/* The size for one emission encoding: HMM355_OBS_LOG decodes need no log-emission buffer
+ * (B*T*N*4 bytes less); hmm355_viterbi_workspace_bytes is the HMM355_OBS_PROB (larger) size. */
+size_t hmm355_viterbi_workspace_bytes_ex(int B, int T, int N, int obs_mode);
 int hmm355_viterbi_f32(const float* obs, int obs_mode, const float* log_P, const float* init,
                        int B, int T, int N, int64_t* states, float* log_delta,
                        float* final_score, void* workspace, size_t workspace_bytes,
@@ -233,15 +219,6 @@ int hmm355_gmm_diag_logprob_f32(const float* x, const float* means, const float*
                                 const float* log_w, int B, int T, int D, int S, int C,
                                 int mix_lse, float* out, void* workspace,
                                 size_t workspace_bytes, void* stream);
-/* The same scores in time slices (first_frames, then slice_frames frames of every sequence,
- * multiples of 16), each followed by a tokened count of the 16-step blocks written
- * (hmm355_count_publish into *ready): the producer side of hmm355_viterbi_ready_f32.  Scores
- * are bit-identical to hmm355_gmm_diag_logprob_f32's. */
-int hmm355_gmm_diag_logprob_ready_f32(const float* x, const float* means, const float* log_vars,
-                                      const float* log_w, int B, int T, int D, int S, int C, int mix_lse,
-                                      float* out, void* workspace, size_t workspace_bytes,
-                                      int first_frames, int slice_frames, int* ready, unsigned token,
-                                      void* stream);
 /* ---------------------------------------------------------------------------------
  * HSMM segment Viterbi.  Replaces HSMMLayer.viterbi_decode_hsmm / _viterbi_decode_single
  * (hsmm.py:208-354), reproducing its candidate order (s' outer, d' inner, strict >), its

@@ -29,7 +29,7 @@ EXPORTS = (
     "hmm355_strerror", "hmm355_version",
     "hmm355_fb_workspace_bytes", "hmm355_fb_workspace_layout", "hmm355_forward_backward_f32",
     "hmm355_forward_backward_ex_f32",
-    "hmm355_viterbi_workspace_bytes", "hmm355_viterbi_f32",
+    "hmm355_viterbi_workspace_bytes", "hmm355_viterbi_workspace_bytes_ex", "hmm355_viterbi_f32",
     "hmm355_gmm_workspace_bytes", "hmm355_gmm_diag_logprob_f32",
     "hmm355_hsmm_workspace_bytes", "hmm355_hsmm_viterbi_f32", "hmm355_hsmm_workspace_bytes_ex",
     "hmm355_hsmm_viterbi_ex_f32",
@@ -42,7 +42,6 @@ EXPORTS = (
     "hmm355_plan_bytes", "hmm355_plan_f32", "hmm355_plan_ex_f32", "hmm355_plan_banded",
     "hmm355_forward_backward_plan_f32", "hmm355_viterbi_plan_f32", "hmm355_viterbi_plan_ex_f32",
     "hmm355_fb_adjoint_f32", "hmm355_tv_fb_adjoint_f32",
-    "hmm355_viterbi_ready_f32", "hmm355_count_token", "hmm355_count_publish", "hmm355_gmm_diag_logprob_ready_f32",
 )
 
 _lib = None
@@ -72,6 +71,7 @@ def lib():
     L.hmm355_forward_backward_ex_f32.argtypes = [P, I, P, P, P, I, I, I, U, P, P, P, P, P, P, S, P]
     L.hmm355_forward_backward_ex_f32.restype = I
     L.hmm355_viterbi_workspace_bytes.argtypes, L.hmm355_viterbi_workspace_bytes.restype = [I, I, I], S
+    L.hmm355_viterbi_workspace_bytes_ex.argtypes, L.hmm355_viterbi_workspace_bytes_ex.restype = [I, I, I, I], S
     L.hmm355_viterbi_f32.argtypes = [P, I, P, P, I, I, I, P, P, P, P, S, P]
     L.hmm355_viterbi_f32.restype = I
     L.hmm355_gmm_workspace_bytes.argtypes, L.hmm355_gmm_workspace_bytes.restype = [I, I, I, I, I], S
@@ -123,12 +123,6 @@ def lib():
     LL = ctypes.c_longlong
     L.hmm355_tv_fb_adjoint_f32.argtypes = [P, P, LL, LL, P, P, P, P, I, I, I, P, P, P]
     L.hmm355_tv_fb_adjoint_f32.restype = I
-    L.hmm355_viterbi_ready_f32.argtypes = [P, P, P, P, U, I, I, I, P, P, P, P, S, P, U, P]
-    L.hmm355_viterbi_ready_f32.restype = I
-    L.hmm355_count_token.argtypes, L.hmm355_count_token.restype = [], U
-    L.hmm355_count_publish.argtypes, L.hmm355_count_publish.restype = [P, I, U, P], I
-    L.hmm355_gmm_diag_logprob_ready_f32.argtypes = [P, P, P, P, I, I, I, I, I, I, P, P, S, I, I, P, U, P]
-    L.hmm355_gmm_diag_logprob_ready_f32.restype = I
     _lib = L
     return L
 

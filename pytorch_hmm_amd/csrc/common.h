@@ -268,12 +268,6 @@ inline bool stream_capturing(hipStream_t st) {
   return hipStreamIsCapturing(st, &cs) == hipSuccess && cs != hipStreamCaptureStatusNone;
 }
 
-// one tokened count store (hmm355_count_publish: a producer kernel's stores are complete and
-// visible device-wide at its end, so a count stored by the next kernel on its stream covers them)
-static __global__ void count_publish_kernel(int* p, int v, unsigned token) {
-  if (threadIdx.x == 0) publish_count(p, v, token);
-}
-
 // Zeroes n 4-byte words (the followers' counters under token 0) as a kernel node: a
 // hipMemsetAsync captured into a HIP graph was measured not to order against the chain launch
 // that follows it in replay (the followers then saw the previous replay's final counts;

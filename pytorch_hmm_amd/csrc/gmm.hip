@@ -465,7 +465,7 @@ HMM355_API size_t hmm355_gmm_workspace_bytes(int B, int T, int D, int S, int C) 
 
 static int gmm_run(const float* x, const float* means, const float* log_vars, const float* log_w, int B, int T,
                    int D, int S, int C, int mix_lse, int t0, int L, float* out, void* workspace,
-                   size_t workspace_bytes, void* stream, bool prep = true, bool quick = false);
+                   size_t workspace_bytes, void* stream);
 
 HMM355_API int hmm355_gmm_diag_logprob_f32(const float* x, const float* means, const float* log_vars,
                                            const float* log_w, int B, int T, int D, int S, int C, int mix_lse,
@@ -475,7 +475,7 @@ HMM355_API int hmm355_gmm_diag_logprob_f32(const float* x, const float* means, c
 
 static int gmm_run(const float* x, const float* means, const float* log_vars, const float* log_w, int B, int T,
                    int D, int S, int C, int mix_lse, int t0, int L, float* out, void* workspace,
-                   size_t workspace_bytes, void* stream, bool prep, bool quick) {
+                   size_t workspace_bytes, void* stream) {
   if (B < 0 || T < 0 || D < 1 || S < 1 || C < 1) return HMM355_E_ARG;
   if (D > kGmmDMax || C > 256 || (size_t)S * C > 65536) return HMM355_E_SHAPE;
   if ((size_t)B * T == 0) return HMM355_OK;
@@ -491,13 +491,10 @@ static int gmm_run(const float* x, const float* means, const float* log_vars, co
   const int nframes = B * L;  // (the v1 scorer below runs whole tensors only: L == T, t0 == 0)
   const size_t ntiles = ((size_t)nframes + kGmmFrames - 1) / kGmmFrames;
   hipStream_t st = static_cast<hipStream_t>(stream);
-  hipError_t e = hipSuccess;
-  if (prep) {  // (the parameter tables: once per call, before its first slice)
-    hipLaunchKernelGGL(gmm_prep_kernel, dim3(PP), dim3(64), 0, st, means, log_vars, log_w, w.pw, w.pmw, w.cst, P, PP,
-                       D, DP);
-    e = hipGetLastError();
-    if (e != hipSuccess) return (int)e;
-  }
+  hipLaunchKernelGGL(gmm_prep_kernel, dim3(PP), dim3(64), 0, st, means, log_vars, log_w, w.pw, w.pmw, w.cst, P, PP,
+                     D, DP);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return (int)e;
   const int cfg = gmm_cfg();  // diagnostic: 0 = the first scorer, 1.. = v2 shapes
   if (!gmm_use_v1(C)) {
     static_assert(G4<1, 4, 16>::CG == 256 && G4<2, 2, 16>::CG == 128 && G4<4, 2, 16>::CG == 64, "gmm_v2_group");
@@ -508,11 +505,7 @@ static int gmm_run(const float* x, const float* means, const float* log_vars, co
     // below and the default, beat the LDS-DMA staging, config 1, by 4-7 %: 311 / 54 / 31 us per
     // call at configs 3 / 2 / 5; identical bits)
 #define G4R(fg, nw, nf) launch_g4<fg, nw, nf, true>(x, w.pw, w.pmw, w.cst, out, nframes, D, NDC, S, C, P, PP, mix_lse, T, t0, L, st)
-    if (quick) {
-      // time slices feeding a decode (hmm355_gmm_diag_logprob_ready_f32): 4 frames per lane, so
-      // a workgroup ends in ~1/4 of the time and a slice's first rows are published sooner
-      e = CG == 256 ? G4R(1, 4, 4) : CG == 128 ? G4R(2, 2, 4) : G4R(4, 2, 4);
-    } else if (CG == 256) {
+    if (CG == 256) {
       e = cfg == 1 ? G4L(1, 4, 16) : cfg == 2 ? G4L(1, 4, 8) : cfg == 3 ? G4L(1, 2, 16) : cfg == 4 ? G4L(1, 1, 16)
                    : G4R(1, 4, 16);
     } else if (CG == 128) {
@@ -540,47 +533,4 @@ static int gmm_run(const float* x, const float* means, const float* log_vars, co
                      S, C, PP, mix_lse);
   e = hipGetLastError();
   return e == hipSuccess ? HMM355_OK : (int)e;
-}
-
-// The emission in time slices, each followed by a tokened count of the 16-step blocks now
-// written for every sequence (hmm355_count_publish's kernel), so a Viterbi chain launched
-// beside it (hmm355_viterbi_ready_f32, another stream) starts on the first slice instead of
-// after the whole tensor.  Slices: first_frames, doubling up to slice_frames (multiples of
-// 16); the first in the 4-frames-per-lane geometry (a workgroup's latency bounds the slice's,
-// and the decode waits for it), the rest in the default one; the first scorer (C not in
-// {1, 2, 4}) runs whole and publishes once.
-HMM355_API int hmm355_gmm_diag_logprob_ready_f32(const float* x, const float* means, const float* log_vars,
-                                                 const float* log_w, int B, int T, int D, int S, int C, int mix_lse,
-                                                 float* out, void* workspace, size_t workspace_bytes,
-                                                 int first_frames, int slice_frames, int* ready, unsigned token,
-                                                 void* stream) {
-  if (!ready || first_frames < 16 || slice_frames < 16 || (first_frames & 15) || (slice_frames & 15))
-    return HMM355_E_ARG;
-  if (T < 0) return HMM355_E_ARG;
-  hipStream_t st = static_cast<hipStream_t>(stream);
-  const int nblocks = (T + 15) / 16;
-  auto publish = [&](int v) -> int {
-    hipLaunchKernelGGL(count_publish_kernel, dim3(1), dim3(64), 0, st, ready, v, token);
-    const hipError_t e = hipGetLastError();
-    return e == hipSuccess ? HMM355_OK : (int)e;
-  };
-  if (gmm_use_v1(C) || T <= first_frames) {
-    const int rc = gmm_run(x, means, log_vars, log_w, B, T, D, S, C, mix_lse, 0, T, out, workspace, workspace_bytes,
-                           stream);
-    return rc != HMM355_OK ? rc : publish(nblocks);
-  }
-  int t0 = 0, L = first_frames;
-  bool prep = true;
-  while (t0 < T) {
-    if (L > T - t0) L = T - t0;
-    const int rc = gmm_run(x, means, log_vars, log_w, B, T, D, S, C, mix_lse, t0, L, out, workspace,
-                           workspace_bytes, stream, prep, prep);
-    if (rc != HMM355_OK) return rc;
-    t0 += L;
-    const int pr = publish(t0 >= T ? nblocks : t0 / 16);
-    if (pr != HMM355_OK) return pr;
-    L = L * 2 < slice_frames ? L * 2 : slice_frames;  // (doubling up to slice_frames)
-    prep = false;
-  }
-  return HMM355_OK;
 }

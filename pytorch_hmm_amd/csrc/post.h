@@ -179,8 +179,6 @@ struct VitArgs {
   const int* lready;
   uint8_t* path;  // (B, nchunks, NP, 64) the decode follower's chunk paths (follow.h)
   unsigned token;  // the counts' call token (common.h)
-  const int* ready;       // hmm355_viterbi_ready_f32: blocks of `obs` published (RecArgs::ready)
-  unsigned ready_token;
 };
 
 // chunk map: G[j] = state at t_lo - 1 given state j at t_hi (psi rows of the chunk in LDS)

@@ -296,23 +296,7 @@ struct RecArgs {
   float* lik_ref;        // FB alpha with publishing: (B) the reference's compute_likelihood value
   uint8_t* path;         // Viterbi decode follower: (B, nchunks, NP, 64) chunk paths (follow.h)
   unsigned token;        // the published counts' call token (common.h poll_count / publish_count)
-  // Viterbi with emissions produced concurrently (hmm355_viterbi_ready_f32): the count of
-  // 16-step blocks of `obs` written for every sequence, under ready_token; the chains' loads of
-  // a block wait for it and read with sc1 loads.  Null: the emissions are complete.
-  const int* ready;
-  unsigned ready_token;
 };
-
-// (emissions produced concurrently) wait until blocks [0, need) of `obs` are published; gives
-// up after 0.2 s without the count reaching it (a producer that never publishes: caller error)
-__device__ __forceinline__ void rec_wait_ready(const RecArgs& a, int need, int nblocks) {
-  if (!a.ready) return;
-  const long long t0 = __builtin_amdgcn_s_memrealtime();
-  while (poll_count(a.ready, a.ready_token, nblocks) < need) {
-    if (__builtin_amdgcn_s_memrealtime() - t0 > 20000000) break;
-    __builtin_amdgcn_s_sleep(8);
-  }
-}
 constexpr int kProgSlots = 8;  // >= kRbHelpers<NP>::NH
 
 // The banded Viterbi chain computes the argmax pointers psi itself (helper waves on the idle
@@ -391,20 +375,6 @@ __device__ __forceinline__ void rec_load(const RecArgs& a, int b, int blk, int w
   for (int k = 0; k < 4; ++k) {
     const bool ok = qok && col + k < a.N;
     r[k] = src[ok ? col + k : 0];  // no select: the wait lands at the first (masked) use
-  }
-}
-
-// the chains' emission load outside the banded staging loop.  Viterbi: blocks [0, blk] waited
-// for when the emissions are produced concurrently (RecArgs::ready), and always sc1 loads (L1
-// bypassed, L2-served: the emissions are read once, so it costs nothing and leaves no branch
-// around the load); forward-backward: plain
-template <int NP, int KIND>
-__device__ __forceinline__ void rec_load_r(const RecArgs& a, int b, int blk, int w, int l, float (&r)[5]) {
-  if constexpr (KIND == kVit) {
-    rec_wait_ready(a, blk + 1, (a.T + 15) / 16);
-    rec_load<NP, KIND, false, true>(a, b, blk, w, l, r);
-  } else {
-    rec_load<NP, KIND>(a, b, blk, w, l, r);
   }
 }
 
@@ -568,9 +538,9 @@ __device__ __forceinline__ void rec_run(const RecArgs& a, float* lds, int b) {
   const int nblocks = (T + 15) / 16;
   float er0[5], er1[5];
   if (KIND == kVit) rec_logt_fill<NP>(lds, l);
-  rec_load_r<NP, KIND>(a, b, 0, w, l, er0);
+  rec_load<NP, KIND>(a, b, 0, w, l, er0);
   rec_stage<NP, KIND>(a, lds, 0, w, l, er0);
-  if (nblocks > 1) rec_load_r<NP, KIND>(a, b, 1, w, l, er1);
+  if (nblocks > 1) rec_load<NP, KIND>(a, b, 1, w, l, er1);
   lds_barrier();
 
   auto emis = [&](int rho, int idx) { return lds[C::OFF_EMIS + (((rho >> 4) % 3) * 16 + (rho & 15)) * NP + idx]; };
@@ -615,7 +585,7 @@ __device__ __forceinline__ void rec_run(const RecArgs& a, float* lds, int b) {
       // straight-line staging and loads (the tail stages a padding block and re-loads the
       // last one), as in the banded helpers: exact waitcnt counts
       rec_stage<NP, KIND>(a, lds, kb + 1, w, l, ernext);
-      rec_load_r<NP, KIND>(a, b, kb + 2 < nblocks ? kb + 2 : nblocks - 1, w, l, erfree);
+      rec_load<NP, KIND>(a, b, kb + 2 < nblocks ? kb + 2 : nblocks - 1, w, l, erfree);
       if (kb >= 2) rec_flush<NP, KIND>(a, lds, b, kb - 2, tid, rec_ls_scan<NP, KIND>(a, lds, b, kb - 2, base, w == C::NW - 1));
     }
     const int q0 = kb * 16 < 1 ? 1 : kb * 16;
@@ -794,9 +764,9 @@ __device__ __forceinline__ void rec_run_bc(const RecArgs& a, float* lds, int b) 
   const int nblocks = (T + 15) / 16;
   float er0[5], er1[5];
   if (KIND == kVit) rec_logt_fill<NP>(lds, l);
-  rec_load_r<NP, KIND>(a, b, 0, w, l, er0);
+  rec_load<NP, KIND>(a, b, 0, w, l, er0);
   rec_stage<NP, KIND>(a, lds, 0, w, l, er0);
-  if (nblocks > 1) rec_load_r<NP, KIND>(a, b, 1, w, l, er1);
+  if (nblocks > 1) rec_load<NP, KIND>(a, b, 1, w, l, er1);
   lds_barrier();
 
   auto emis = [&](int rho, int idx) { return lds[C::OFF_EMIS + (((rho >> 4) % 3) * 16 + (rho & 15)) * NP + idx]; };
@@ -829,7 +799,7 @@ __device__ __forceinline__ void rec_run_bc(const RecArgs& a, float* lds, int b) 
 
   auto run_block = [&](int kb, float(&ernext)[5], float(&erfree)[5]) {
     rec_stage<NP, KIND>(a, lds, kb + 1, w, l, ernext);
-    rec_load_r<NP, KIND>(a, b, kb + 2 < nblocks ? kb + 2 : nblocks - 1, w, l, erfree);
+    rec_load<NP, KIND>(a, b, kb + 2 < nblocks ? kb + 2 : nblocks - 1, w, l, erfree);
     if (kb >= 2) rec_flush<NP, KIND>(a, lds, b, kb - 2, tid, rec_ls_scan<NP, KIND>(a, lds, b, kb - 2, base, w == C::NW - 1));
     const int q0 = kb * 16 < 1 ? 1 : kb * 16;
     const int q1 = (kb + 1) * 16 < T ? (kb + 1) * 16 : T;
@@ -974,8 +944,8 @@ __device__ __forceinline__ void rec_rb_helper(const RecArgs& a, float* lds, int 
   float er[2][2][5];
   if (KIND == kVit) rec_logt_fill<NP>(lds, l);
   if (nblocks > kb0 + 1) {
-    rec_load_r<NP, KIND>(a, b, kb0 + 1, 2 * h, l, er[1][0]);
-    rec_load_r<NP, KIND>(a, b, kb0 + 1, 2 * h + 1, l, er[1][1]);
+    rec_load<NP, KIND>(a, b, kb0 + 1, 2 * h, l, er[1][0]);
+    rec_load<NP, KIND>(a, b, kb0 + 1, 2 * h + 1, l, er[1][1]);
   }
   lds_barrier();  // (the chain's: block 0 staged)
   lds_barrier();  // (the chain's: row 0 written)
@@ -1008,8 +978,8 @@ __device__ __forceinline__ void rec_rb_helper(const RecArgs& a, float* lds, int 
         if (kb >= kb0 + 3 && ((kb - 2) & 3) == 0) publish(kb - 2);
         break;
       case 1: if (kb + 1 < nblocks) rec_stage<NP, KIND>(a, lds, kb + 1, 2 * h + 1, l, cur[1]); break;
-      case 2: rec_load_r<NP, KIND>(a, b, kb + 2 < nblocks ? kb + 2 : nblocks - 1, 2 * h, l, nxt[0]); break;
-      case 3: rec_load_r<NP, KIND>(a, b, kb + 2 < nblocks ? kb + 2 : nblocks - 1, 2 * h + 1, l, nxt[1]); break;
+      case 2: rec_load<NP, KIND>(a, b, kb + 2 < nblocks ? kb + 2 : nblocks - 1, 2 * h, l, nxt[0]); break;
+      case 3: rec_load<NP, KIND>(a, b, kb + 2 < nblocks ? kb + 2 : nblocks - 1, 2 * h + 1, l, nxt[1]); break;
       case 4: if (kb >= kb0 + 2) lsv = rec_ls_scan<NP, KIND>(a, lds, b, kb - 2, base, h == NH - 1); break;
       case 5: if (kb >= kb0 + 2) rec_flush<NP, KIND>(a, lds, b, kb - 2, th, lsv); break;
       case 6:
@@ -1124,7 +1094,7 @@ __device__ __forceinline__ void rec_run_rb(const RecArgs& a, float* lds, int b) 
   {
     float er0[5];
     if (KIND == kVit) rec_logt_fill<NP>(lds, l);
-    rec_load_r<NP, KIND>(a, b, 0, w, l, er0);
+    rec_load<NP, KIND>(a, b, 0, w, l, er0);
     rec_stage<NP, KIND>(a, lds, 0, w, l, er0);
   }
   lds_barrier();  // (block 1 on: the helpers stage)
@@ -1574,10 +1544,10 @@ __device__ __forceinline__ void rec_band(const RecArgs& a, float* lds, int b, co
       const int vw = vw_of(h);
       if (vw < C::NW) {
         float er[5];
-        rec_load_r<NP, KIND>(a, b, 0, vw, l, er);
+        rec_load<NP, KIND>(a, b, 0, vw, l, er);
         rec_stage<NP, KIND, FUSE>(a, lds, 0, vw, l, er);
-        if (nblocks > 1) rec_load_r<NP, KIND>(a, b, 1, vw, l, er1[h]);
-        if (nblocks > 2) rec_load_r<NP, KIND>(a, b, 2, vw, l, er2[h]);
+        if (nblocks > 1) rec_load<NP, KIND>(a, b, 1, vw, l, er1[h]);
+        if (nblocks > 2) rec_load<NP, KIND>(a, b, 2, vw, l, er2[h]);
       }
     }
   }
@@ -1735,15 +1705,13 @@ __device__ __forceinline__ void rec_band(const RecArgs& a, float* lds, int b, co
       const bool fromlog = KIND == kVit && a.lobuf && kload >= 4 && lp >= kload + 1;
       const float* src = fromlog ? a.lobuf : a.obs;
       const float vmode = (fromlog || a.obs_mode == HMM355_OBS_LOG) ? 1.f : 0.f;
-      // (emissions produced concurrently: block kload published, read with sc1 loads)
-      if (KIND == kVit && a.ready) rec_wait_ready(a, kload + 1, nblocks);
 #pragma unroll
       for (int h = 0; h < HV; ++h) {
         const int vw = vw_of(h);
         if (vw < C::NW && !(kAbl & 32768)) {
           if (!(kAbl & 64)) {
             rec_stage<NP, KIND, FUSE>(a, lds, kb + 1, vw, l, ernext[h]);
-            rec_load<NP, KIND, decltype(FULLC)::value, KIND == kVit>(a, b, kload, vw, l, erfree[h], src, vmode);
+            rec_load<NP, KIND, decltype(FULLC)::value, FUSE>(a, b, kload, vw, l, erfree[h], src, vmode);
           }
           if (!(kAbl & 32) && kb >= 2) rec_flush<NP, KIND>(a, lds, b, kb - 2, l + 64 * vw, lsv);
         }

@@ -339,8 +339,6 @@ hipError_t launch_vit(const VitArgs& va, bool prep, hipStream_t sm) {
   ra.states = va.states;
   ra.final_score = va.final_score;
   ra.nchunks = va.nchunks;
-  ra.ready = va.ready;
-  ra.ready_token = va.ready_token;
   if (va.pub) {
     // the decode beside the banded chain (follow.h): B chains + B decode workgroups, nothing after
     ra.pub = va.pub;

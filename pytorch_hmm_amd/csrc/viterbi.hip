@@ -64,17 +64,28 @@ __global__ void __launch_bounds__(256) vit_log_obs_kernel(const float* __restric
     lo[i] = logcr_fast(x[i] + 1e-8f, g_logcr_tab);
 }
 
-HMM355_API size_t hmm355_viterbi_workspace_bytes(int B, int T, int N) {
+// the log-emission buffer: OBS_PROB decodes only (the log pass / log leaders write it)
+static size_t vit_lobuf_bytes(int B, int T, int N, int obs_mode) {
+  return obs_mode == HMM355_OBS_PROB ? align_up((size_t)B * T * N * sizeof(float), 256) : 0;
+}
+
+HMM355_API size_t hmm355_viterbi_workspace_bytes_ex(int B, int T, int N, int obs_mode) {
   if (B < 0 || T < 1 || N < 1 || N > 256) return 0;
+  if (obs_mode != HMM355_OBS_PROB && obs_mode != HMM355_OBS_LOG) return 0;
   const size_t NP = pad_states(N);
   const size_t nc = (T + kChunk - 1) / kChunk;
-  // psi rows, chunk maps, the plan-less band descriptor, the log-emissions of a dense plan, the
+  // psi rows, chunk maps, the plan-less band descriptor, the log-emissions (OBS_PROB), the
   // decode follower's chunk paths (follow.h), the psi followers' progress and done words, the
   // banded followers' counts (last)
   return align_up((size_t)B * T * NP, 256) + align_up((size_t)B * nc * NP, 256) + align_up(sizeof(BandDesc), 256) +
-         align_up((size_t)B * T * N * sizeof(float), 256) + align_up((size_t)B * nc * kChunk * NP, 256) +
+         vit_lobuf_bytes(B, T, N, obs_mode) + align_up((size_t)B * nc * kChunk * NP, 256) +
          align_up((size_t)B * kProgSlots * sizeof(int), 256) +
          align_up((size_t)B * nc, 256) + (size_t)2 * B * kPubStride * sizeof(int);
+}
+
+// (every encoding: the OBS_PROB size, the larger)
+HMM355_API size_t hmm355_viterbi_workspace_bytes(int B, int T, int N) {
+  return hmm355_viterbi_workspace_bytes_ex(B, T, N, HMM355_OBS_PROB);
 }
 
 // CUs of the current device, queried once per device (a relaxed atomic per slot: concurrent
@@ -107,8 +118,7 @@ static bool vit_follow_ok(unsigned flags, const void* plan, int B, int T, int N)
 
 static int viterbi_run(const float* obs, int obs_mode, const float* log_P, const float* init, const void* plan,
                        unsigned flags, int B, int T, int N, int64_t* states, float* log_delta, float* final_score,
-                       void* workspace, size_t workspace_bytes, void* stream, const int* ready = nullptr,
-                       unsigned ready_token = 0u) {
+                       void* workspace, size_t workspace_bytes, void* stream) {
   if (B < 0 || N < 0) return HMM355_E_ARG;
   if (N < 1 || N > 256) return HMM355_E_STATES;
   if (T < 1) return HMM355_E_SHAPE;
@@ -118,22 +128,19 @@ static int viterbi_run(const float* obs, int obs_mode, const float* log_P, const
   if (obs_mode != HMM355_OBS_PROB && obs_mode != HMM355_OBS_LOG) return HMM355_E_ARG;
   if ((size_t)B * T > (size_t)1 << 40 || B > 65535) return HMM355_E_SHAPE;
   if ((size_t)T * N * sizeof(float) >= ((size_t)1 << 31)) return HMM355_E_SHAPE;  // (per-sequence buffer loads)
-  if (ready && obs_mode != HMM355_OBS_LOG) return HMM355_E_ARG;
-  if (workspace_bytes < hmm355_viterbi_workspace_bytes(B, T, N)) return HMM355_E_WORKSPACE;
+  if (workspace_bytes < hmm355_viterbi_workspace_bytes_ex(B, T, N, obs_mode)) return HMM355_E_WORKSPACE;
   const int NP = pad_states(N);
   const int nc = (T + kChunk - 1) / kChunk;
   uint8_t* psi = static_cast<uint8_t*>(workspace);
   uint8_t* G = psi + align_up((size_t)B * T * NP, 256);
   uint8_t* bandp = G + align_up((size_t)B * nc * NP, 256);
   float* lobuf = reinterpret_cast<float*>(bandp + align_up(sizeof(BandDesc), 256));
-  uint8_t* path = reinterpret_cast<uint8_t*>(lobuf) + align_up((size_t)B * T * N * sizeof(float), 256);
+  uint8_t* path = reinterpret_cast<uint8_t*>(lobuf) + vit_lobuf_bytes(B, T, N, obs_mode);
   int* prog = reinterpret_cast<int*>(path + align_up((size_t)B * nc * kChunk * NP, 256));
   uint8_t* done = reinterpret_cast<uint8_t*>(prog) + align_up((size_t)B * kProgSlots * sizeof(int), 256);
   int* counts = reinterpret_cast<int*>(done + align_up((size_t)B * nc, 256));  // (2B x kPubStride) follow.h
   BandDesc* band = plan ? static_cast<BandDesc*>(const_cast<void*>(plan)) : reinterpret_cast<BandDesc*>(bandp);
   VitArgs va{obs, log_P, init, log_delta, final_score, states, psi, G, B, T, N, obs_mode, nc, band};
-  va.ready = ready;
-  va.ready_token = ready_token;
   hipStream_t sm = static_cast<hipStream_t>(stream);
   hipError_t e;
   if (vit_follow_ok(flags, plan, B, T, N)) {
@@ -194,24 +201,6 @@ HMM355_API int hmm355_viterbi_plan_ex_f32(const float* obs, int obs_mode, const 
                                           size_t workspace_bytes, void* stream) {
   return viterbi_run(obs, obs_mode, log_P, init, plan, flags, B, T, N, states, log_delta, final_score, workspace,
                      workspace_bytes, stream);
-}
-
-HMM355_API int hmm355_viterbi_ready_f32(const float* obs, const float* log_P, const float* init, const void* plan,
-                                        unsigned flags, int B, int T, int N, int64_t* states, float* log_delta,
-                                        float* final_score, void* workspace, size_t workspace_bytes,
-                                        const int* ready, unsigned ready_token, void* stream) {
-  if (!ready) return HMM355_E_ARG;
-  return viterbi_run(obs, HMM355_OBS_LOG, log_P, init, plan, flags, B, T, N, states, log_delta, final_score, workspace,
-                     workspace_bytes, stream, ready, ready_token);
-}
-
-HMM355_API unsigned hmm355_count_token(void) { return next_count_token(); }
-
-HMM355_API int hmm355_count_publish(int* counter, int value, unsigned token, void* stream) {
-  if (!counter || value < 0) return HMM355_E_ARG;
-  hipLaunchKernelGGL(count_publish_kernel, dim3(1), dim3(64), 0, static_cast<hipStream_t>(stream), counter, value, token);
-  const hipError_t e = hipGetLastError();
-  return e == hipSuccess ? HMM355_OK : (int)e;
 }
 
 HMM355_API int hmm355_viterbi_plan_f32(const float* obs, int obs_mode, const float* log_P, const float* init,

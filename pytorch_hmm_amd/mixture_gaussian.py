@@ -229,10 +229,8 @@ class MixtureGaussianHMMLayer(nn.Module):
                               f"{self.max_sequence_length}. Consider chunked processing.")
             with torch.no_grad():
                 log_T, log_w, init, plan = self._inference_tables(observations.device)
-                # (the decode's chains start at once and load each block of scores as the
-                # scorer publishes it: ops.gmm_viterbi; the same bits as the two calls in series)
-                states, _, scores = ops.gmm_viterbi(observations, self.means, self._component_log_vars(), log_w,
-                                                    log_T, init, plan)
+                lp = ops.gmm_diag_logprob(observations, self.means, self._component_log_vars(), log_w, 1)
+                states, _, scores = ops.viterbi(lp, log_T, init, ops.OBS_LOG, plan)
             return (states, scores) if return_log_probs else (states, None)
         log_transitions = self._safe_log(self.get_transition_matrix())
         obs_log_probs = self.get_observation_log_probs(observations)

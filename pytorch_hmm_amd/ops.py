@@ -14,7 +14,6 @@ shape-only fake implementations; their only real implementation is the HIP libra
       -> (posterior, forward, backward, loglik, lik_ref)
   torch.ops.hmm355.tv_viterbi(log_obs, log_A, init) -> (states, log_delta)
 """
-import ctypes
 from typing import Optional, Tuple
 
 import torch
@@ -182,7 +181,7 @@ def viterbi(obs: Tensor, log_P: Tensor, init: Tensor, obs_mode: int,
     final = torch.empty(B, device=dev)
     if B == 0:
         return states, delta, final
-    ws = _workspace(L.hmm355_viterbi_workspace_bytes(B, T, N), dev)
+    ws = _workspace(L.hmm355_viterbi_workspace_bytes_ex(B, T, N, obs_mode), dev)
     flags = 0
     if plan is not None and follow is not False:
         if getattr(plan, "_hmm355_banded", False) is True:
@@ -229,85 +228,6 @@ def gmm_diag_logprob(x: Tensor, means: Tensor, log_vars: Tensor, log_w: Tensor, 
 @gmm_diag_logprob.register_fake
 def _(x, means, log_vars, log_w, mix_lse):
     return x.new_empty((x.shape[0], x.shape[1], means.shape[0]))
-
-
-# ------------------------------------------------------------- GMM emission + Viterbi
-_SIDE_STREAMS = {}
-
-
-def _side_stream(dev) -> "torch.cuda.Stream":
-    """the producer stream paired with the current stream of `dev` (one per pair, reused)"""
-    key = (str(dev), torch.cuda.current_stream(dev).cuda_stream)
-    s = _SIDE_STREAMS.get(key)
-    if s is None:
-        s = _SIDE_STREAMS[key] = torch.cuda.Stream(dev)
-    return s
-
-
-def gmm_viterbi(x: Tensor, means: Tensor, log_vars: Tensor, log_w: Tensor, log_T: Tensor, init: Tensor,
-                plan: Optional[Tensor] = None, mix_lse: int = 1, overlap: Optional[bool] = None,
-                first_frames: int = 256, slice_frames: int = 256) -> Tuple[Tensor, Tensor, Tensor]:
-    """gmm_diag_logprob followed by viterbi(OBS_LOG) -- MixtureGaussianHMMLayer's inference
-    (mixture_gaussian.py:157-214 then :290-338) -- with the decode's chains started at once: the
-    chain launch goes first on the current stream (hmm355_viterbi_ready_f32) and the scorer
-    runs in time slices on a paired side stream, publishing each slice's blocks
-    (hmm355_gmm_diag_logprob_ready_f32); the chains load a block once it is published.  The
-    current stream then waits for the side stream.  Identical bits to the two calls in series,
-    which run instead when overlap is False, while a graph is being captured (tokens would be
-    shared by the replays), or when the chains and their followers leave too few CUs for the
-    scorer (3B + 32 > CUs).  Slices of 256 frames (tools/time_gmm_vit.py at config 3: series
-    0.900 ms, 256/256 0.803, 128/256 0.809, 64/1024 0.960 -- the scorer beside the chain runs
-    slower, so smaller slices keep the chain fed).  Returns (states, log_delta, final_score)."""
-    nat.require_gpu(x, means, log_vars, log_w, log_T, init)
-    x, means, log_vars, log_w = _f32c(x), _f32c(means), _f32c(log_vars), _f32c(log_w)
-    log_T, init = _f32c(log_T), _f32c(init)
-    B, T, D = x.shape
-    S, C, _ = means.shape
-    dev = x.device
-    if overlap is None:
-        overlap = (B * T > 0 and T > first_frames and 3 * B + 32 <= _cus(dev)
-                   and not torch.cuda.is_current_stream_capturing())
-    if not overlap:
-        lp = gmm_diag_logprob(x, means, log_vars, log_w, mix_lse)
-        return viterbi(lp, log_T, init, OBS_LOG, plan)
-    L = nat.lib()
-    lp = torch.empty((B, T, S), device=dev)
-    ready = torch.empty(32, dtype=torch.int32, device=dev)  # one 128-B count word (tokened: no reset)
-    token = L.hmm355_count_token()
-    states = torch.empty((B, T), dtype=torch.int64, device=dev)
-    delta = torch.empty((B, T, S), device=dev)
-    final = torch.empty(B, device=dev)
-    ws = _workspace(L.hmm355_viterbi_workspace_bytes(B, T, S), dev)
-    flags = 0
-    if plan is not None:
-        flags = VIT_PLAN_BANDED if getattr(plan, "_hmm355_banded", False) is True else VIT_PLAN_DENSE
-    main = torch.cuda.current_stream(dev)
-    side = _side_stream(dev)
-    fork = torch.cuda.Event()
-    fork.record(main)
-    with torch.cuda.device(dev):
-        # the consumer first: its chains take their CUs before the scorer's slices fill the chip
-        nat.check(L.hmm355_viterbi_ready_f32(
-            nat.ptr(lp), nat.ptr(log_T), nat.ptr(init), nat.ptr(plan), flags, B, T, S, nat.ptr(states),
-            nat.ptr(delta), nat.ptr(final), nat.ptr(ws), ws.numel(), nat.ptr(ready), token, nat.stream_of(dev)))
-        side.wait_event(fork)
-        with torch.cuda.stream(side):
-            gws = _workspace(L.hmm355_gmm_workspace_bytes(B, T, D, S, C), dev)
-            nat.check(L.hmm355_gmm_diag_logprob_ready_f32(
-                nat.ptr(x), nat.ptr(means), nat.ptr(log_vars), nat.ptr(log_w), B, T, D, S, C, mix_lse,
-                nat.ptr(lp), nat.ptr(gws), gws.numel(), first_frames, slice_frames, nat.ptr(ready), token,
-                ctypes.c_void_p(side.cuda_stream)))
-    for t_ in (lp, ready, x, means, log_vars, log_w):
-        t_.record_stream(side)
-    main.wait_stream(side)
-    return states, delta, final
-
-
-def _cus(dev) -> int:
-    key = str(dev)
-    if key not in _CUS:
-        _CUS[key] = torch.cuda.get_device_properties(dev).multi_processor_count
-    return _CUS[key]
 
 
 # ------------------------------------------------------------------------------- HSMM

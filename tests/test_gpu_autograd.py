@@ -41,7 +41,7 @@ def close(a, b, rel=1e-4):
 
 @pytest.mark.parametrize("kind", ["ref", "exact"])
 @pytest.mark.parametrize("B,T,N,mat", [(2, 12, 5, "l2r"), (3, 30, 16, "rand"), (2, 25, 70, "ergodic"),
-                                       (1, 40, 128, "l2r")])
+                                       (1, 40, 128, "l2r"), (1, 30, 200, "l2r"), (1, 30, 200, "rand")])
 def test_loglik_gradients(kind, B, T, N, mat):
     rng = np.random.default_rng(T * N)
     if mat == "l2r":
@@ -139,7 +139,7 @@ def _matrix(kind, N):
     return torch.softmax(torch.randn(N, N, generator=g), -1)
 
 
-@pytest.mark.parametrize("N", [5, 70, 128])
+@pytest.mark.parametrize("N", [5, 70, 128, 200])   # (200: the NP = 256 chains' CA / CB)
 @pytest.mark.parametrize("kind", ["l2r", "ergodic", "random"])
 @pytest.mark.parametrize("log_mode", [False, True])
 @pytest.mark.parametrize("outs", ["post", "all"])

@@ -175,3 +175,31 @@ def test_hsmm_layer(name, S, D, Dm, seed):
     states, scores = h(x)
     assert np.array_equal(states.cpu().numpy(), g["states"])
     np.testing.assert_allclose(scores.cpu().numpy(), g["scores"], rtol=2e-6)
+
+
+def test_mixture_inference_tables_follow_data_writes():
+    """The no-grad forward caches log T / log w per parameter version: writes through
+    .data are invisible to the version counter, refresh_tables() drops the cache, and a parameter
+    replaced by vector_to_parameters (a new .data pointer) is seen without it.  After each, the
+    decode equals a fresh layer holding the same parameters."""
+    torch.manual_seed(0)
+    S, D, C, B, T = 16, 8, 3, 2, 60
+    m = ph.MixtureGaussianHMMLayer(S, D, num_components=C).to(DEV).eval()
+    x = torch.randn(B, T, D, device=DEV)
+
+    def fresh():
+        f = ph.MixtureGaussianHMMLayer(S, D, num_components=C).to(DEV).eval()
+        f.load_state_dict(m.state_dict())
+        return f(x)[0]
+
+    s0 = m(x)[0]
+    with torch.no_grad():
+        m.transition_logits.data.copy_(torch.randn_like(m.transition_logits) * 4)
+        m.mixture_weights_logits.data -= 3 * torch.randn_like(m.mixture_weights_logits)
+    m.refresh_tables()
+    s1 = m(x)[0]
+    assert torch.equal(s1, fresh())
+    assert not torch.equal(s0, s1)
+    vec = torch.nn.utils.parameters_to_vector(m.parameters())
+    torch.nn.utils.vector_to_parameters(vec + 0.5 * torch.randn_like(vec), m.parameters())
+    assert torch.equal(m(x)[0], fresh())

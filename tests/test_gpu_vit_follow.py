@@ -112,7 +112,8 @@ def _abi_viterbi(lo_dev, lPd, lp0d, plan, flags, stream=None):
     states = torch.zeros(B, T, dtype=torch.int64, device=DEV)
     delta = torch.empty(B, T, N, device=DEV)
     final = torch.zeros(B, device=DEV)
-    ws = torch.empty(L.hmm355_viterbi_workspace_bytes(B, T, N), dtype=torch.uint8, device=DEV)
+    # (the OBS_LOG size: test_followers_complete_chunks reads the done words from the end)
+    ws = torch.empty(L.hmm355_viterbi_workspace_bytes_ex(B, T, N, ops.OBS_LOG), dtype=torch.uint8, device=DEV)
     p = lambda t: ctypes.c_void_p(t.data_ptr())
     st = nat.stream_of(torch.device(DEV, 0)) if stream is None else ctypes.c_void_p(stream.cuda_stream)
     rc = L.hmm355_viterbi_plan_ex_f32(p(lo_dev), ops.OBS_LOG, p(lPd), p(lp0d), p(plan), flags, B, T, N,

@@ -72,6 +72,10 @@ def test_workspace_sizes(L):
     assert fb >= 2 * B * T * 128 * 4 + 2 * B * T * 4  # scaled alpha/beta rows + log-scales
     vit = L.hmm355_viterbi_workspace_bytes(B, T, N)
     assert vit >= B * T * 128                          # uint8 backpointers
+    # OBS_LOG decodes take no log-emission buffer; the default size is OBS_PROB's
+    assert L.hmm355_viterbi_workspace_bytes_ex(B, T, N, 0) == vit
+    assert L.hmm355_viterbi_workspace_bytes_ex(B, T, N, 1) == vit - B * T * N * 4
+    assert L.hmm355_viterbi_workspace_bytes_ex(B, T, N, 2) == 0
     assert L.hmm355_gmm_workspace_bytes(32, 2000, 80, 128, 4) > 0
     assert L.hmm355_hsmm_workspace_bytes(16, 2000, 64, 40) > 0
 
