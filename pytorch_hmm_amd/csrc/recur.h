@@ -458,7 +458,8 @@ __device__ __forceinline__ float rec_ls_scan(const RecArgs& a, const float* lds,
 // lsv: rec_ls_scan's vector (LS of row j in lane j).  A row whose log-scale is below -110 is
 // exactly 0 (x <= N <= 256 < e^6 and e^-104 is below the smallest fp32 denormal), as the
 // reference's exp underflows: no transcendentals for it.
-template <int NP, int KIND>
+// (WHAT: 1 the stored rows, 2 the exp outputs, 3 both)
+template <int NP, int KIND, int WHAT = 3>
 __device__ __forceinline__ void rec_flush(const RecArgs& a, const float* lds, int b, int blk, int tid, float lsv) {
   using C = RC<NP>;
   const int q_base = blk * 16;
@@ -470,7 +471,7 @@ __device__ __forceinline__ void rec_flush(const RecArgs& a, const float* lds, in
     // ends in an s_waitcnt vmcnt(0) join that drains the helper's emission prefetches
     const float4 v = *reinterpret_cast<const float4*>(lds + C::OFF_RING + (q & (C::RING - 1)) * NP + c4);
     const size_t tr = (size_t)b * a.T + rec_tau<KIND>(q, a.T);
-    if (q < a.T) {
+    if ((WHAT & 1) && q < a.T) {
       if (a.pub && !(kFAbl & 4)) {
         // followers read these rows in this launch: write-through (sc1) 16-B stores (follow.h)
         const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
@@ -481,7 +482,7 @@ __device__ __forceinline__ void rec_flush(const RecArgs& a, const float* lds, in
         *reinterpret_cast<float4*>(a.rows + tr * NP + c4) = v;
       }
     }
-    if constexpr (KIND != kVit) {
+    if constexpr (KIND != kVit && (WHAT & 2)) {
       if (a.out_exp) {
         const float ls = __shfl(lsv, row);
         const bool live = ls >= -110.f;
@@ -505,7 +506,7 @@ __device__ __forceinline__ void rec_flush(const RecArgs& a, const float* lds, in
       const int q = q_base + row;
       float* dst = a.rows + ((size_t)b * a.T + rec_tau<KIND>(q, a.T)) * a.row_stride + col;
       const float v = lds[C::OFF_RING + (q & (C::RING - 1)) * NP + col];
-      if (q < a.T) {
+      if ((WHAT & 1) && q < a.T) {
         if (a.pub && !(kFAbl & 4)) __hip_atomic_store(dst, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // (sc1)
         else *dst = v;
       }
@@ -1769,12 +1770,33 @@ __device__ __forceinline__ void rec_band(const RecArgs& a, float* lds, int b, co
     }
     const float lsv2 = nblocks >= 2 ? rec_ls_scan<NP, KIND>(a, lds, b, nblocks - 2, base, w == 1) : 0.f;
     const float lsv1 = rec_ls_scan<NP, KIND>(a, lds, b, nblocks - 1, base, w == 1);
+    if (FB && pubon) {
+      // the last two blocks' rows first, then completion published, then their exp outputs
+      // (the followers read only the rows)
+#pragma unroll
+      for (int h = 0; h < HV; ++h) {
+        const int vw = vw_of(h);
+        if (vw < C::NW) {
+          if (nblocks >= 2) rec_flush<NP, KIND, 1>(a, lds, b, nblocks - 2, l + 64 * vw, lsv2);
+          rec_flush<NP, KIND, 1>(a, lds, b, nblocks - 1, l + 64 * vw, lsv1);
+        }
+      }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();  // (the chain wave has ended: the helpers alone)
+      if (hi == 0 && l == 0) publish_count(pubp, nblocks + 1, a.token);
+      if (kStamp && hi == 0 && l == 0) g_rec_stamps[((size_t)blockIdx.x * 16 % kStampWaves) * 8 + 2] = __builtin_amdgcn_s_memrealtime();
+    }
 #pragma unroll
     for (int h = 0; h < HV; ++h) {
       const int vw = vw_of(h);
       if (vw < C::NW) {
-        if (nblocks >= 2) rec_flush<NP, KIND>(a, lds, b, nblocks - 2, l + 64 * vw, lsv2);
-        rec_flush<NP, KIND>(a, lds, b, nblocks - 1, l + 64 * vw, lsv1);
+        if (FB && pubon) {
+          if (nblocks >= 2) rec_flush<NP, KIND, 2>(a, lds, b, nblocks - 2, l + 64 * vw, lsv2);
+          rec_flush<NP, KIND, 2>(a, lds, b, nblocks - 1, l + 64 * vw, lsv1);
+        } else {
+          if (nblocks >= 2) rec_flush<NP, KIND>(a, lds, b, nblocks - 2, l + 64 * vw, lsv2);
+          rec_flush<NP, KIND>(a, lds, b, nblocks - 1, l + 64 * vw, lsv1);
+        }
         if (KIND == kFbAlpha && a.loglik && vw == C::NW - 1 && l == 0)
           a.loglik[b] = (float)(base + (double)__logf(lds[C::OFF_SC + 64 * ((T - 1) & (C::RING - 1))]));
       }
@@ -1807,7 +1829,7 @@ __device__ __forceinline__ void rec_band(const RecArgs& a, float* lds, int b, co
       psi_copy(nblocks - 2);
       psi_copy(nblocks - 1);
     }
-    if (pubon) {
+    if (!FB && pubon) {
       // everything stored: every helper's stores retired, then one lane publishes completion
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();  // (the chain and psi waves have ended: the helpers alone)
